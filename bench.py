@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""Decode benchmark of the MI355X BitNet b1.58 hot path (BASELINE.json metric: decode tokens/sec +
+GEMV HBM GB/s, bitnet-b1.58-2B-4T).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--ctx C] [--wfmt tq|i2s]
+
+One "step" = one decode token for every sequence of the batch through all 30 layers and the bf16
+LM head (greedy), replayed as one HIP graph; inputs (weights, KV context, token) resident in HBM.
+Default workload = BASELINE configs[1]: batch 1 on one MI355X, synthetic random-init weights of the
+2B-4T architecture (no checkpoint offline), KV context pre-filled to --ctx positions.
+N > 1 (torch.distributed.run, one rank per GPU): independent replicas, no data-path collective
+(SURVEY §8e); value = all ranks' tokens / max-over-ranks time.
+
+Also measured live: per-op kernel durations with HIP events (each launch preceded by an L2/MALL
+flush so weights come from HBM), the dominant kernel's achieved HBM GB/s vs the 8 TB/s peak, and
+the CPU oracle's decode speed on this host's cores (rank 0, N = 1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "wrinklefree-inference-engine_amd" / "python"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--ctx", type=int, default=1024)
+    ap.add_argument("--wfmt", choices=["tq", "i2s"], default="tq")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-op-timing", action="store_true")
+    return ap.parse_args()
+
+
+def op_timing(dec, ctx):
+    """Per-op average kernel duration (HIP events on the launch stream) with a cache flush before
+    every launch, plus algorithmic bytes per launch."""
+    import torch
+    from wfamd import _lib
+    L = dec.cfg.layers
+    flush = torch.empty(384 * 1024 * 1024, dtype=torch.uint8, device="cuda")  # > 256 MiB Infinity Cache
+    ops = [(_lib.WF_OP_QKV, "qkv"), (_lib.WF_OP_ATTN, "attn"), (_lib.WF_OP_O, "o_proj"),
+           (_lib.WF_OP_GATE_UP, "gate_up"), (_lib.WF_OP_DOWN, "down"), (_lib.WF_OP_LM_HEAD, "lm_head")]
+    rec = []
+    st = torch.cuda.current_stream()
+    for rep in range(2):
+        for op, name in ops:
+            layers = [0] if op == _lib.WF_OP_LM_HEAD else range(L)
+            for l in layers:
+                flush.fill_(rep)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                dec.launch_op(l, op)
+                e1.record(st)
+                rec.append((name, op, e0, e1))
+    torch.cuda.synchronize()
+    out = {}
+    for name, op, e0, e1 in rec:
+        out.setdefault(name, {"op": op, "ms": []})["ms"].append(e0.elapsed_time(e1))
+    res = {}
+    for name, v in out.items():
+        us = 1000.0 * sum(v["ms"]) / len(v["ms"])
+        nbytes = dec.op_bytes(v["op"], ctx)
+        per_tok = 1 if v["op"] == _lib.WF_OP_LM_HEAD else L
+        res[name] = {"us": round(us, 3), "bytes": nbytes, "gbs": round(nbytes / us / 1e3, 1),
+                     "launches_per_step": per_tok, "us_per_step": round(us * per_tok, 2)}
+    del flush
+    return res
+
+
+def cpu_baseline(ctx: int, seconds: float):
+    """The C oracle's full decode step (oracle/wf_oracle.c orc_decode_step) of the same 2B model shape
+    on this host's cores; random weights (timing only), bounded sample."""
+    import numpy as np
+    import torch
+    from oracle import oracle as orc
+    from wfamd.model import BITNET_2B as cfg, rope_tables
+    libname = "liborc_native.so"
+    try:
+        orc.build(march="native", name=libname)
+    except Exception:
+        libname = "liborc.so"
+        orc.build()
+    rng = np.random.default_rng(0)
+    H, L, HQ, HKV, D, I, V = cfg.hidden, cfg.layers, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, cfg.inter, cfg.vocab
+    S = ctx + 64
+    lut = np.array([((v // 27) % 3) << 6 | ((v // 9) % 3) << 4 | ((v // 3) % 3) << 2 | (v % 3) for v in range(81)],
+                   dtype=np.uint8)
+
+    def tern(*shape):
+        return lut[rng.integers(0, 81, size=shape, dtype=np.uint8)]
+
+    def bf16_small(*shape):  # random bf16 bit patterns of magnitude ~0.01 (timing only)
+        sign = rng.integers(0, 2, size=shape, dtype=np.uint16) << 15
+        return (0x3C00 + rng.integers(0, 0x100, size=shape, dtype=np.uint16)) | sign
+
+    def bf16_one(*shape):
+        return np.full(shape, 0x3F80, dtype=np.uint16)
+
+    cos, sin = rope_tables(D, S, cfg.rope_theta)
+    a = {
+        "cfg": np.array([H, L, HQ, HKV, D, I, V, S], dtype=np.int64), "eps": np.float32(cfg.eps),
+        "embed": bf16_small(V, H), "final_norm": bf16_one(H),
+        "rope_cos": cos.view(torch.int16).numpy().view(np.uint16),
+        "rope_sin": sin.view(torch.int16).numpy().view(np.uint16),
+        "ln_in": bf16_one(L, H), "ln_post": bf16_one(L, H), "attn_sub": bf16_one(L, H), "ffn_sub": bf16_one(L, I),
+        "wq": tern(L, H, H // 4), "wk": tern(L, HKV * D, H // 4), "wv": tern(L, HKV * D, H // 4),
+        "wo": tern(L, H, H // 4), "wg": tern(L, I, H // 4), "wu": tern(L, I, H // 4), "wd": tern(L, H, I // 4),
+        "wscale": np.full((L, 7), 1.75, dtype=np.float32),
+    }
+    m = orc.DecodeModel(a, libname)
+    m.k_cache[:, :, :ctx] = bf16_small(L, HKV, ctx, D)
+    m.v_cache[:, :, :ctx] = bf16_small(L, HKV, ctx, D)
+    m.step(1, ctx)  # warm (page in weights)
+    n, t0 = 0, time.perf_counter()
+    tok = 1
+    while True:
+        _, tok = m.step(tok, ctx + 1 + n)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 60:
+            break
+    return {"value": round(n / el, 3), "unit": "tokens/s", "cores": orc.num_threads(libname), "kind": "port",
+            "sample": f"oracle/wf_oracle.c orc_decode_step, full 30-layer bitnet-b1.58-2B-4T shape, batch 1, "
+                      f"ctx {ctx}, {n} tokens in {el:.1f}s (random weights)",
+            "ms_per_token": round(1000 * el / n, 2)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from wfamd import WF_FMT_I2S, WF_FMT_TQ, _lib
+    from wfamd.model import BITNET_2B, BitNetDecoder, synthetic_weights
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if not _lib.kernel_available():
+        raise SystemExit("gfx950 HIP kernels unavailable: build with __graft_entry__.build()")
+
+    cfg = BITNET_2B
+    B = args.batch
+    wfmt = WF_FMT_TQ if args.wfmt == "tq" else WF_FMT_I2S
+    total = args.warmup + args.steps
+    ctx = max(1, min(args.ctx, cfg.max_seq - total - 1))
+    w = synthetic_weights(cfg, seed=0, device="cuda")
+    dec = BitNetDecoder(cfg, w, batch=B, wfmt=wfmt)
+    del w
+    torch.cuda.empty_cache()
+    dec.fill_kv_random(ctx, seed=1)
+    dec.set_state([1] * B, [ctx] * B)
+
+    for _ in range(args.warmup):
+        dec.step(graph=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dec.step(graph=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    tok_s = B * args.steps * world / el
+    ms_step = 1000.0 * el / args.steps
+
+    kern = {} if args.no_op_timing else op_timing(dec, ctx + total // 2)
+    roof = None
+    if kern:
+        dom_name = max(kern, key=lambda k: kern[k]["us_per_step"])
+        dom = kern[dom_name]
+        traffic = None
+        pmc = ROOT / "profiles" / "pmc_traffic.json"
+        if pmc.exists():
+            try:
+                traffic = json.loads(pmc.read_text()).get(dom_name, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roof = {"bound": "hbm", "achieved": dom["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom_name,
+                "bytes_per_launch": dom["bytes"], "us_per_launch": dom["us"]}
+    step_bytes = cfg.weight_bytes_per_token(wfmt) + B * cfg.kv_bytes_per_token(ctx + total // 2)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(ctx, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "decode tokens/sec + GEMV HBM GB/s, bitnet-b1.58-2B-4T, batch 1/128",
+            "value": round(tok_s, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int8", "data": "synthetic",
+            "config": {"workload": f"decode batch={B} (BASELINE configs[1])" if B == 1 else f"decode batch={B}",
+                       "model": "bitnet-b1.58-2B-4T (random init)", "global_batch": B * world, "seq_len": ctx,
+                       "parallelism": f"replicas{world}", "weights": "ternary " + ("TQ ~1.6-bit" if wfmt else "I2_S 2-bit"),
+                       "activations": "int8 per-token", "lm_head": "bf16", "kv": "bf16"},
+            "step_hbm_gbs": round(step_bytes / (ms_step / 1000.0) / 1e9, 1),
+            "gemv_hbm_gbs": kern.get("gate_up", {}).get("gbs") if kern else None,
+            "roofline": roof, "cpu_baseline": cpu, "kernels": kern,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,158 @@
+/*
+ * wf_bitnet.h -- C-ABI of the MI355X (gfx950) BitNet 1.58-bit hot path.
+ *
+ * This is the drop-in boundary that replaces the sgl-kernel CPU ops of the reference
+ * (extern/sglang-bitnet/sgl-kernel, un-vendored; API recovered in SURVEY.md §8b) and the kernels
+ * behind src/wrinklefree_inference/{kernels,kv_cache}. Plain pointers and sizes only: device
+ * pointers for tensor data, `stream` = a hipStream_t (NULL = the default stream). Every call is
+ * stream-ordered with no hidden synchronisation and no allocation (graph-capturable), except
+ * wf_model_* which own device memory.
+ *
+ * Return codes: WF_OK (0), WF_EINVAL (1, bad argument: the Python layer raises ValueError /
+ * RuntimeError like the reference's TORCH_CHECKs), WF_EHIP (2, HIP error), WF_ENOTSUP (3).
+ * wf_last_error() holds the message of the last failure on the calling thread.
+ *
+ * Packed-weight formats (enc = w + 1 in {0,1,2}):
+ *   WF_FMT_I2S : blocked I2_S [N, K/4] (cache/bitnet_converter.py:26-77) -- the reference layout.
+ *   WF_FMT_TQ  : ~1.6-bit [N, ceil(K/80)*16], 5 trits per byte (load-time bijection of I2_S).
+ */
+#ifndef WF_BITNET_H
+#define WF_BITNET_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WF_OK 0
+#define WF_EINVAL 1
+#define WF_EHIP 2
+#define WF_ENOTSUP 3
+
+enum { WF_F32 = 0, WF_BF16 = 1, WF_F16 = 2, WF_I8 = 3, WF_U8 = 4 };
+enum { WF_FMT_I2S = 0, WF_FMT_TQ = 1 };
+
+/* ---- library ------------------------------------------------------------------------------ */
+const char* wf_last_error(void);
+int wf_abi_version(void);
+/* sgl_kernel.quantization.bitnet_check_kernel_available (kernels/bitnet_patch.py:22;
+ * scripts/launch_sglang_bitnet.sh:44-50): 1 when a gfx950 device is visible and the kernels load. */
+int wf_check_kernel_available(void);
+
+/* ---- ternary GEMV / GEMM ------------------------------------------------ */
+/* torch.ops.sgl_kernel.bitnet_gemv_cpu(packed_weights, activations, scale)
+ * (docs/research/sglang_optimization_plan.md:61-64; call sites kernels/bitnet_patch.py:69,
+ * scripts/benchmark_kernels.py:46): y[n] = float(sum_k enc(W[n,k]) * a[k]) * scale. K % 128 == 0. */
+int wf_bitnet_gemv(const uint8_t* w, const int8_t* a, float scale, int N, int K, float* y, void* stream);
+/* torch.ops.sgl_kernel.bitnet_gemm_cpu (sglang_optimization_plan.md:66-70; bitnet_patch.py:73):
+ * Y[m,n] = float(sum_k enc(W[n,k]) * A[m,k]) * scale, one scale for the batch. */
+int wf_bitnet_gemm(const uint8_t* w, const int8_t* a, float scale, int M, int N, int K, float* y, void* stream);
+/* Same contract, any weight format and strides (lda/ldy in elements, lda % 16 == 0). */
+int wf_bitnet_gemm_ex(int fmt, const uint8_t* w, const int8_t* a, int64_t lda, float scale, int M, int N, int K,
+                      float* y, int64_t ldy, void* stream);
+/* kernels/native.py:27-65 (wrinklefree_inference.kernels.native gemv/gemm): signed (bits-1) dot
+ * on the LSB-interleaved layout byte[j] = w[4j] | w[4j+1]<<2 | ..., float(sum) * scale. */
+int wf_bitnet_gemm_lsb(const uint8_t* w, const int8_t* a, float scale, int M, int N, int K, float* y, void* stream);
+
+/* ---- activation int8 quantizer --------------------------------------------- */
+/* torch.ops.sgl_kernel.bitnet_quantize_activations_cpu (sglang_optimization_plan.md:72-74;
+ * semantics tests/test_bitnet_core.py:139-146): per-tensor m = max|x|, s = m/127 (double; m -> 1
+ * when m < 1e-6), q = clamp(rne(x / float(s)), -128, 127). Writes q and m (device float; the host
+ * forms s = double(m)/127 exactly as the reference). `dtype` of x: WF_F32 / WF_BF16 / WF_F16. */
+int wf_quantize_i8(const void* x, int dtype, int64_t n, int8_t* q, float* absmax, void* stream);
+/* Per-row variant (one scale per token; used by batched decode): row_absmax [M]. */
+int wf_quantize_i8_rows(const void* x, int dtype, int M, int K, int8_t* q, float* row_absmax, void* stream);
+/* kernels/native.py:244-256 variant: float32 scale, truncating cast. */
+int wf_quantize_i8_trunc(const void* x, int dtype, int64_t n, int8_t* q, float* absmax, void* stream);
+
+/* ---- load-time weight formats -------------------------------- */
+/* cache/bitnet_converter.py:26-77: float ternary weights [N,K] -> blocked I2_S [N,K/4]. */
+int wf_pack_i2s(const void* w, int dtype, int N, int K, uint8_t* out, void* stream);
+/* tests/test_bitnet_core.py:21-53 then :56-106: HF [N/4,K] uint8 -> I2_S [N,K/4]. */
+int wf_hf_to_i2s(const uint8_t* hf, int Np, int K, uint8_t* out, void* stream);
+/* I2_S [N,K/4] <-> TQ [N, ceil(K/80)*16] (bijection, K % 128 == 0). */
+int wf_i2s_to_tq(const uint8_t* i2s, int N, int K, uint8_t* tq, void* stream);
+int wf_tq_to_i2s(const uint8_t* tq, int N, int K, uint8_t* i2s, void* stream);
+int64_t wf_tq_row_bytes(int K);
+
+/* ---- KV cache ----------------------------------------------------- */
+/* sgl_kernel.kvcache.KVCacheManager.scatter_kv / gather_kv (tests/test_kv_cache_cpp.py:283-373;
+ * Python twin :20-127): pool [max_pages, L, 2, H, D] of elem_bytes-sized elements; k/v [T, H*D].
+ * gather writes into caller buffers. Page ids must be in [0, max_pages) (checked on device:
+ * out-of-range tokens are skipped and counted in *bad if bad != NULL). */
+int wf_kv_scatter(void* pool, int elem_bytes, int max_pages, int L, int H, int D, const void* k, const void* v,
+                  const int32_t* pages, int T, int layer, int32_t* bad, void* stream);
+int wf_kv_gather(const void* pool, int elem_bytes, int max_pages, int L, int H, int D, void* k_out, void* v_out,
+                 const int32_t* pages, int T, int layer, int32_t* bad, void* stream);
+/* KVCache._quantize_to_int8 / _quantize_to_fp8 (kv_cache/kv_cache.py:159-218): given m = max|x|
+ * (device), q = clamp(rne(x * float(127/m')), -127, 127), m' = m or 1 if m < 1e-6. */
+int wf_kv_quant_i8(const void* x, int dtype, int64_t n, const float* absmax, int8_t* q, void* stream);
+/* _dequantize_* (kv_cache.py:187-228): out = (float(q) * scale[0]) rounded to out_dtype. */
+int wf_kv_dequant_i8(const int8_t* q, int64_t n, const float* scale, void* out, int out_dtype, void* stream);
+
+/* Split-K decode attention for one query token per sequence (kv_cache.py:316-369 without GQA;
+ * scripts/direct_inference_full.py:229-244 with GQA). Strides are in elements.
+ *   q   : [B, Hq, D] (q_dtype)            out : [B, Hq, D] (out_dtype)
+ *   k,v : element (b, g, t, d) at b*kv_sb + g*kv_sh + t*kv_st + d (kv_dtype: BF16/F16/F32/I8;
+ *         I8 caches are dequantized as rbf16(float(q) * k_scale) like kv_cache.py:220-228)
+ *   seq_lens : [B] int32 device (NULL -> every sequence has S keys)
+ *   ws : workspace of wf_decode_attention_ws_bytes(B, Hq, D, S) bytes.                           */
+int64_t wf_decode_attention_ws_bytes(int B, int Hq, int D, int S);
+int wf_decode_attention(const void* q, int q_dtype, int64_t q_sb, int64_t q_sh, const void* k, const void* v,
+                        int kv_dtype, int64_t kv_sb, int64_t kv_sh, int64_t kv_st, float k_scale, float v_scale,
+                        int B, int Hq, int Hkv, int D, int S, const int32_t* seq_lens, float sm_scale, void* out,
+                        int out_dtype, int64_t o_sb, int64_t o_sh, void* ws, void* stream);
+
+/* ---- whole decode step (scripts/direct_inference_full.py:181-302) ------ */
+typedef struct {
+    int hidden, layers, n_heads, n_kv_heads, head_dim, inter, vocab, max_seq, batch;
+    float eps;
+    int wfmt;                     /* WF_FMT_I2S or WF_FMT_TQ for the ternary weights below         */
+    const uint16_t* embed;        /* [vocab, hidden] bf16 (tied LM head)                          */
+    const uint16_t* final_norm;   /* [hidden]                                                     */
+    const uint16_t* rope_cos;     /* [max_seq, head_dim/2] bf16                                   */
+    const uint16_t* rope_sin;
+    const uint16_t* ln_in;        /* [layers, hidden]                                             */
+    const uint16_t* ln_post;
+    const uint16_t* attn_sub;
+    const uint16_t* ffn_sub;      /* [layers, inter]                                              */
+    const uint8_t* w_qkv;         /* [layers, (Hq+2Hkv)*D rows] packed, rows q|k|v                */
+    const uint8_t* w_o;           /* [layers, hidden rows]                                        */
+    const uint8_t* w_gu;          /* [layers, 2*inter rows], gate/up interleaved in 8-row tiles   */
+    const uint8_t* w_d;           /* [layers, hidden rows] (K = inter)                            */
+    const float* wscale;          /* HOST [layers, 7] q,k,v,o,gate,up,down (copied at create)      */
+    /* caller-owned device state (read and written by every step)                                */
+    int32_t* tokens;              /* [batch]: input token; the step stores the greedy next token   */
+    int32_t* positions;           /* [batch]: position of the input token; the step increments it  */
+    uint16_t* logits;             /* [batch, vocab] bf16                                           */
+    uint16_t* k_cache;            /* [layers, batch, n_kv_heads, max_seq, head_dim] bf16           */
+    uint16_t* v_cache;
+} wf_model_desc;
+
+typedef struct wf_model wf_model;
+/* Validates the descriptor and allocates the private workspaces (activations, attention partials). */
+int wf_model_create(const wf_model_desc* d, wf_model** out);
+int wf_model_destroy(wf_model* m);
+/* One decode step for every sequence of the batch, stream-ordered; capturable into a HIP graph. */
+int wf_model_step(wf_model* m, void* stream);
+/* Capture wf_model_step into a graph once, then replay it (no host work per token). */
+int wf_model_graph_launch(wf_model* m, void* stream);
+/* Launch one op of the step (profiling / per-kernel timing). Ops, in step order: */
+enum {
+    WF_OP_EMBED = 0,      /* h = embed[token]                                   (layer ignored) */
+    WF_OP_QKV = 1,        /* fused norm + quantize + q|k|v GEMV + RoPE + cache write           */
+    WF_OP_ATTN = 2,       /* split-K GQA decode attention (+ combine)                          */
+    WF_OP_O = 3,          /* fused attn_sub_norm + o_proj + residual                           */
+    WF_OP_GATE_UP = 4,    /* fused post_attention_layernorm + gate|up + relu^2 * up            */
+    WF_OP_DOWN = 5,       /* fused ffn_sub_norm + down_proj + residual                         */
+    WF_OP_FINAL_NORM = 6, /*                                                    (layer ignored) */
+    WF_OP_LM_HEAD = 7,    /* tied bf16 LM head + per-block argmax               (layer ignored) */
+    WF_OP_ARGMAX = 8      /* greedy token + position advance                    (layer ignored) */
+};
+int wf_model_launch_op(wf_model* m, int layer, int op, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,143 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads and exports every symbol that
+include/wf_bitnet.h declares, the Python bindings cover them, the reference-facing modules import
+with the reference's names, and the host-side logic (layouts, numpy helpers, bookkeeping) matches
+the reference. No kernel is launched here (no GPU in this container)."""
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, load_golden
+
+HEADER = ROOT / "include" / "wf_bitnet.h"
+
+
+def declared_functions():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(wf_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    from wfamd import _lib
+    lib = _lib.load()
+    names = declared_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in wf_bitnet.h but not exported"
+    assert set(names) == set(_lib.SIGNATURES), "ctypes signature table out of sync with the header"
+    assert lib.wf_abi_version() == 1
+
+
+def test_library_has_gfx950_code_object():
+    so = ROOT / "wrinklefree-inference-engine_amd" / "lib" / "libwfbitnet.so"
+    blob = so.read_bytes()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob  # offload bundle entry of the gfx950 code object
+
+
+def test_no_device_means_not_available():
+    from sgl_kernel.quantization import bitnet_check_kernel_available
+    from sgl_kernel.quantization.bitnet import check_kernel_available
+    if not torch.cuda.is_available():
+        assert bitnet_check_kernel_available() is False
+        assert check_kernel_available() is False
+
+
+def test_reference_surface_names():
+    import sgl_kernel
+    from sgl_kernel import quantization as q
+    from sgl_kernel.quantization import bitnet as qb
+    for n in ("bitnet_gemv", "bitnet_gemm", "bitnet_quantize_activations", "bitnet_check_kernel_available",
+              "BITNET_BLOCK_SIZE", "quantize_activations_i8"):
+        assert hasattr(q, n), n
+    for n in ("bitnet_gemv", "quantize_activations_i8", "check_kernel_available", "auto_tune_tiles"):
+        assert hasattr(qb, n), n
+    assert q.BITNET_BLOCK_SIZE == 128
+    from sgl_kernel.kvcache import KVCacheManager, check_kernel_available  # noqa: F401
+    from wrinklefree_inference.kernels import (NATIVE_KERNELS_AVAILABLE, BitNetLinearNative,  # noqa: F401
+                                               benchmark_kernels, patch_model_with_native_kernels)
+    from wrinklefree_inference.kernels.bitnet_patch import extract_packed_weight_and_scale, pack_ternary_weights  # noqa
+    from wrinklefree_inference.kernels.native import (build_kernel, get_kernel, pack_weights,  # noqa: F401
+                                                      quantize_activations, repack_hf_weights, unpack_weights)
+    from wrinklefree_inference.kv_cache import (KVCache, KVCacheConfig, KVCacheDtype,  # noqa: F401
+                                                attention_with_kv_cache, compute_kv_cache_memory)
+    assert hasattr(torch.ops.sgl_kernel, "bitnet_gemv_cpu")
+    assert hasattr(torch.ops.sgl_kernel, "bitnet_gemm_cpu")
+    assert hasattr(torch.ops.sgl_kernel, "bitnet_quantize_activations_cpu")
+
+
+def test_torch_op_fake_impls():
+    """torch.compile shape propagation (docs/research/sglang_optimization_plan.md:61-74)."""
+    import sgl_kernel  # noqa: F401
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    with FakeTensorMode():
+        w = torch.empty(640, 640, dtype=torch.uint8)
+        a = torch.empty(2560, dtype=torch.int8)
+        assert torch.ops.sgl_kernel.bitnet_gemv_cpu(w, a, 0.5).shape == (640,)
+        a2 = torch.empty(4, 2560, dtype=torch.int8)
+        assert torch.ops.sgl_kernel.bitnet_gemm_cpu(w, a2, 0.5).shape == (4, 640)
+        q, s = torch.ops.sgl_kernel.bitnet_quantize_activations_cpu(torch.empty(3, 2560))
+        assert q.dtype == torch.int8 and q.shape == (3, 2560)
+
+
+def test_native_numpy_helpers_match_reference():
+    from wrinklefree_inference.kernels.native import pack_weights, quantize_activations, repack_hf_weights, unpack_weights
+    g = load_golden("packing")
+    assert np.array_equal(pack_weights(g["lsb_w"].astype(np.float32)), g["lsb_p"])
+    assert np.array_equal(unpack_weights(g["lsb_p"]).astype(np.int8), g["lsb_w"])
+    assert np.array_equal(repack_hf_weights(g["hf2lsb_in"]), g["hf2lsb_out"])
+    q = load_golden("quant")
+    for i in range(8):
+        qi, si = quantize_activations(q[f"x{i}"])
+        assert np.array_equal(qi, q[f"qt{i}"]) and np.float32(si) == q[f"st{i}"]
+
+
+def test_lsb_pack_matches_reference():
+    from wrinklefree_inference.kernels.bitnet_patch import pack_ternary_weights
+    g = load_golden("packing")
+    p, s = pack_ternary_weights(torch.from_numpy(g["lsb_w"].astype(np.float32)))
+    assert np.array_equal(p.numpy(), g["lsb_p"])
+
+
+def test_kv_memory_calc_matches_reference():
+    from wrinklefree_inference.kv_cache import KVCacheDtype, compute_kv_cache_memory
+    g = load_golden("kv")
+    mem = compute_kv_cache_memory({"num_layers": 30, "num_heads": 5, "head_dim": 128}, 4096, KVCacheDtype.BF16)
+    assert mem["total_mb"] == float(g["mem_total_mb"]) and mem["per_token_kb"] == float(g["mem_per_token_kb"])
+
+
+def test_kv_manager_allocation_semantics():
+    """tests/test_kv_cache_cpp.py:20-73 allocation order / failure behaviour (host bookkeeping)."""
+    from sgl_kernel.kvcache import KVCacheManager
+    g = load_golden("kv")
+    m = KVCacheManager(num_layers=3, num_heads=2, head_dim=8, page_size=16, max_pages=10, device="cpu")
+    a = m.allocate_pages(4)
+    m.free_pages(a[1:3])
+    b = m.allocate_pages(3)
+    single = m.allocate_page()
+    too_many = m.allocate_pages(100)
+    assert np.array_equal(a.numpy(), g["pg_a"]) and np.array_equal(b.numpy(), g["pg_b"])
+    assert single == int(g["pg_single"]) and too_many.numel() == int(g["pg_too_many"])
+    assert m.num_free_pages() == int(g["pg_free_after"])
+    with pytest.raises(RuntimeError):
+        m.scatter_kv(torch.zeros(1, 16), torch.zeros(1, 16), torch.tensor([0]), None, 0)
+
+
+def test_model_layout_permutations():
+    from wfamd.model import gate_up_interleave, qkv_row_permutation
+    p = qkv_row_permutation(3, 128)
+    assert sorted(p.tolist()) == list(range(384))
+    # block t of head h holds dims 8t..8t+7 and 64+8t..64+8t+7
+    blk = p[16 * 9:16 * 10].tolist()  # head 1, tile 1
+    assert blk == [128 + 8 + i for i in range(8)] + [128 + 72 + i for i in range(8)]
+    gu = gate_up_interleave(32)
+    assert sorted(gu.tolist()) == list(range(64))
+    assert gu[:16].tolist() == list(range(8)) + list(range(32, 40))
+
+
+def test_bytes_accounting():
+    from wfamd.model import BITNET_2B
+    assert BITNET_2B.ternary_weights() == 2_084_044_800
+    assert BITNET_2B.kv_bytes_per_token(1) == 76_800

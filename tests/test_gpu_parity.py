@@ -1,0 +1,350 @@
+"""GPU parity: every HIP kernel, called through the C-ABI, against the reference's golden vectors
+and the CPU oracle on the same seeded inputs. Integer/byte/index work is bit-exact; bf16 outputs
+use relative-L2 tolerances stated per test."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from wfamd import _lib
+    assert _lib.kernel_available(), "gfx950 kernels must load on the GPU box (no fallback)"
+    torch.cuda.set_device(0)
+
+
+def cu(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def bits(t: torch.Tensor) -> np.ndarray:
+    return t.contiguous().view(torch.int16).cpu().numpy().view(np.uint16)
+
+
+def rel_l2(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+# ------------------------------------------------------------------------------------------------
+# a1/a2 raw GEMV/GEMM
+# ------------------------------------------------------------------------------------------------
+def test_gemv_gemm_golden_bitexact():
+    from wfamd import ops
+    g = load_golden("gemv")
+    for i in range(7):
+        m, n, k = (int(v) for v in g[f"shape{i}"])
+        if k % 128:
+            with pytest.raises(ValueError):
+                ops.bitnet_gemm(cu(g[f"p{i}"]), cu(g[f"a{i}"]), float(g[f"scale{i}"]))
+            continue
+        y = ops.bitnet_gemm(cu(g[f"p{i}"]), cu(g[f"a{i}"]), float(g[f"scale{i}"])).cpu().numpy()
+        assert np.array_equal(y.view(np.uint32), g[f"y{i}"].view(np.uint32)), i
+        if m == 1:
+            y1 = ops.bitnet_gemv(cu(g[f"p{i}"]), cu(g[f"a{i}"][0]), float(g[f"scale{i}"])).cpu().numpy()
+            assert np.array_equal(y1, g[f"y{i}"][0]), i
+
+
+@pytest.mark.parametrize("n,k", [(2560, 2560), (640, 2560), (6912, 2560), (2560, 6912), (13824, 2560), (3840, 2560)])
+def test_gemv_model_shapes_vs_oracle(orc, n, k):
+    from wfamd import ops
+    from wfamd._lib import WF_FMT_TQ
+    rng = np.random.default_rng(n * 7 + k)
+    p = rng.integers(0, 81, size=(n, k // 4))
+    lut = np.array([((v // 27) % 3) << 6 | ((v // 9) % 3) << 4 | ((v // 3) % 3) << 2 | (v % 3) for v in range(81)],
+                   dtype=np.uint8)
+    p = lut[p]
+    a = rng.integers(-128, 128, size=k).astype(np.int8)
+    ref = orc.gemv_i2s(p, a, 0.01)
+    y = ops.bitnet_gemv(cu(p), cu(a), 0.01).cpu().numpy()
+    assert np.array_equal(y, ref)
+    # the ~1.6-bit TQ format gives the identical raw result
+    tq = ops.i2s_to_tq(cu(p))
+    assert np.array_equal(tq.cpu().numpy(), orc.pack_tq(p))
+    y2 = ops.bitnet_gemm_ex(tq, cu(a), 0.01, WF_FMT_TQ, in_features=k).cpu().numpy()
+    assert np.array_equal(y2, ref)
+    assert np.array_equal(ops.tq_to_i2s(tq, k).cpu().numpy(), p)
+
+
+@pytest.mark.parametrize("m", [2, 3, 5, 8, 16, 33])
+def test_gemm_batches_vs_oracle(orc, m):
+    from wfamd import ops
+    rng = np.random.default_rng(m)
+    w = rng.integers(-1, 2, size=(320, 1280)).astype(np.float32)
+    p = orc.pack_i2s(w)
+    a = rng.integers(-128, 128, size=(m, 1280)).astype(np.int8)
+    y = ops.bitnet_gemm(cu(p), cu(a), 1.7).cpu().numpy()
+    assert np.array_equal(y, orc.gemm_i2s(p, a, 1.7))
+    # GEMV == GEMM row consistency (tests/test_bitnet_weight_loading.py:270-302)
+    y0 = ops.bitnet_gemv(cu(p), cu(a[0]), 1.7).cpu().numpy()
+    assert np.array_equal(y0, y[0])
+
+
+def test_known_answer_and_errors():
+    """tests/test_bitnet_weight_loading.py:141-169: W=1, x=1, ws=2 -> raw 130048, corrected 2*K."""
+    from wfamd import ops
+    g = load_golden("gemv")
+    p = ops.pack_i2s(torch.ones(4, 256, device="cuda"))
+    q, s = ops.quantize_activations_i8(torch.ones(256, device="cuda"))
+    raw = ops.bitnet_gemv(p, q, 2.0).cpu().numpy()
+    assert np.array_equal(raw, g["ka_raw"]) and s == float(g["ka_s"])
+    corr = (torch.from_numpy(raw) - 2.0 * q.float().sum().item()) * s
+    assert np.allclose(corr.numpy(), g["ka_corr"])
+    with pytest.raises(ValueError):
+        ops.bitnet_gemv(torch.zeros(4, 40, dtype=torch.uint8, device="cuda"), torch.zeros(160, dtype=torch.int8,
+                                                                                          device="cuda"), 1.0)
+    with pytest.raises(ValueError):
+        ops.bitnet_gemv(torch.zeros(4, 64, dtype=torch.uint8, device="cuda"), torch.zeros(256, dtype=torch.float32,
+                                                                                          device="cuda"), 1.0)
+
+
+def test_host_tensors_roundtrip_through_gpu():
+    """Reference callers pass host tensors to the sgl-kernel ops: same values, returned on the host."""
+    from sgl_kernel.quantization import bitnet_gemv, bitnet_quantize_activations
+    g = load_golden("gemv")
+    y = bitnet_gemv(torch.from_numpy(g["p1"]), torch.from_numpy(g["a1"][0]), float(g["scale1"]))
+    assert not y.is_cuda and np.array_equal(y.numpy(), g["y1"][0])
+    q, s = bitnet_quantize_activations(torch.from_numpy(load_golden("quant")["x0"]))
+    assert not q.is_cuda
+    y2 = torch.ops.sgl_kernel.bitnet_gemv_cpu(torch.from_numpy(g["p1"]).cuda(), torch.from_numpy(g["a1"][0]).cuda(),
+                                              float(g["scale1"]))
+    assert np.array_equal(y2.cpu().numpy(), g["y1"][0])
+
+
+# ------------------------------------------------------------------------------------------------
+# a3 quantizers
+# ------------------------------------------------------------------------------------------------
+def test_quantize_golden_bitexact():
+    from wfamd import ops
+    g = load_golden("quant")
+    for i in range(8):
+        x = cu(g[f"x{i}"])
+        q, s = ops.quantize_activations_i8(x)
+        assert np.array_equal(q.cpu().numpy(), g[f"q{i}"]), i
+        assert s == float(g[f"s{i}"]), i
+        qt, st = ops.quantize_activations_trunc(x)
+        assert np.array_equal(qt.cpu().numpy(), g[f"qt{i}"]), i
+        assert np.float32(st) == g[f"st{i}"], i
+        # bf16 input path
+        xb = x.to(torch.bfloat16)
+        qb, sb = ops.quantize_activations_i8(xb)
+        from oracle import oracle as orc
+        qo, so = orc.quantize_i8(xb.float().cpu().numpy())
+        assert np.array_equal(qb.cpu().numpy(), qo) and sb == so
+
+
+def test_quantize_rows_vs_oracle(orc):
+    from wfamd import ops
+    x = np.random.default_rng(3).standard_normal((7, 2560)).astype(np.float32) * 5
+    q, s = ops.quantize_activations_rows(cu(x))
+    qo, so = orc.quantize_i8_rows(x)
+    assert np.array_equal(q.cpu().numpy(), qo)
+    assert np.array_equal(s.cpu().numpy(), so)
+
+
+# ------------------------------------------------------------------------------------------------
+# formats
+# ------------------------------------------------------------------------------------------------
+def test_pack_formats_golden():
+    from wfamd import ops
+    g = load_golden("packing")
+    for i in range(4):  # K % 128 == 0 cases
+        p = ops.pack_i2s(cu(g[f"w{i}"].astype(np.float32))).cpu().numpy()
+        assert np.array_equal(p, g[f"p{i}"]), i
+    # HF [N/4, K] -> I2_S through the reference's unpack+pack (incl. invalid code 3)
+    rng = np.random.default_rng(5)
+    hf = rng.integers(0, 256, size=(32, 256)).astype(np.uint8)
+    from oracle import oracle as orc
+    ref = orc.pack_i2s(orc.unpack_hf(hf))
+    assert np.array_equal(ops.hf_to_i2s(cu(hf)).cpu().numpy(), ref)
+
+
+def test_lsb_native_kernel_golden():
+    from wrinklefree_inference.kernels.native import build_kernel
+    g = load_golden("gemv")
+    k = build_kernel()
+    y = k.gemv(g["lsb_p"], g["lsb_a"], float(g["lsb_scale"]))
+    np.testing.assert_allclose(y, g["lsb_y"], rtol=1e-6, atol=1e-6)
+    assert k.num_threads() > 0
+
+
+# ------------------------------------------------------------------------------------------------
+# KV cache (a8/a9/a11)
+# ------------------------------------------------------------------------------------------------
+def test_kvcache_golden_all_dtypes():
+    from wrinklefree_inference.kv_cache import KVCache, KVCacheConfig, KVCacheDtype
+    g = load_golden("kv")
+    for name in ["BF16", "FP16", "FP32", "INT8", "FP8_E4M3"]:
+        cfg = KVCacheConfig(max_seq_len=32, num_layers=2, num_heads=4, head_dim=16, dtype=KVCacheDtype[name])
+        c = KVCache(cfg)
+        c.update(1, torch.from_numpy(g[f"{name}_k1"]), torch.from_numpy(g[f"{name}_v1"]), 0)
+        c.update(1, torch.from_numpy(g[f"{name}_k2"]), torch.from_numpy(g[f"{name}_v2"]), 5)
+        kg, vg = c.get(1)
+        assert np.array_equal(kg.float().cpu().numpy(), g[f"{name}_kget"]), name
+        assert np.array_equal(vg.float().cpu().numpy(), g[f"{name}_vget"]), name
+        st = c.cache[1, :, :8]
+        st = st.float() if name in ("BF16", "FP16", "FP32") else st.view(torch.int8)
+        assert np.array_equal(st.cpu().numpy(), g[f"{name}_storage"]), name
+        assert np.array_equal(c.k_scales.cpu().numpy(), g[f"{name}_kscale"]), name
+        assert np.array_equal(c.v_scales.cpu().numpy(), g[f"{name}_vscale"]), name
+
+
+def test_attention_with_kv_cache_golden():
+    """kv_cache.py:316-369 with a float32 query; tolerance rel-L2 1e-5 (fp32 summation order)."""
+    from wrinklefree_inference.kv_cache import KVCache, KVCacheConfig, KVCacheDtype, attention_with_kv_cache
+    g = load_golden("kv")
+    c = KVCache(KVCacheConfig(max_seq_len=64, num_layers=1, num_heads=4, head_dim=32, dtype=KVCacheDtype.BF16))
+    for pos in range(6):
+        o = attention_with_kv_cache(torch.from_numpy(g["att_q"][pos]), c, 0, torch.from_numpy(g["att_k"][pos]),
+                                    torch.from_numpy(g["att_v"][pos]), pos)
+        assert o.shape == (1, 4, 1, 32)
+        assert rel_l2(o.numpy(), g["att_o"][pos]) < 1e-5, pos
+
+
+def test_kv_manager_scatter_gather():
+    from sgl_kernel.kvcache import KVCacheManager
+    g = load_golden("kv")
+    m = KVCacheManager(num_layers=3, num_heads=2, head_dim=8, page_size=16, max_pages=10)
+    a = m.allocate_pages(4)
+    m.free_pages(a[1:3])
+    b = m.allocate_pages(3)
+    m.scatter_kv(torch.from_numpy(g["pg_k"]).reshape(3, -1), torch.from_numpy(g["pg_v"]).reshape(3, -1), b,
+                 torch.zeros(3, dtype=torch.int32), 2)
+    ko, vo = torch.zeros(3, 16), torch.zeros(3, 16)
+    m.gather_kv(ko, vo, b, torch.zeros(3, dtype=torch.int32), 2)
+    assert np.array_equal(ko.reshape(3, 2, 8).numpy(), g["pg_ko"])
+    assert np.array_equal(vo.reshape(3, 2, 8).numpy(), g["pg_vo"])
+    # reference shape: BitNet 20 heads x 128, 32 layers, all layers independent (tests/test_kv_cache_cpp.py:347-373)
+    m = KVCacheManager(num_layers=32, num_heads=20, head_dim=128, page_size=256, max_pages=100)
+    pages = m.allocate_pages(8)
+    ks = [torch.randn(8, 2560, device="cuda") for _ in range(32)]
+    vs = [torch.randn(8, 2560, device="cuda") for _ in range(32)]
+    for l in range(32):
+        m.scatter_kv(ks[l], vs[l], pages, None, l)
+    for l in range(32):
+        ko = torch.zeros(8, 2560, device="cuda")
+        vo = torch.zeros(8, 2560, device="cuda")
+        m.gather_kv(ko, vo, pages, None, l)
+        assert torch.equal(ko, ks[l]) and torch.equal(vo, vs[l])
+    bad = torch.tensor([0, 999], dtype=torch.int32)
+    m.scatter_kv(ks[0][:2], vs[0][:2], bad, None, 0)
+    assert m.invalid_page_count() == 1
+
+
+# ------------------------------------------------------------------------------------------------
+# decode attention (a10)
+# ------------------------------------------------------------------------------------------------
+def test_gqa_attention_golden():
+    """F.scaled_dot_product_attention(enable_gqa) in bf16 (golden) vs the HIP kernel: rel-L2 <= 5e-3."""
+    from wfamd import ops
+    g = load_golden("attention")
+    for i in range(4):
+        s = int(g[f"s{i}"])
+        q = cu(g[f"q{i}"].astype(np.int16)).view(torch.bfloat16).reshape(1, 20, 128)
+        k = cu(g[f"k{i}"].astype(np.int16)).view(torch.bfloat16)  # [S, Hkv, D]
+        v = cu(g[f"v{i}"].astype(np.int16)).view(torch.bfloat16)
+        o = ops.decode_attention(q, k, v, kv_strides=(0, 128, 5 * 128), B=1, Hq=20, Hkv=5, D=128, S=s)
+        got = o.float().cpu().numpy().reshape(-1)
+        ref = (g[f"o{i}"].astype(np.uint32) << 16).view(np.float32)
+        assert rel_l2(got, ref) < 5e-3, (i, rel_l2(got, ref))
+
+
+@pytest.mark.parametrize("S,B", [(4096, 1), (1000, 3), (64, 128)])
+def test_decode_attention_vs_oracle(orc, S, B):
+    """Long contexts / batches with ragged lengths vs the double-precision oracle: rel-L2 <= 4e-3 (bf16 out)."""
+    from wfamd import ops
+    rng = np.random.default_rng(S + B)
+    Hq, Hkv, D = 20, 5, 128
+    k = torch.randn(B, Hkv, S, D, device="cuda").to(torch.bfloat16)
+    v = torch.randn(B, Hkv, S, D, device="cuda").to(torch.bfloat16)
+    q = torch.randn(B, Hq, D, device="cuda").to(torch.bfloat16)
+    lens = torch.from_numpy(rng.integers(1, S + 1, size=B).astype(np.int32))
+    lens[0] = S
+    o = ops.decode_attention(q, k, v, kv_strides=(Hkv * S * D, S * D, D), B=B, Hq=Hq, Hkv=Hkv, D=D, S=S,
+                             seq_lens=lens.cuda())
+    for b in range(min(B, 4)):
+        ref = orc.attention_gqa_bf16(bits(q[b]), bits(k[b]), bits(v[b]), int(lens[b]))
+        assert rel_l2(orc.bf16_to_f32(bits(o[b])), orc.bf16_to_f32(ref)) < 4e-3, b
+
+
+# ------------------------------------------------------------------------------------------------
+# whole decode step (§8f rank 4)
+# ------------------------------------------------------------------------------------------------
+def _small_decoder(wfmt, batch=1):
+    from wfamd.model import BitNetConfig, BitNetDecoder, weights_from_arrays
+    g = load_golden("decode")
+    H, L, HQ, HKV, D, I, V, S = (int(v) for v in g["cfg"])
+    cfg = BitNetConfig(hidden=H, layers=L, n_heads=HQ, n_kv_heads=HKV, head_dim=D, inter=I, vocab=V, max_seq=S)
+    return g, BitNetDecoder(cfg, weights_from_arrays(g), batch=batch, wfmt=wfmt)
+
+
+@pytest.mark.parametrize("wfmt", [0, 1])
+def test_decode_steps_match_reference(orc, wfmt):
+    """Six decode tokens through the fused, graph-replayed step vs the reference golden logits
+    (scripts/direct_inference_full.py:267-302 run on the reference's functions) and vs the oracle.
+    Tolerance: rel-L2 of bf16 logits <= 1e-3; greedy token identical when the top-2 gap is clear."""
+    g, dec = _small_decoder(wfmt)
+    m = orc.DecodeModel(g)
+    for pos, tok in enumerate(g["tokens"]):
+        dec.set_state([int(tok)], [pos])
+        dec.step(graph=True)
+        torch.cuda.synchronize()
+        got = orc.bf16_to_f32(bits(dec.logits[0]))
+        ref = orc.bf16_to_f32(g["logits"][pos])
+        assert rel_l2(got, ref) < 1e-3, (pos, rel_l2(got, ref))
+        ologits, onext = m.step(int(tok), pos)
+        assert rel_l2(got, orc.bf16_to_f32(ologits)) < 1e-3
+        top2 = np.sort(ref)[-2:]
+        if top2[1] - top2[0] > 0.05 * abs(top2[1]):
+            assert int(dec.tokens[0].item()) == int(np.argmax(ref))
+        assert int(dec.positions[0].item()) == pos + 1
+    # the cache holds exactly what the reference wrote: compare K/V of layer 0 at the last position
+    kref = m.k_cache[0, :, len(g["tokens"]) - 1]
+    kgot = bits(dec.k_cache[0, 0, :, len(g["tokens"]) - 1])
+    assert rel_l2(orc.bf16_to_f32(kgot), orc.bf16_to_f32(kref)) < 1e-2
+
+
+def test_decode_graph_equals_eager_and_batch_rows_independent():
+    g, dec1 = _small_decoder(1, batch=1)
+    _, dec2 = _small_decoder(1, batch=1)
+    _, decb = _small_decoder(1, batch=4)
+    toks = [int(t) for t in g["tokens"]]
+    dec1.set_state([toks[0]], [0])
+    dec2.set_state([toks[0]], [0])
+    decb.set_state([toks[0]] * 4, [0] * 4)
+    for _ in range(4):
+        dec1.step(graph=True)
+        dec2.step(graph=False)
+        decb.step(graph=True)
+    torch.cuda.synchronize()
+    assert torch.equal(dec1.logits, dec2.logits)
+    assert torch.equal(dec1.tokens, dec2.tokens)
+    for b in range(4):
+        assert torch.equal(decb.logits[b], dec1.logits[0])
+        assert int(decb.tokens[b]) == int(dec1.tokens[0])
+
+
+def test_bitnet_linear_native_patch():
+    """kernels/bitnet_patch.py BitNetLinearNative on the HIP kernels equals the reference formula
+    (per-tensor quantize, scale = ws * act_scale, raw blocked-layout kernel, no correction)."""
+    from oracle import oracle as orc
+    from wrinklefree_inference.kernels.bitnet_patch import BitNetLinearNative
+    rng = np.random.default_rng(9)
+    w = rng.integers(-1, 2, size=(256, 512)).astype(np.float32)
+    p = orc.pack_i2s(w)
+    lin = BitNetLinearNative(512, 256, cu(p), torch.tensor(1.5))
+    x = rng.standard_normal((3, 512)).astype(np.float32)
+    y = lin(cu(x)).cpu().numpy()
+    q, s = orc.quantize_i8(x)
+    ref = orc.gemm_i2s(p, q, np.float32(1.5 * s))
+    assert np.array_equal(y, ref)
+    y1 = lin(cu(x[:1])).cpu().numpy()
+    q1, s1 = orc.quantize_i8(x[:1])
+    assert np.array_equal(y1, orc.gemm_i2s(p, q1, np.float32(1.5 * s1)))

@@ -1,0 +1,235 @@
+// wf_device.h -- gfx950 device helpers shared by the BitNet HIP kernels.
+//
+// Wave = 64 lanes (CDNA4). Packed-weight formats:
+//   I2S : the reference's blocked 2-bit layout (cache/bitnet_converter.py:26-77), [N][K/4] bytes.
+//         A 16-byte chunk c of a row = half h=c&1 of 128-wide block b=c>>1; byte j holds
+//         enc(w[128b+16h+j]) << 6 | enc(w[+32]) << 4 | enc(w[+64]) << 2 | enc(w[+96]).
+//   TQ  : the build's ~1.6-bit format (5 trits/byte, base 3; oracle/wf_oracle.c pack_tq), [N][C*16]
+//         bytes with C = ceil(K/80); chunk c, byte j, digit i <-> weight 80c + 16i + j.
+// Both store enc = w + 1 in {0,1,2}; the kernels accumulate sum(enc * a) exactly in int32, which is
+// the raw sgl-kernel semantics (tests/test_bitnet_core.py:149-167).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wf {
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------------------------------------
+// bf16 <-> f32 (bit exact, round-to-nearest-even; NaN stays NaN like torch .to(bfloat16))
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
+__device__ __forceinline__ float h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+__device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+
+// dtype codes shared with include/wf_bitnet.h
+enum { DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2, DT_I8 = 3, DT_U8 = 4 };
+
+__device__ __forceinline__ float load_as_f32(const void* p, int64_t i, int dt) {
+    if (dt == DT_F32) return ((const float*)p)[i];
+    if (dt == DT_BF16) return bf2f(((const uint16_t*)p)[i]);
+    return h2f(((const uint16_t*)p)[i]);
+}
+__device__ __forceinline__ void store_from_f32(void* p, int64_t i, int dt, float v) {
+    if (dt == DT_F32) ((float*)p)[i] = v;
+    else if (dt == DT_BF16) ((uint16_t*)p)[i] = f2bf(v);
+    else ((uint16_t*)p)[i] = f2h(v);
+}
+
+// ---------------------------------------------------------------------------------------------
+// wave / block reductions (wave64)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+// Reduce across the 16 lanes of a 16-lane group.
+__device__ __forceinline__ int group16_sum_i(int v) {
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 1, 64);
+    return v;
+}
+
+// Block-wide reductions over blockDim.x (multiple of 64, <= 1024). `red` is >= 16 floats of LDS.
+__device__ __forceinline__ float block_max(float v, float* red) {
+    v = wave_max(v);
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    float r = red[0];
+    for (int i = 1; i < nw; ++i) r = fmaxf(r, red[i]);
+    return r;
+}
+// Deterministic fixed-order sum (per-wave tree, then waves in order).
+__device__ __forceinline__ float block_sum(float v, float* red) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    float r = red[0];
+    for (int i = 1; i < nw; ++i) r += red[i];
+    return r;
+}
+__device__ __forceinline__ int block_sum_i(int v, int* red) {
+    v = wave_sum_i(v);
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    int r = red[0];
+    for (int i = 1; i < nw; ++i) r += red[i];
+    return r;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Activation quantization (tests/test_bitnet_core.py:139-146): s = double(m)/127 (m -> 1 if
+// m < 1e-6); q = clamp(rne(x / float(s)), -128, 127). Division is IEEE (hipcc's default
+// correctly-rounded fp32 divide), rint() is round-half-even.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double act_scale_from_max(float m) {
+    double md = (double)m;
+    if (md < 1e-6) md = 1.0;
+    return md / 127.0;
+}
+__device__ __forceinline__ int8_t quant_one(float x, float sf) {
+    float v = rintf(x / sf);
+    v = fminf(fmaxf(v, -128.f), 127.f);
+    return (int8_t)(int)v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Packed-weight formats and their LDS activation images.
+//
+// The GEMV kernels put 16 lanes on one weight row; lane `sub` (0..15) takes chunks c = sub + 16*i.
+// The activation image in LDS is laid out so that, for a fixed (i, group g), the 16 lanes' 16-byte
+// activation pieces are one contiguous 256-byte bank row -> every ds_read_b128 is conflict-free
+// (the other 48 lanes of the wave read the same addresses: broadcast).
+// ---------------------------------------------------------------------------------------------
+struct FmtI2S {
+    static constexpr int kGroups = 4;   // 16-byte activation pieces per chunk
+    static constexpr int kChunkW = 64;  // weights per 16-byte chunk
+    __host__ __device__ static int64_t row_bytes(int K) { return K / 4; }
+    __host__ __device__ static int chunks(int K) { return K / 64; }
+    __host__ __device__ static int k_pad(int K) { return K; }
+    // LDS byte offset of activation element k.
+    __device__ static __forceinline__ int lds_off(int k) {
+        const int b = k >> 7, r = k & 127, g = r >> 5, t = r & 31, h = t >> 4, j = t & 15;
+        const int c = 2 * b + h;
+        return (((c >> 4) * 4 + g) << 8) + ((c & 15) << 4) + j;
+    }
+};
+
+struct FmtTQ {
+    static constexpr int kGroups = 5;
+    static constexpr int kChunkW = 80;
+    __host__ __device__ static int chunks(int K) { return (K + 79) / 80; }
+    __host__ __device__ static int64_t row_bytes(int K) { return (int64_t)chunks(K) * 16; }
+    __host__ __device__ static int k_pad(int K) { return chunks(K) * 80; }
+    __device__ static __forceinline__ int lds_off(int k) {
+        const int c = k / 80, r = k - c * 80, g = r >> 4, j = r & 15;
+        return (((c >> 4) * 5 + g) << 8) + ((c & 15) << 4) + j;
+    }
+};
+
+// LDS bytes for one activation row image of K elements (rounded to whole 16-chunk stripes).
+template <class F>
+__host__ __device__ constexpr int lds_image_bytes(int K) {
+    return ((F::chunks(K) + 15) / 16) * F::kGroups * 256;
+}
+
+__device__ __forceinline__ int sdot4(uint32_t a, uint32_t b, int c) {
+    return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
+}
+
+// Per-chunk decode: fill `e[g][t]` = 4 enc bytes (one dword) of group g, dword t, for the chunk.
+// I2S: group g of dword t = (d_t >> (6 - 2g)) & 0x03030303.
+__device__ __forceinline__ void decode_i2s(const uint4 w, uint32_t (&e)[4][4]) {
+    const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+    constexpr uint32_t M = 0x03030303u;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        e[0][t] = (d[t] >> 6) & M;
+        e[1][t] = (d[t] >> 4) & M;
+        e[2][t] = (d[t] >> 2) & M;
+        e[3][t] = d[t] & M;
+    }
+}
+
+// TQ: bytes hold q; digit i = ((q*3^i mod 256)*3) >> 8. Even/odd bytes ride in 16-bit lanes so
+// one 24-bit multiply by 3 advances two bytes per register; the digit is the high byte of
+// each 16-bit lane (3*255 < 768 -> {0,1,2}), the low byte is the next q.
+__device__ __forceinline__ void decode_tq(const uint4 w, uint32_t (&e)[5][4]) {
+    const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        uint32_t E = d[t] & 0x00ff00ffu;
+        uint32_t O = (d[t] >> 8) & 0x00ff00ffu;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const uint32_t YE = (E << 1) + E;  // v_lshl_add_u32
+            const uint32_t YO = (O << 1) + O;
+            e[i][t] = ((YE >> 8) & 0x00ff00ffu) | (YO & 0xff00ff00u);
+            E = YE & 0x00ff00ffu;
+            O = YO & 0x00ff00ffu;
+        }
+    }
+}
+
+template <class F>
+struct Decoded;
+template <>
+struct Decoded<FmtI2S> {
+    uint32_t e[4][4];
+    __device__ __forceinline__ void load(const uint4 w) { decode_i2s(w, e); }
+};
+template <>
+struct Decoded<FmtTQ> {
+    uint32_t e[5][4];
+    __device__ __forceinline__ void load(const uint4 w) { decode_tq(w, e); }
+};
+
+// sum_g,t dot4(e[g][t], act[g][t]) with act read from the LDS image at stripe base `abase`
+// (abase = image + (i*G)*256 + sub*16; group g adds g*256).
+template <class F>
+__device__ __forceinline__ int chunk_dot(const Decoded<F>& dw, const int8_t* abase, int acc) {
+#pragma unroll
+    for (int g = 0; g < F::kGroups; ++g) {
+        const uint4 a = *reinterpret_cast<const uint4*>(abase + g * 256);
+        acc = sdot4(dw.e[g][0], a.x, acc);
+        acc = sdot4(dw.e[g][1], a.y, acc);
+        acc = sdot4(dw.e[g][2], a.z, acc);
+        acc = sdot4(dw.e[g][3], a.w, acc);
+    }
+    return acc;
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ldg_nt(const uint8_t* p) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+}  // namespace wf

@@ -1,0 +1,247 @@
+"""BitNet b1.58 decode runner on the fused HIP decode step (wf_model_* in include/wf_bitnet.h).
+
+Semantics follow scripts/direct_inference_full.py:181-302 (RMSNorm, BitNet linear with the
+encoding correction, half-split RoPE θ=5e5, GQA SDPA, attn_sub_norm, ReLU² MLP with ffn_sub_norm,
+tied bf16 LM head, greedy argmax). Per-token activation scales: sequence b of a batch computes
+exactly what a batch-1 decode of that sequence computes.
+
+Weights enter in the reference's canonical per-projection blocked I2_S layout
+([layers, out, in/4]); `build_device_layout` fuses them into the kernel layout:
+  * q|k|v rows concatenated; inside each 128-row head, row tile t holds dims 8t..8t+7 and
+    64+8t..64+8t+7 (so the RoPE pairs land in one block);
+  * gate/up interleaved in 8-row tiles [gate 8t..8t+7 | up 8t..8t+7];
+  * optionally repacked to the ~1.6-bit TQ format (lossless, wf_i2s_to_tq).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from . import _lib, ops
+from ._lib import WF_FMT_I2S, WF_FMT_TQ, WFModelDesc, call
+
+
+@dataclass
+class BitNetConfig:
+    hidden: int = 2560
+    layers: int = 30
+    n_heads: int = 20
+    n_kv_heads: int = 5
+    head_dim: int = 128
+    inter: int = 6912
+    vocab: int = 128256
+    max_seq: int = 4096
+    eps: float = 1e-5
+    rope_theta: float = 500000.0
+
+    @property
+    def kv_dim(self) -> int:
+        return self.n_kv_heads * self.head_dim
+
+    def ternary_weights(self) -> int:
+        h, i, kv = self.hidden, self.inter, self.kv_dim
+        return self.layers * (2 * h * h + 2 * kv * h + 3 * i * h)
+
+    def weight_bytes_per_token(self, wfmt: int) -> int:
+        """Algorithmic HBM bytes of one batch-1 decode step's weight stream (ternary + bf16 LM head)."""
+        h, i, kv = self.hidden, self.inter, self.kv_dim
+        rb = (lambda k: k // 4) if wfmt == WF_FMT_I2S else ops.tq_row_bytes
+        tern = self.layers * ((h + 2 * kv) * rb(h) + h * rb(h) + 2 * i * rb(h) + h * rb(i))
+        return tern + self.vocab * h * 2
+
+    def kv_bytes_per_token(self, ctx: int) -> int:
+        return self.layers * 2 * self.kv_dim * 2 * ctx
+
+
+BITNET_2B = BitNetConfig()
+
+
+def rope_tables(head_dim: int, max_seq: int, base: float):
+    """scripts/direct_inference_full.py:31-44 (fp32 freqs, cos/sin cast to bf16)."""
+    inv = 1.0 / (base ** (torch.arange(0, head_dim, 2, dtype=torch.float32) / head_dim))
+    fr = torch.outer(torch.arange(max_seq, dtype=torch.float32), inv)
+    return torch.cos(fr).to(torch.bfloat16), torch.sin(fr).to(torch.bfloat16)
+
+
+def _as_bf16(x, device) -> torch.Tensor:
+    if isinstance(x, np.ndarray):
+        if x.dtype == np.uint16:
+            return torch.from_numpy(x.astype(np.int16)).view(torch.bfloat16).to(device)
+        return torch.from_numpy(x).to(device=device, dtype=torch.bfloat16)
+    return x.to(device=device, dtype=torch.bfloat16)
+
+
+def _as_u8(x, device) -> torch.Tensor:
+    if isinstance(x, np.ndarray):
+        return torch.from_numpy(np.ascontiguousarray(x)).to(device)
+    return x.to(device)
+
+
+def qkv_row_permutation(n_heads_total: int, head_dim: int = 128) -> torch.Tensor:
+    half = head_dim // 2
+    per = []
+    for t in range(half // 8):
+        per.extend(range(8 * t, 8 * t + 8))
+        per.extend(range(half + 8 * t, half + 8 * t + 8))
+    per = torch.tensor(per, dtype=torch.long)
+    return torch.cat([h * head_dim + per for h in range(n_heads_total)])
+
+
+def gate_up_interleave(inter: int) -> torch.Tensor:
+    idx = []
+    for t in range(inter // 8):
+        idx.extend(range(8 * t, 8 * t + 8))
+        idx.extend(range(inter + 8 * t, inter + 8 * t + 8))
+    return torch.tensor(idx, dtype=torch.long)
+
+
+_LUT81 = None
+
+
+def random_i2s(shape, generator: torch.Generator) -> torch.Tensor:
+    """Uniform ternary weights (randint(-1, 2), scripts/benchmark_kernels.py:35) packed as I2_S bytes:
+    every byte holds 4 independent enc codes in {0,1,2}. Generated on the generator's device."""
+    global _LUT81
+    dev = generator.device
+    if _LUT81 is None or _LUT81.device != dev:
+        lut = torch.zeros(81, dtype=torch.uint8)
+        for v in range(81):
+            d = [(v // 3 ** i) % 3 for i in range(4)]
+            lut[v] = (d[0] << 6) | (d[1] << 4) | (d[2] << 2) | d[3]
+        _LUT81 = lut.to(dev)
+    idx = torch.randint(0, 81, shape, generator=generator, device=dev, dtype=torch.int64)
+    return _LUT81[idx]
+
+
+def synthetic_weights(cfg: BitNetConfig, seed: int = 0, device="cuda") -> Dict[str, torch.Tensor]:
+    """Random-init weights of the bitnet-b1.58-2B-4T architecture (no checkpoint offline)."""
+    device = torch.device(device)
+    g = torch.Generator(device=device).manual_seed(seed)
+    h, i, kv, L = cfg.hidden, cfg.inter, cfg.kv_dim, cfg.layers
+    w = {}
+    shapes = {"wq": (h, h // 4), "wk": (kv, h // 4), "wv": (kv, h // 4), "wo": (h, h // 4),
+              "wg": (i, h // 4), "wu": (i, h // 4), "wd": (h, i // 4)}
+    for name, shp in shapes.items():
+        w[name] = torch.stack([random_i2s(shp, g) for _ in range(L)])
+    w["embed"] = (torch.randn(cfg.vocab, h, generator=g, device=device) * 0.02).to(torch.bfloat16)
+    w["final_norm"] = (1.0 + 0.1 * torch.randn(h, generator=g, device=device)).to(torch.bfloat16)
+    for name, n in (("ln_in", h), ("ln_post", h), ("attn_sub", h), ("ffn_sub", i)):
+        w[name] = (1.0 + 0.1 * torch.randn(L, n, generator=g, device=device)).to(torch.bfloat16)
+    w["wscale"] = (torch.rand(L, 7, generator=g, device=device) * 0.5 + 1.5).to(torch.float32).cpu()
+    return w
+
+
+def weights_from_arrays(a: dict, device="cuda") -> Dict[str, torch.Tensor]:
+    """Host arrays in the tests/golden/decode.npz layout -> device tensors."""
+    w = {n: _as_u8(a[n], device) for n in ("wq", "wk", "wv", "wo", "wg", "wu", "wd")}
+    for n in ("embed", "final_norm", "ln_in", "ln_post", "attn_sub", "ffn_sub"):
+        w[n] = _as_bf16(a[n], device)
+    w["wscale"] = torch.from_numpy(np.asarray(a["wscale"], dtype=np.float32))
+    return w
+
+
+def build_device_layout(cfg: BitNetConfig, w: Dict[str, torch.Tensor], wfmt: int = WF_FMT_TQ):
+    """Fuse per-projection I2_S weights into the kernel layout (and repack to TQ if asked)."""
+    dev = w["wq"].device
+    hq_tot = cfg.n_heads + 2 * cfg.n_kv_heads
+    perm = qkv_row_permutation(hq_tot, cfg.head_dim).to(dev)
+    gu = gate_up_interleave(cfg.inter).to(dev)
+    out = {"w_qkv": [], "w_o": [], "w_gu": [], "w_d": []}
+    for l in range(cfg.layers):
+        qkv = torch.cat([w["wq"][l], w["wk"][l], w["wv"][l]], dim=0).index_select(0, perm)
+        gate_up = torch.cat([w["wg"][l], w["wu"][l]], dim=0).index_select(0, gu)
+        parts = {"w_qkv": qkv, "w_o": w["wo"][l], "w_gu": gate_up, "w_d": w["wd"][l]}
+        for name, t in parts.items():
+            out[name].append(ops.i2s_to_tq(t.contiguous()) if wfmt == WF_FMT_TQ else t.contiguous())
+    return {k: torch.stack(v).contiguous() for k, v in out.items()}
+
+
+class BitNetDecoder:
+    """Owns the device layout, the caller-side state tensors and the wf_model handle."""
+
+    def __init__(self, cfg: BitNetConfig, weights: Dict[str, torch.Tensor], batch: int = 1,
+                 wfmt: int = WF_FMT_TQ, device="cuda"):
+        self.cfg, self.batch, self.wfmt = cfg, batch, wfmt
+        self.dev = torch.device(device)
+        lay = build_device_layout(cfg, weights, wfmt)
+        self.w_qkv, self.w_o, self.w_gu, self.w_d = lay["w_qkv"], lay["w_o"], lay["w_gu"], lay["w_d"]
+        self.embed = weights["embed"].contiguous()
+        self.final_norm = weights["final_norm"].contiguous()
+        self.norms = {n: weights[n].contiguous() for n in ("ln_in", "ln_post", "attn_sub", "ffn_sub")}
+        cos, sin = rope_tables(cfg.head_dim, cfg.max_seq, cfg.rope_theta)
+        self.rope_cos, self.rope_sin = cos.to(self.dev).contiguous(), sin.to(self.dev).contiguous()
+        self.wscale = weights["wscale"].detach().cpu().to(torch.float32).contiguous()
+        L, B = cfg.layers, batch
+        self.tokens = torch.zeros(B, dtype=torch.int32, device=self.dev)
+        self.positions = torch.zeros(B, dtype=torch.int32, device=self.dev)
+        self.logits = torch.zeros(B, cfg.vocab, dtype=torch.bfloat16, device=self.dev)
+        kv_shape = (L, B, cfg.n_kv_heads, cfg.max_seq, cfg.head_dim)
+        self.k_cache = torch.zeros(kv_shape, dtype=torch.bfloat16, device=self.dev)
+        self.v_cache = torch.zeros(kv_shape, dtype=torch.bfloat16, device=self.dev)
+        d = WFModelDesc()
+        d.hidden, d.layers, d.n_heads, d.n_kv_heads = cfg.hidden, L, cfg.n_heads, cfg.n_kv_heads
+        d.head_dim, d.inter, d.vocab, d.max_seq, d.batch = cfg.head_dim, cfg.inter, cfg.vocab, cfg.max_seq, B
+        d.eps, d.wfmt = cfg.eps, wfmt
+        d.embed, d.final_norm = self.embed.data_ptr(), self.final_norm.data_ptr()
+        d.rope_cos, d.rope_sin = self.rope_cos.data_ptr(), self.rope_sin.data_ptr()
+        d.ln_in, d.ln_post = self.norms["ln_in"].data_ptr(), self.norms["ln_post"].data_ptr()
+        d.attn_sub, d.ffn_sub = self.norms["attn_sub"].data_ptr(), self.norms["ffn_sub"].data_ptr()
+        d.w_qkv, d.w_o, d.w_gu, d.w_d = (t.data_ptr() for t in (self.w_qkv, self.w_o, self.w_gu, self.w_d))
+        d.wscale = self.wscale.data_ptr()
+        d.tokens, d.positions, d.logits = self.tokens.data_ptr(), self.positions.data_ptr(), self.logits.data_ptr()
+        d.k_cache, d.v_cache = self.k_cache.data_ptr(), self.v_cache.data_ptr()
+        self._desc = d
+        h = C.c_void_p()
+        call("wf_model_create", C.addressof(d), C.addressof(h))
+        self._h = h
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None) and self._h.value:
+                _lib.load().wf_model_destroy(self._h)
+                self._h = C.c_void_p()
+        except Exception:
+            pass
+
+    def set_state(self, tokens, positions) -> None:
+        self.tokens.copy_(torch.as_tensor(tokens, dtype=torch.int32))
+        self.positions.copy_(torch.as_tensor(positions, dtype=torch.int32))
+
+    def fill_kv_random(self, ctx: int, seed: int = 0) -> None:
+        """Synthetic context: random bf16 K/V for positions [0, ctx) of every sequence."""
+        g = torch.Generator(device=self.dev).manual_seed(seed)
+        for l in range(self.cfg.layers):
+            for c in (self.k_cache, self.v_cache):
+                c[l, :, :, :ctx].normal_(generator=g)
+
+    def step(self, graph: bool = True) -> None:
+        """One decode token for every sequence (stream-ordered; no host sync)."""
+        st = torch.cuda.current_stream().cuda_stream
+        call("wf_model_graph_launch" if graph else "wf_model_step", self._h, st)
+
+    @property
+    def weight_bytes(self) -> int:
+        return sum(t.numel() for t in (self.w_qkv, self.w_o, self.w_gu, self.w_d)) + self.embed.numel() * 2
+
+    def launch_op(self, layer: int, op: int) -> None:
+        """Launch one op of the decode step (WF_OP_*), for per-kernel timing/profiling."""
+        call("wf_model_launch_op", self._h, int(layer), int(op), torch.cuda.current_stream().cuda_stream)
+
+    def op_bytes(self, op: int, ctx: int = 0) -> int:
+        """Algorithmic HBM bytes of one launch of `op` at batch `self.batch` (weights once, activations
+        and outputs per sequence, K/V rows per cached position)."""
+        cfg, B = self.cfg, self.batch
+        h, i, kv, D = cfg.hidden, cfg.inter, cfg.kv_dim, cfg.head_dim
+        per_layer = {
+            _lib.WF_OP_QKV: self.w_qkv[0].numel() + B * (2 * h + 2 * (h + 2 * kv)),
+            _lib.WF_OP_O: self.w_o[0].numel() + B * (2 * h + 4 * h),
+            _lib.WF_OP_GATE_UP: self.w_gu[0].numel() + B * (2 * h + 2 * i),
+            _lib.WF_OP_DOWN: self.w_d[0].numel() + B * (2 * i + 4 * h),
+            _lib.WF_OP_ATTN: B * (2 * kv * 2 * ctx + 2 * 2 * h),
+            _lib.WF_OP_LM_HEAD: self.embed.numel() * 2 + B * (2 * h + 2 * cfg.vocab),
+        }
+        return int(per_layer.get(op, 0))
