@@ -45,9 +45,11 @@ def parse():
     return ap.parse_args()
 
 
-def op_timing(dec, ctx):
-    """Per-op average kernel duration (HIP events on the launch stream) with a cache flush before
-    every launch, plus algorithmic bytes per launch."""
+def op_timing(dec, ctx, reps: int = 3):
+    """Per-op average kernel duration measured with HIP events on the launch stream. Each
+    measurement starts after an Infinity-Cache flush (so weights stream from HBM) and brackets the
+    op's launches for all 30 layers back to back (its real in-step cadence: one launch per layer,
+    distinct weights each time); the LM head is one launch. Also returns algorithmic bytes."""
     import torch
     from wfamd import _lib
     L = dec.cfg.layers
@@ -56,23 +58,23 @@ def op_timing(dec, ctx):
            (_lib.WF_OP_GATE_UP, "gate_up"), (_lib.WF_OP_DOWN, "down"), (_lib.WF_OP_LM_HEAD, "lm_head")]
     rec = []
     st = torch.cuda.current_stream()
-    for rep in range(2):
+    for rep in range(reps):
         for op, name in ops:
-            layers = [0] if op == _lib.WF_OP_LM_HEAD else range(L)
+            layers = [0] if op == _lib.WF_OP_LM_HEAD else list(range(L))
+            flush.fill_(rep)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
             for l in layers:
-                flush.fill_(rep)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(st)
                 dec.launch_op(l, op)
-                e1.record(st)
-                rec.append((name, op, e0, e1))
+            e1.record(st)
+            rec.append((name, op, len(layers), e0, e1))
     torch.cuda.synchronize()
     out = {}
-    for name, op, e0, e1 in rec:
-        out.setdefault(name, {"op": op, "ms": []})["ms"].append(e0.elapsed_time(e1))
+    for name, op, n, e0, e1 in rec:
+        out.setdefault(name, {"op": op, "us": []})["us"].append(1000.0 * e0.elapsed_time(e1) / n)
     res = {}
     for name, v in out.items():
-        us = 1000.0 * sum(v["ms"]) / len(v["ms"])
+        us = min(v["us"])
         nbytes = dec.op_bytes(v["op"], ctx)
         per_tok = 1 if v["op"] == _lib.WF_OP_LM_HEAD else L
         res[name] = {"us": round(us, 3), "bytes": nbytes, "gbs": round(nbytes / us / 1e3, 1),

@@ -13,20 +13,12 @@
 namespace wf {
 
 constexpr int kAttnThreads = 256;
-constexpr int kAttnMinSplit = 64;   // keys per split (lower bound)
-constexpr int kAttnTargetBlocks = 512;
+constexpr int kAttnU = 4;  // key positions per lane group per split (all loads issued up front)
 
-static inline int attn_splits(int B, int Hkv, int S) {
-    int target = (kAttnTargetBlocks + B * Hkv - 1) / (B * Hkv);
-    if (target < 1) target = 1;
-    int T = (S + target - 1) / target;
-    if (T < kAttnMinSplit) T = kAttnMinSplit;
-    return (S + T - 1) / T;
-}
-static inline int attn_split_len(int B, int Hkv, int S) {
-    const int ns = attn_splits(B, Hkv, S);
-    return (S + ns - 1) / ns;
-}
+// keys per split: kAttnU positions x (256 / (D/8)) lane groups  (D = 128 -> 64)
+static inline int attn_split_len(int D) { return kAttnU * (kAttnThreads / (D / 8)); }
+static inline int attn_splits(int D, int S) { return (S + attn_split_len(D) - 1) / attn_split_len(D); }
+static inline int64_t attn_cnt_bytes(int B, int Hkv) { return (((int64_t)B * Hkv * 4) + 255) / 256 * 256; }
 
 // Load 8 consecutive KV elements as f32.
 template <int KVDT>
@@ -57,34 +49,74 @@ __device__ __forceinline__ void load8(const void* base, int64_t off, float scale
     }
 }
 
-// One block = one (sequence b, kv head g, split s). Partial results (m, l, o[D]) per query head
-// go to the workspace; k_attn_combine merges the splits.
+// Raw 16-byte KV load (decoded later, so every load of the split is in flight at once).
+template <int KVDT>
+struct KVRaw {
+    uint4 a, b;  // b used by f32 only
+    __device__ __forceinline__ void load(const void* base, int64_t off) {
+        if constexpr (KVDT == DT_F32) {
+            const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(base) + off);
+            a = p[0];
+            b = p[1];
+        } else if constexpr (KVDT == DT_I8) {
+            const uint2 r = *reinterpret_cast<const uint2*>(reinterpret_cast<const int8_t*>(base) + off);
+            a = make_uint4(r.x, r.y, 0, 0);
+        } else {
+            a = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(base) + off);
+        }
+    }
+    __device__ __forceinline__ void decode(float scale, float (&x)[8]) const {
+        const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+        if constexpr (KVDT == DT_BF16) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { x[2 * i] = __uint_as_float(w[i] << 16); x[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
+        } else if constexpr (KVDT == DT_F16) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { x[2 * i] = h2f((uint16_t)(w[i] & 0xffffu)); x[2 * i + 1] = h2f((uint16_t)(w[i] >> 16)); }
+        } else if constexpr (KVDT == DT_F32) {
+            x[0] = __uint_as_float(a.x); x[1] = __uint_as_float(a.y); x[2] = __uint_as_float(a.z); x[3] = __uint_as_float(a.w);
+            x[4] = __uint_as_float(b.x); x[5] = __uint_as_float(b.y); x[6] = __uint_as_float(b.z); x[7] = __uint_as_float(b.w);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[i] = rbf((float)(int8_t)(w[i >> 2] >> (8 * (i & 3))) * scale);
+        }
+    }
+};
+
+template <class T>
+__device__ __forceinline__ void st_sc1(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <class T>
+__device__ __forceinline__ T ld_sc1(const T* p) { return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// One block = one (sequence b, kv head g, split s of T keys). Lane group `gid` (D/8 lanes, 8 head
+// dims per lane) owns keys t0 + gid + NG*u, u < kAttnU, loads all of them first, then does a local
+// softmax; groups merge by shuffles and through LDS. With NS > 1 the block publishes (m, l, o)
+// partials write-through (sc1) and bumps a per-(b, g) ticket; the last arriver merges the splits
+// and writes the output (MI355X_MICROARCH.md "Valid forms" row 1: sc1 stores, vmcnt(0) in every
+// storing wave, a barrier, one agent-scope atomic add; sc1 loads in the last arriver). The last
+// arriver also re-arms the ticket for the next launch.
 template <int D, int G, int KVDT>
 __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
     const void* __restrict__ q, int qdt, int64_t q_sb, int64_t q_sh, const void* __restrict__ K,
     const void* __restrict__ V, int64_t kv_sb, int64_t kv_sh, int64_t kv_st, float k_scale, float v_scale, int Hq,
-    int Hkv, int S, const int32_t* __restrict__ seq_lens, float sm_scale, int NS, int T, float* __restrict__ ws) {
-    constexpr int LP = D / 8;        // lanes per key position
-    constexpr int PW = 64 / LP;      // positions per wave-instruction
+    int Hkv, int S, const int32_t* __restrict__ seq_lens, float sm_scale, int NS, unsigned* __restrict__ cnt,
+    float* __restrict__ part, void* __restrict__ out, int odt, int64_t o_sb, int64_t o_sh) {
+    constexpr int LP = D / 8;                // lanes per key position
+    constexpr int NG = kAttnThreads / LP;    // lane groups per block
     constexpr int NW = kAttnThreads / 64;
+    constexpr int T = kAttnU * NG;
     const int s = blockIdx.x, g = blockIdx.y, b = blockIdx.z;
-    const int grp = Hq / Hkv;        // runtime group size (<= G)
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int pg = lane / LP, li = lane % LP;
+    const int grp = Hq / Hkv;
+    const int wave = threadIdx.x >> 6;
+    const int gid = threadIdx.x / LP, li = threadIdx.x % LP;
     const int Sb = seq_lens ? min(seq_lens[b], S) : S;
-    const int t0 = s * T, t1 = min(Sb, t0 + T);
+    const int t0 = s * T;
+    const int nact = (Sb + T - 1) / T;       // splits that hold keys for this sequence
 
-    float qv[G][8];
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qv[h][j] = 0.f;
-        if (h < grp) {
-            const int64_t qo = b * q_sb + (int64_t)(g * grp + h) * q_sh + li * 8;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) qv[h][j] = load_as_f32(q, qo + j, qdt);
-        }
-    }
+    __shared__ float sm_m[NW][G], sm_l[NW][G];
+    __shared__ float sm_o[NW][G][D];
+    __shared__ int sh_last;
+
     float m[G], l[G], o[G][8];
 #pragma unroll
     for (int h = 0; h < G; ++h) {
@@ -93,35 +125,66 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[h][j] = 0.f;
     }
-    const int64_t kvb = b * kv_sb + g * kv_sh + li * 8;
-    for (int t = t0 + wave * PW + pg; t < t1; t += NW * PW) {
-        float kx[8], vx[8];
-        load8<KVDT>(K, kvb + t * kv_st, k_scale, kx);
-        load8<KVDT>(V, kvb + t * kv_st, v_scale, vx);
-        float sc[G];
+    if (t0 < Sb) {
+        const int64_t kvb = b * kv_sb + g * kv_sh + li * 8;
+        KVRaw<KVDT> kr[kAttnU], vr[kAttnU];
+#pragma unroll
+        for (int u = 0; u < kAttnU; ++u) {
+            const int t = min(t0 + gid + NG * u, Sb - 1);
+            kr[u].load(K, kvb + t * kv_st);
+            vr[u].load(V, kvb + t * kv_st);
+        }
+        float qv[G][8];
 #pragma unroll
         for (int h = 0; h < G; ++h) {
-            float d = 0.f;
+            const int64_t qo = b * q_sb + (int64_t)(g * grp + min(h, grp - 1)) * q_sh + li * 8;
+            if (qdt == DT_BF16) {
+                const uint4 r = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(q) + qo);
+                const uint32_t w[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
-            for (int j = 0; j < 8; ++j) d = fmaf(qv[h][j], kx[j], d);
+                for (int i = 0; i < 4; ++i) { qv[h][2 * i] = __uint_as_float(w[i] << 16); qv[h][2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
+            } else {
 #pragma unroll
-            for (int off = LP / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
-            sc[h] = d * sm_scale;
+                for (int j = 0; j < 8; ++j) qv[h][j] = load_as_f32(q, qo + j, qdt);
+            }
+        }
+        float sc[kAttnU][G];
+#pragma unroll
+        for (int u = 0; u < kAttnU; ++u) {
+            float kx[8];
+            kr[u].decode(k_scale, kx);
+            const bool valid = t0 + gid + NG * u < Sb;
+#pragma unroll
+            for (int h = 0; h < G; ++h) {
+                float d = 0.f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) d = fmaf(qv[h][j], kx[j], d);
+#pragma unroll
+                for (int off = LP / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+                sc[u][h] = valid ? d * sm_scale : -INFINITY;
+            }
         }
 #pragma unroll
         for (int h = 0; h < G; ++h) {
-            if (h < grp) {
-                const float mn = fmaxf(m[h], sc[h]);
-                const float al = __expf(m[h] - mn);
-                const float p = __expf(sc[h] - mn);
-                l[h] = l[h] * al + p;
+            float mx = sc[0][h];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) o[h][j] = fmaf(p, vx[j], o[h][j] * al);
-                m[h] = mn;
+            for (int u = 1; u < kAttnU; ++u) mx = fmaxf(mx, sc[u][h]);
+            m[h] = mx;
+        }
+#pragma unroll
+        for (int u = 0; u < kAttnU; ++u) {
+            float vx[8];
+            vr[u].decode(v_scale, vx);
+#pragma unroll
+            for (int h = 0; h < G; ++h) {
+                const float p = (sc[u][h] == -INFINITY) ? 0.f : __expf(sc[u][h] - m[h]);
+                l[h] += p;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o[h][j] = fmaf(p, vx[j], o[h][j]);
             }
         }
     }
-    // merge the PW position groups of the wave (same li, different pg)
+    // merge the GW lane groups of a wave (same li, different gid)
 #pragma unroll
     for (int off = LP; off < 64; off <<= 1) {
 #pragma unroll
@@ -132,17 +195,11 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
             const float c = (mo == -INFINITY) ? 0.f : __expf(mo - mn);
             l[h] = l[h] * a + lo * c;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float oo = __shfl_xor(o[h][j], off, 64);
-                o[h][j] = o[h][j] * a + oo * c;
-            }
+            for (int j = 0; j < 8; ++j) o[h][j] = o[h][j] * a + __shfl_xor(o[h][j], off, 64) * c;
             m[h] = mn;
         }
     }
-    // merge the NW waves through LDS (lanes with pg == 0 hold the wave's result)
-    __shared__ float sm_m[NW][G], sm_l[NW][G];
-    __shared__ float sm_o[NW][G][D];
-    if (pg == 0) {
+    if ((threadIdx.x & 63) < LP) {
 #pragma unroll
         for (int h = 0; h < G; ++h) {
             if (li == 0) { sm_m[wave][h] = m[h]; sm_l[wave][h] = l[h]; }
@@ -151,7 +208,7 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
         }
     }
     __syncthreads();
-    // thread -> (h, d): G*D outputs over 256 threads
+    // block result per (h, d); thread -> idx
     for (int idx = threadIdx.x; idx < grp * D; idx += kAttnThreads) {
         const int h = idx / D, d = idx - h * D;
         float mx = -INFINITY;
@@ -165,29 +222,71 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
             os += sm_o[w][h][d] * a;
         }
         const int hq = g * grp + h;
-        float* po = ws + (((int64_t)b * Hq + hq) * NS + s) * (D + 2);
-        po[2 + d] = os;
-        if (d == 0) { po[0] = mx; po[1] = ls; }
-    }
-}
-
-// Merge NS split partials per (b, query head) and write the output row.
-__global__ void k_attn_combine(const float* __restrict__ ws, int Hq, int D, int NS, void* __restrict__ out, int odt,
-                               int64_t o_sb, int64_t o_sh) {
-    const int h = blockIdx.x, b = blockIdx.y;
-    const float* p = ws + ((int64_t)b * Hq + h) * NS * (D + 2);
-    float mx = -INFINITY;
-    for (int s = 0; s < NS; ++s) mx = fmaxf(mx, p[s * (D + 2)]);
-    for (int d = threadIdx.x; d < D; d += blockDim.x) {
-        float ls = 0.f, os = 0.f;
-        for (int s = 0; s < NS; ++s) {
-            const float ms = p[s * (D + 2)];
-            const float a = (ms == -INFINITY) ? 0.f : __expf(ms - mx);
-            ls += p[s * (D + 2) + 1] * a;
-            os += p[s * (D + 2) + 2 + d] * a;
+        if (NS == 1) {
+            store_from_f32(out, b * o_sb + (int64_t)hq * o_sh + d, odt, os / ls);
+        } else if (t0 < Sb) {
+            float* po = part + (((int64_t)b * Hq + hq) * NS + s) * (D + 2);
+            st_sc1(po + 2 + d, os);
+            if (d == 0) { st_sc1(po, mx); st_sc1(po + 1, ls); }
         }
-        store_from_f32(out, b * o_sb + (int64_t)h * o_sh + d, odt, os / ls);
     }
+    if (NS == 1) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add(cnt + b * Hkv + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sh_last = (old == (unsigned)NS - 1u);
+    }
+    __syncthreads();
+    if (!sh_last) return;
+    // last arriver: merge the nact active splits of every query head of the group
+    const int na = min(nact, NS);
+    // (m_s, l_s) for s < na (na <= NS; kept in LDS when <= 64, else streamed)
+    float* ml = sm_o[0][0];  // reuse the LDS of sm_o as [grp][2][na] (capacity NW*G*D floats)
+    const int cap = NW * G * D / (2 * G);
+    const bool in_lds = na <= cap;
+    if (in_lds) {
+        for (int idx = threadIdx.x; idx < grp * na; idx += kAttnThreads) {
+            const int h = idx / na, sp = idx - h * na;
+            const float* po = part + (((int64_t)b * Hq + g * grp + h) * NS + sp) * (D + 2);
+            ml[(h * 2) * na + sp] = ld_sc1(po);
+            ml[(h * 2 + 1) * na + sp] = ld_sc1(po + 1);
+        }
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < grp * D; idx += kAttnThreads) {
+        const int h = idx / D, d = idx - h * D;
+        const int hq = g * grp + h;
+        const float* pb = part + ((int64_t)b * Hq + hq) * NS * (D + 2);
+        float mx = -INFINITY;
+        for (int sp = 0; sp < na; ++sp) mx = fmaxf(mx, in_lds ? ml[(h * 2) * na + sp] : ld_sc1(pb + sp * (D + 2)));
+        float ls = 0.f, os = 0.f;
+        int sp = 0;
+        for (; sp + 4 <= na; sp += 4) {
+            float mv[4], lv[4], ov[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                mv[u] = in_lds ? ml[(h * 2) * na + sp + u] : ld_sc1(pb + (sp + u) * (D + 2));
+                lv[u] = in_lds ? ml[(h * 2 + 1) * na + sp + u] : ld_sc1(pb + (sp + u) * (D + 2) + 1);
+                ov[u] = ld_sc1(pb + (sp + u) * (D + 2) + 2 + d);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float a = (mv[u] == -INFINITY) ? 0.f : __expf(mv[u] - mx);
+                ls += lv[u] * a;
+                os += ov[u] * a;
+            }
+        }
+        for (; sp < na; ++sp) {
+            const float mv = in_lds ? ml[(h * 2) * na + sp] : ld_sc1(pb + sp * (D + 2));
+            const float lv = in_lds ? ml[(h * 2 + 1) * na + sp] : ld_sc1(pb + sp * (D + 2) + 1);
+            const float a = (mv == -INFINITY) ? 0.f : __expf(mv - mx);
+            ls += lv * a;
+            os += ld_sc1(pb + sp * (D + 2) + 2 + d) * a;
+        }
+        store_from_f32(out, b * o_sb + (int64_t)hq * o_sh + d, odt, os / ls);
+    }
+    if (threadIdx.x == 0) st_sc1(cnt + b * Hkv + g, 0u);  // re-arm for the next launch
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -215,56 +314,62 @@ __global__ void k_kv_page_copy(uint8_t* __restrict__ pool, const uint8_t* __rest
     }
 }
 
+struct AttnArgs {
+    const void* q; int qdt; int64_t q_sb, q_sh;
+    const void* k; const void* v; int64_t kv_sb, kv_sh, kv_st; float ks, vs;
+    int Hq, Hkv, S; const int32_t* sl; float sm; int NS; unsigned* cnt; float* part;
+    void* out; int odt; int64_t o_sb, o_sh;
+};
+
 template <int D, int G, int KVDT>
-static void launch_attn(dim3 grid, hipStream_t st, const void* q, int qdt, int64_t q_sb, int64_t q_sh, const void* k,
-                        const void* v, int64_t kv_sb, int64_t kv_sh, int64_t kv_st, float ks, float vs, int Hq, int Hkv,
-                        int S, const int32_t* sl, float sm, int NS, int T, float* ws) {
-    hipLaunchKernelGGL((k_attn_split<D, G, KVDT>), grid, dim3(kAttnThreads), 0, st, q, qdt, q_sb, q_sh, k, v, kv_sb,
-                       kv_sh, kv_st, ks, vs, Hq, Hkv, S, sl, sm, NS, T, ws);
+static void launch_attn(dim3 grid, hipStream_t st, const AttnArgs& a) {
+    hipLaunchKernelGGL((k_attn_split<D, G, KVDT>), grid, dim3(kAttnThreads), 0, st, a.q, a.qdt, a.q_sb, a.q_sh, a.k,
+                       a.v, a.kv_sb, a.kv_sh, a.kv_st, a.ks, a.vs, a.Hq, a.Hkv, a.S, a.sl, a.sm, a.NS, a.cnt, a.part,
+                       a.out, a.odt, a.o_sb, a.o_sh);
 }
 
 template <int D, int G>
-static int dispatch_kvdt(int kvdt, dim3 grid, hipStream_t st, const void* q, int qdt, int64_t q_sb, int64_t q_sh,
-                         const void* k, const void* v, int64_t kv_sb, int64_t kv_sh, int64_t kv_st, float ks, float vs,
-                         int Hq, int Hkv, int S, const int32_t* sl, float sm, int NS, int T, float* ws) {
+static int dispatch_kvdt(int kvdt, dim3 grid, hipStream_t st, const AttnArgs& a) {
     switch (kvdt) {
-        case DT_BF16: launch_attn<D, G, DT_BF16>(grid, st, q, qdt, q_sb, q_sh, k, v, kv_sb, kv_sh, kv_st, ks, vs, Hq, Hkv, S, sl, sm, NS, T, ws); return 0;
-        case DT_F16: launch_attn<D, G, DT_F16>(grid, st, q, qdt, q_sb, q_sh, k, v, kv_sb, kv_sh, kv_st, ks, vs, Hq, Hkv, S, sl, sm, NS, T, ws); return 0;
-        case DT_F32: launch_attn<D, G, DT_F32>(grid, st, q, qdt, q_sb, q_sh, k, v, kv_sb, kv_sh, kv_st, ks, vs, Hq, Hkv, S, sl, sm, NS, T, ws); return 0;
-        case DT_I8: launch_attn<D, G, DT_I8>(grid, st, q, qdt, q_sb, q_sh, k, v, kv_sb, kv_sh, kv_st, ks, vs, Hq, Hkv, S, sl, sm, NS, T, ws); return 0;
+        case DT_BF16: launch_attn<D, G, DT_BF16>(grid, st, a); return 0;
+        case DT_F16: launch_attn<D, G, DT_F16>(grid, st, a); return 0;
+        case DT_F32: launch_attn<D, G, DT_F32>(grid, st, a); return 0;
+        case DT_I8: launch_attn<D, G, DT_I8>(grid, st, a); return 0;
     }
     return 1;
 }
 
 template <int D>
-static int dispatch_g(int grp, int kvdt, dim3 grid, hipStream_t st, const void* q, int qdt, int64_t q_sb, int64_t q_sh,
-                      const void* k, const void* v, int64_t kv_sb, int64_t kv_sh, int64_t kv_st, float ks, float vs,
-                      int Hq, int Hkv, int S, const int32_t* sl, float sm, int NS, int T, float* ws) {
-    if (grp == 1) return dispatch_kvdt<D, 1>(kvdt, grid, st, q, qdt, q_sb, q_sh, k, v, kv_sb, kv_sh, kv_st, ks, vs, Hq, Hkv, S, sl, sm, NS, T, ws);
-    if (grp == 2) return dispatch_kvdt<D, 2>(kvdt, grid, st, q, qdt, q_sb, q_sh, k, v, kv_sb, kv_sh, kv_st, ks, vs, Hq, Hkv, S, sl, sm, NS, T, ws);
-    if (grp <= 4) return dispatch_kvdt<D, 4>(kvdt, grid, st, q, qdt, q_sb, q_sh, k, v, kv_sb, kv_sh, kv_st, ks, vs, Hq, Hkv, S, sl, sm, NS, T, ws);
-    if (grp <= 8) return dispatch_kvdt<D, 8>(kvdt, grid, st, q, qdt, q_sb, q_sh, k, v, kv_sb, kv_sh, kv_st, ks, vs, Hq, Hkv, S, sl, sm, NS, T, ws);
+static int dispatch_g(int grp, int kvdt, dim3 grid, hipStream_t st, const AttnArgs& a) {
+    if (grp == 1) return dispatch_kvdt<D, 1>(kvdt, grid, st, a);
+    if (grp == 2) return dispatch_kvdt<D, 2>(kvdt, grid, st, a);
+    if (grp <= 4) return dispatch_kvdt<D, 4>(kvdt, grid, st, a);
+    if (grp <= 8) return dispatch_kvdt<D, 8>(kvdt, grid, st, a);
     return 1;
 }
 
+// ws = [tickets: B*Hkv uint32, 256-B aligned block][partials: B*Hq*NS*(D+2) f32]. The tickets must
+// be zero before the first launch; every launch leaves them zero again.
 int decode_attention_impl(const void* q, int q_dtype, int64_t q_sb, int64_t q_sh, const void* k, const void* v,
                           int kv_dtype, int64_t kv_sb, int64_t kv_sh, int64_t kv_st, float k_scale, float v_scale, int B,
                           int Hq, int Hkv, int D, int S, const int32_t* seq_lens, float sm_scale, void* out,
                           int out_dtype, int64_t o_sb, int64_t o_sh, void* ws, hipStream_t st) {
-    const int NS = attn_splits(B, Hkv, S), T = attn_split_len(B, Hkv, S);
+    WF_REQUIRE(D == 16 || D == 32 || D == 64 || D == 128, "decode_attention: head_dim %d unsupported", D);
+    const int NS = attn_splits(D, S);
+    AttnArgs a{q, q_dtype, q_sb, q_sh, k, v, kv_sb, kv_sh, kv_st, k_scale, v_scale, Hq, Hkv, S, seq_lens, sm_scale, NS,
+               reinterpret_cast<unsigned*>(ws),
+               reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(ws) + attn_cnt_bytes(B, Hkv)), out, out_dtype,
+               o_sb, o_sh};
     const dim3 grid(NS, Hkv, B);
     const int grp = Hq / Hkv;
-    float* wsf = reinterpret_cast<float*>(ws);
     int bad = 1;
     switch (D) {
-        case 16: bad = dispatch_g<16>(grp, kv_dtype, grid, st, q, q_dtype, q_sb, q_sh, k, v, kv_sb, kv_sh, kv_st, k_scale, v_scale, Hq, Hkv, S, seq_lens, sm_scale, NS, T, wsf); break;
-        case 32: bad = dispatch_g<32>(grp, kv_dtype, grid, st, q, q_dtype, q_sb, q_sh, k, v, kv_sb, kv_sh, kv_st, k_scale, v_scale, Hq, Hkv, S, seq_lens, sm_scale, NS, T, wsf); break;
-        case 64: bad = dispatch_g<64>(grp, kv_dtype, grid, st, q, q_dtype, q_sb, q_sh, k, v, kv_sb, kv_sh, kv_st, k_scale, v_scale, Hq, Hkv, S, seq_lens, sm_scale, NS, T, wsf); break;
-        case 128: bad = dispatch_g<128>(grp, kv_dtype, grid, st, q, q_dtype, q_sb, q_sh, k, v, kv_sb, kv_sh, kv_st, k_scale, v_scale, Hq, Hkv, S, seq_lens, sm_scale, NS, T, wsf); break;
+        case 16: bad = dispatch_g<16>(grp, kv_dtype, grid, st, a); break;
+        case 32: bad = dispatch_g<32>(grp, kv_dtype, grid, st, a); break;
+        case 64: bad = dispatch_g<64>(grp, kv_dtype, grid, st, a); break;
+        case 128: bad = dispatch_g<128>(grp, kv_dtype, grid, st, a); break;
     }
     WF_REQUIRE(!bad, "decode_attention: unsupported D=%d / group=%d / kv dtype=%d", D, grp, kv_dtype);
-    hipLaunchKernelGGL(k_attn_combine, dim3(Hq, B), dim3(D < 64 ? 64 : D), 0, st, wsf, Hq, D, NS, out, out_dtype, o_sb,
-                       o_sh);
     return check_launch("decode_attention");
 }
 
@@ -275,8 +380,8 @@ using namespace wf;
 extern "C" {
 
 int64_t wf_decode_attention_ws_bytes(int B, int Hq, int D, int S) {
-    // worst case over Hkv >= 1: the split count grows as Hkv shrinks
-    return (int64_t)B * Hq * attn_splits(B, 1, S) * (D + 2) * (int64_t)sizeof(float);
+    if (D <= 0 || D % 8) return 0;
+    return attn_cnt_bytes(B, Hq) + (int64_t)B * Hq * attn_splits(D, S) * (D + 2) * (int64_t)sizeof(float);
 }
 
 int wf_decode_attention(const void* q, int q_dtype, int64_t q_sb, int64_t q_sh, const void* k, const void* v,
@@ -290,6 +395,7 @@ int wf_decode_attention(const void* q, int q_dtype, int64_t q_sb, int64_t q_sh, 
     WF_REQUIRE(out_dtype == WF_F32 || out_dtype == WF_BF16 || out_dtype == WF_F16, "decode_attention: bad out dtype");
     WF_REQUIRE(kv_st % 8 == 0 && kv_sh % 8 == 0 && kv_sb % 8 == 0, "decode_attention: KV strides must be multiples of 8");
     WF_REQUIRE(aligned16(k) && aligned16(v), "decode_attention: K/V must be 16-byte aligned");
+    WF_HIP(hipMemsetAsync(ws, 0, attn_cnt_bytes(B, Hkv), as_stream(stream)));  // tickets (graph-capturable)
     return decode_attention_impl(q, q_dtype, q_sb, q_sh, k, v, kv_dtype, kv_sb, kv_sh, kv_st, k_scale, v_scale, B, Hq,
                                  Hkv, D, S, seq_lens, sm_scale, out, out_dtype, o_sb, o_sh, ws, as_stream(stream));
 }

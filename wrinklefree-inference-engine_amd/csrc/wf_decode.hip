@@ -53,44 +53,67 @@ struct LayerArgs {
     int64_t kv_b_stride;      // Hkv*S*D
 };
 
-// rms_norm + quantize one activation row into the block's LDS image. Returns via LDS scalars:
-// red_f[0] = float(act scale), red_i[0] = sum(q) (exact).
-template <class F>
-__device__ void prologue_row(const uint16_t* __restrict__ x, const uint16_t* __restrict__ nw, int K, float eps,
-                             int8_t* img, float* red, int* redi, float* out_sf, int* out_asum) {
-    float xv[kMaxVec][4], wv[kMaxVec][4];
+// rms_norm + int8 quantize of one activation row into the block's LDS image, in three phases with
+// one barrier each (per-wave partials in LDS, no reuse hazards):
+//   load:   raw bf16 x and norm weight -> registers (issued before the weight stream)
+//   finish: sum(x^2) -> r = bf16(rsqrt(mean + eps)); y = bf16(bf16(x*r)*w); max|y|; q = rne(y/s)
+// Exact reference float sequence (direct_inference_full.py:181-184, 196; test_bitnet_core.py:139-146).
+struct RowRaw {
+    uint2 x[kMaxVec], w[kMaxVec];
+};
+
+__device__ __forceinline__ void prologue_load(const uint16_t* __restrict__ x, const uint16_t* __restrict__ nw, int K,
+                                              RowRaw& r) {
     const int nvec = K / 4;
-    float ss = 0.f;
 #pragma unroll
     for (int v = 0; v < kMaxVec; ++v) {
         const int e = threadIdx.x + v * blockDim.x;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { xv[v][j] = 0.f; wv[v][j] = 0.f; }
+        r.x[v] = make_uint2(0, 0);
+        r.w[v] = make_uint2(0, 0);
         if (e < nvec) {
-            const uint2 xr = *reinterpret_cast<const uint2*>(x + 4 * e);
-            const uint2 wr = *reinterpret_cast<const uint2*>(nw + 4 * e);
-            xv[v][0] = __uint_as_float(xr.x << 16); xv[v][1] = __uint_as_float(xr.x & 0xffff0000u);
-            xv[v][2] = __uint_as_float(xr.y << 16); xv[v][3] = __uint_as_float(xr.y & 0xffff0000u);
-            wv[v][0] = __uint_as_float(wr.x << 16); wv[v][1] = __uint_as_float(wr.x & 0xffff0000u);
-            wv[v][2] = __uint_as_float(wr.y << 16); wv[v][3] = __uint_as_float(wr.y & 0xffff0000u);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) ss = fmaf(xv[v][j], xv[v][j], ss);
+            r.x[v] = *reinterpret_cast<const uint2*>(x + 4 * e);
+            r.w[v] = *reinterpret_cast<const uint2*>(nw + 4 * e);
         }
     }
-    ss = block_sum(ss, red);
-    // direct_inference_full.py:181-184: (x * rsqrt(mean(x^2) + eps).to(bf16)) * w
-    const float r = rbf(1.0f / sqrtf(ss / (float)K + eps));
+}
+
+template <class F>
+__device__ __forceinline__ void prologue_finish(const RowRaw& r, int K, float eps, int8_t* img, float* red,
+                                                int* redi_row, float* out_sf) {
+    const int nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nvec = K / 4;
+    float xv[kMaxVec][4];
+    float ss = 0.f;
+#pragma unroll
+    for (int v = 0; v < kMaxVec; ++v) {
+        xv[v][0] = __uint_as_float(r.x[v].x << 16); xv[v][1] = __uint_as_float(r.x[v].x & 0xffff0000u);
+        xv[v][2] = __uint_as_float(r.x[v].y << 16); xv[v][3] = __uint_as_float(r.x[v].y & 0xffff0000u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ss = fmaf(xv[v][j], xv[v][j], ss);
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) red[wave] = ss;
+    __syncthreads();
+    ss = red[0];
+    for (int i = 1; i < nw; ++i) ss += red[i];
+    const float rr = rbf(1.0f / sqrtf(ss / (float)K + eps));
     float mx = 0.f;
 #pragma unroll
-    for (int v = 0; v < kMaxVec; ++v)
+    for (int v = 0; v < kMaxVec; ++v) {
+        const float w4[4] = {__uint_as_float(r.w[v].x << 16), __uint_as_float(r.w[v].x & 0xffff0000u),
+                             __uint_as_float(r.w[v].y << 16), __uint_as_float(r.w[v].y & 0xffff0000u)};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            xv[v][j] = rbf(rbf(xv[v][j] * r) * wv[v][j]);
+            xv[v][j] = rbf(rbf(xv[v][j] * rr) * w4[j]);
             mx = fmaxf(mx, fabsf(xv[v][j]));
         }
-    mx = block_max(mx, red);
-    const double s = act_scale_from_max(mx);
-    const float sf = (float)s;
+    }
+    mx = wave_max(mx);
+    if (lane == 0) red[16 + wave] = mx;
+    __syncthreads();
+    mx = red[16];
+    for (int i = 1; i < nw; ++i) mx = fmaxf(mx, red[16 + i]);
+    const float sf = (float)act_scale_from_max(mx);
     int asum = 0;
 #pragma unroll
     for (int v = 0; v < kMaxVec; ++v) {
@@ -106,12 +129,12 @@ __device__ void prologue_row(const uint16_t* __restrict__ x, const uint16_t* __r
             *reinterpret_cast<uint32_t*>(img + F::lds_off(4 * e)) = packed;
         }
     }
-    // TQ pad weights read zero activations
-    for (int k = K + 4 * threadIdx.x; k < F::k_pad(K); k += 4 * blockDim.x)
+    for (int k = K + 4 * threadIdx.x; k < F::k_pad(K); k += 4 * blockDim.x)  // TQ pad weights see zeros
         *reinterpret_cast<uint32_t*>(img + F::lds_off(k)) = 0u;
-    asum = block_sum_i(asum, redi);
+    asum = wave_sum_i(asum);
+    if (lane == 0) redi_row[wave] = asum;
     *out_sf = sf;
-    *out_asum = asum;
+    // the caller's __syncthreads() publishes the image and the per-wave sums
 }
 
 // Reference correction (direct_inference_full.py:201-208) for one output:
@@ -125,10 +148,9 @@ __device__ __forceinline__ float corrected(int S, float ws, int asum, float sf) 
 template <class F, int MODE, int MB>
 __global__ __launch_bounds__(256) void k_fused_gemv(LayerArgs a) {
     extern __shared__ __attribute__((aligned(16))) int8_t smem[];
-    __shared__ float red[16];
-    __shared__ int redi[16];
+    __shared__ float red[32];
+    __shared__ int redi[MB][4];
     __shared__ float s_sf[MB];
-    __shared__ int s_asum[MB];
     __shared__ float s_out[MB][16];
 
     const int K = a.K, N = a.N;
@@ -139,7 +161,10 @@ __global__ __launch_bounds__(256) void k_fused_gemv(LayerArgs a) {
     const int row = blockIdx.x * kRowsPerBlockFused + lrow;
     const int C = F::chunks(K);
 
-    // Issue the first weight loads before the prologue so HBM latency overlaps the norm.
+    // activation row loads first, then the weight stream: vmcnt retires loads in order, so the
+    // prologue only waits for its own (L2-near) data while the weights are in flight.
+    RowRaw raw;
+    prologue_load(a.x + (int64_t)b0 * a.x_stride, a.norm_w, K, raw);
     const uint8_t* wr = a.w + (int64_t)min(row, N - 1) * F::row_bytes(K) + sub * 16;
     uint4 wpre[kPrefetch];
 #pragma unroll
@@ -147,16 +172,17 @@ __global__ __launch_bounds__(256) void k_fused_gemv(LayerArgs a) {
         const int c = 16 * u + sub;
         wpre[u] = (c < C) ? ldg_nt(wr + (int64_t)(16 * u) * 16) : make_uint4(0, 0, 0, 0);
     }
-
 #pragma unroll 1
     for (int m = 0; m < MB; ++m) {
+        if (m > 0) prologue_load(a.x + (int64_t)(b0 + m) * a.x_stride, a.norm_w, K, raw);
         float sf;
-        int asum;
-        prologue_row<F>(a.x + (int64_t)(b0 + m) * a.x_stride, a.norm_w, K, a.eps, smem + m * img, red, redi, &sf,
-                        &asum);
-        if (threadIdx.x == 0) { s_sf[m] = sf; s_asum[m] = asum; }
+        prologue_finish<F>(raw, K, a.eps, smem + m * img, red, redi[m], &sf);
+        if (threadIdx.x == 0) s_sf[m] = sf;
     }
     __syncthreads();
+    int s_asum[MB];
+#pragma unroll
+    for (int m = 0; m < MB; ++m) s_asum[m] = redi[m][0] + redi[m][1] + redi[m][2] + redi[m][3];
 
     int acc[MB];
 #pragma unroll
@@ -579,6 +605,10 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_ALLOC(m->am_val, sizeof(float) * B * m->lm_blocks);
     WF_ALLOC(m->am_idx, sizeof(int32_t) * B * m->lm_blocks);
 #undef WF_ALLOC
+    // attention tickets must start at zero (every launch re-arms them)
+    if ((e = hipMemset(m->attn_ws, 0, (size_t)wf_decode_attention_ws_bytes(B, d.n_heads, d.head_dim, d.max_seq))) !=
+        hipSuccess)
+        return fail(e);
     if ((e = hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking)) != hipSuccess) return fail(e);
     *out = m;
     return WF_OK;
