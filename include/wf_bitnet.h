@@ -128,6 +128,8 @@ typedef struct {
     uint16_t* logits;             /* [batch, vocab] bf16                                           */
     uint16_t* k_cache;            /* [layers, batch, n_kv_heads, max_seq, head_dim] bf16           */
     uint16_t* v_cache;
+    int debug_flags;              /* 0; ablation switches for timing studies (1: no norm/quantize
+                                     prologue, 2: no weight loads) -- results are then meaningless */
 } wf_model_desc;
 
 typedef struct wf_model wf_model;
@@ -140,15 +142,13 @@ int wf_model_step(wf_model* m, void* stream);
 int wf_model_graph_launch(wf_model* m, void* stream);
 /* Launch one op of the step (profiling / per-kernel timing). Ops, in step order: */
 enum {
-    WF_OP_EMBED = 0,      /* h = embed[token]                                   (layer ignored) */
-    WF_OP_QKV = 1,        /* fused norm + quantize + q|k|v GEMV + RoPE + cache write           */
-    WF_OP_ATTN = 2,       /* split-K GQA decode attention (+ combine)                          */
-    WF_OP_O = 3,          /* fused attn_sub_norm + o_proj + residual                           */
-    WF_OP_GATE_UP = 4,    /* fused post_attention_layernorm + gate|up + relu^2 * up            */
-    WF_OP_DOWN = 5,       /* fused ffn_sub_norm + down_proj + residual                         */
-    WF_OP_FINAL_NORM = 6, /*                                                    (layer ignored) */
-    WF_OP_LM_HEAD = 7,    /* tied bf16 LM head + per-block argmax               (layer ignored) */
-    WF_OP_ARGMAX = 8      /* greedy token + position advance                    (layer ignored) */
+    WF_OP_EMBED = 0,      /* h = embed[token] + layer-0 input norm / quantize  (layer ignored) */
+    WF_OP_QKV = 1,        /* q|k|v ternary GEMV + correction + RoPE + cache write              */
+    WF_OP_ATTN = 2,       /* split-K GQA decode attention; last block: attn_sub_norm + quantize */
+    WF_OP_O = 3,          /* o_proj + residual; last block: post_attention_layernorm + quantize */
+    WF_OP_GATE_UP = 4,    /* gate|up + relu^2 * up; last block: ffn_sub_norm + quantize         */
+    WF_OP_DOWN = 5,       /* down_proj + residual; last block: next input norm or final norm    */
+    WF_OP_LM_HEAD = 6     /* tied bf16 LM head + greedy argmax + position advance (layer ignored) */
 };
 int wf_model_launch_op(wf_model* m, int layer, int op, void* stream);
 

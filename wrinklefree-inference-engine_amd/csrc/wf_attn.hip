@@ -9,16 +9,19 @@
 
 #include "wf_common.h"
 #include "wf_device.h"
+#include "wf_norm.h"
 
 namespace wf {
 
 constexpr int kAttnThreads = 256;
 constexpr int kAttnU = 4;  // key positions per lane group per split (all loads issued up front)
+constexpr int kAttnMaxSplits = 256;  // splits per sequence (S <= 256 * split length)
 
 // keys per split: kAttnU positions x (256 / (D/8)) lane groups  (D = 128 -> 64)
 static inline int attn_split_len(int D) { return kAttnU * (kAttnThreads / (D / 8)); }
 static inline int attn_splits(int D, int S) { return (S + attn_split_len(D) - 1) / attn_split_len(D); }
 static inline int64_t attn_cnt_bytes(int B, int Hkv) { return (((int64_t)B * Hkv * 4) + 255) / 256 * 256; }
+static inline int64_t attn_rec_floats(int D) { return D + 4; }
 
 // Load 8 consecutive KV elements as f32.
 template <int KVDT>
@@ -83,10 +86,30 @@ struct KVRaw {
     }
 };
 
-template <class T>
-__device__ __forceinline__ void st_sc1(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-template <class T>
-__device__ __forceinline__ T ld_sc1(const T* p) { return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// Optional fused follow-up (decode step): when every kv group of row b has written its heads
+// (sc1 stores), the last one normalises the full attention row (attn_sub_norm) and quantises it
+// for the O projection (wf_norm.h). ticket2 == nullptr disables it (generic C-ABI use).
+struct AttnNext {
+    unsigned* ticket2;
+    const uint16_t* nw;
+    float eps;
+    int8_t* q8;
+    int64_t q8_stride;
+    float* sf;
+    int* asum;
+};
+
+// store 4 consecutive outputs (write-through bf16x4 when the fused follow-up reads them)
+__device__ __forceinline__ void store_out4(void* out, int64_t off, int odt, const float (&v)[4], bool sc1) {
+    if (sc1) {  // odt == BF16 (checked on the host)
+        const uint64_t pk = (uint64_t)f2bf(v[0]) | ((uint64_t)f2bf(v[1]) << 16) | ((uint64_t)f2bf(v[2]) << 32) |
+                            ((uint64_t)f2bf(v[3]) << 48);
+        st_sc1(reinterpret_cast<uint64_t*>(reinterpret_cast<uint16_t*>(out) + off), pk);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) store_from_f32(out, off + j, odt, v[j]);
+    }
+}
 
 // One block = one (sequence b, kv head g, split s of T keys). Lane group `gid` (D/8 lanes, 8 head
 // dims per lane) owns keys t0 + gid + NG*u, u < kAttnU, loads all of them first, then does a local
@@ -100,7 +123,7 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
     const void* __restrict__ q, int qdt, int64_t q_sb, int64_t q_sh, const void* __restrict__ K,
     const void* __restrict__ V, int64_t kv_sb, int64_t kv_sh, int64_t kv_st, float k_scale, float v_scale, int Hq,
     int Hkv, int S, const int32_t* __restrict__ seq_lens, float sm_scale, int NS, unsigned* __restrict__ cnt,
-    float* __restrict__ part, void* __restrict__ out, int odt, int64_t o_sb, int64_t o_sh) {
+    float* __restrict__ part, void* __restrict__ out, int odt, int64_t o_sb, int64_t o_sh, AttnNext nx) {
     constexpr int LP = D / 8;                // lanes per key position
     constexpr int NG = kAttnThreads / LP;    // lane groups per block
     constexpr int NW = kAttnThreads / 64;
@@ -208,30 +231,47 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
         }
     }
     __syncthreads();
-    // block result per (h, d); thread -> idx
-    for (int idx = threadIdx.x; idx < grp * D; idx += kAttnThreads) {
-        const int h = idx / D, d = idx - h * D;
+    // block result per (h, 4 consecutive d)
+    constexpr int D4 = D / 4;
+    const int rec = D + 4;  // partial record: m, l, 0, 0, o[D]
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(part, (short)0, 0x7fffffff, 0x00020000);
+    for (int idx = threadIdx.x; idx < grp * D4; idx += kAttnThreads) {
+        const int h = idx / D4, d = (idx - h * D4) * 4;
         float mx = -INFINITY;
 #pragma unroll
         for (int w = 0; w < NW; ++w) mx = fmaxf(mx, sm_m[w][h]);
-        float ls = 0.f, os = 0.f;
+        float ls = 0.f;
+        float os[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
             const float a = (sm_m[w][h] == -INFINITY) ? 0.f : __expf(sm_m[w][h] - mx);
             ls += sm_l[w][h] * a;
-            os += sm_o[w][h][d] * a;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) os[j] += sm_o[w][h][d + j] * a;
         }
         const int hq = g * grp + h;
         if (NS == 1) {
-            store_from_f32(out, b * o_sb + (int64_t)hq * o_sh + d, odt, os / ls);
+            const float ov[4] = {os[0] / ls, os[1] / ls, os[2] / ls, os[3] / ls};
+            store_out4(out, b * o_sb + (int64_t)hq * o_sh + d, odt, ov, nx.ticket2 != nullptr);
         } else if (t0 < Sb) {
-            float* po = part + (((int64_t)b * Hq + hq) * NS + s) * (D + 2);
-            st_sc1(po + 2 + d, os);
-            if (d == 0) { st_sc1(po, mx); st_sc1(po + 1, ls); }
+            const int off = (int)((((int64_t)b * Hq + hq) * NS + s) * rec) * 4;  // bytes
+            const float4 ov = make_float4(os[0], os[1], os[2], os[3]);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ov), rs, off + 16 + 4 * d, 0, 16 /*sc1*/);
+            if (d == 0)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_float4(mx, ls, 0.f, 0.f)), rs,
+                                                       off, 0, 16);
         }
     }
-    if (NS == 1) return;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __shared__ float red_n[48];
+    if (NS == 1) {
+        if (nx.ticket2 && ticket_arrive(nx.ticket2 + b, Hkv, &sh_last)) {
+            NormOut no{nx.q8 + (int64_t)b * nx.q8_stride, nx.sf + b, nx.asum + b, nullptr};
+            norm_quant_row<true>(reinterpret_cast<const uint16_t*>(out) + b * o_sb, nx.nw, Hq * D, nx.eps, no, red_n);
+            ticket_rearm(nx.ticket2 + b);
+        }
+        return;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned old = __hip_atomic_fetch_add(cnt + b * Hkv + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -239,54 +279,86 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
     }
     __syncthreads();
     if (!sh_last) return;
-    // last arriver: merge the nact active splits of every query head of the group
-    const int na = min(nact, NS);
-    // (m_s, l_s) for s < na (na <= NS; kept in LDS when <= 64, else streamed)
-    float* ml = sm_o[0][0];  // reuse the LDS of sm_o as [grp][2][na] (capacity NW*G*D floats)
-    const int cap = NW * G * D / (2 * G);
-    const bool in_lds = na <= cap;
-    if (in_lds) {
-        for (int idx = threadIdx.x; idx < grp * na; idx += kAttnThreads) {
-            const int h = idx / na, sp = idx - h * na;
-            const float* po = part + (((int64_t)b * Hq + g * grp + h) * NS + sp) * (D + 2);
-            ml[(h * 2) * na + sp] = ld_sc1(po);
-            ml[(h * 2 + 1) * na + sp] = ld_sc1(po + 1);
-        }
+    // ---- last arriver: merge the active splits of every query head of this kv group ----
+    const int na = min(nact, NS);  // <= kAttnMaxSplits (host check)
+    __shared__ float sm_ml[G][kAttnMaxSplits][2];
+    __shared__ float sm_ML[G][2];
+    for (int idx = threadIdx.x; idx < grp * na; idx += kAttnThreads) {  // round 1: (m, l) records
+        const int h = idx / na, sp = idx - h * na;
+        const int off = (int)((((int64_t)b * Hq + g * grp + h) * NS + sp) * rec) * 4;
+        const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
+        sm_ml[h][sp][0] = v.x;
+        sm_ml[h][sp][1] = v.y;
     }
     __syncthreads();
-    for (int idx = threadIdx.x; idx < grp * D; idx += kAttnThreads) {
-        const int h = idx / D, d = idx - h * D;
-        const int hq = g * grp + h;
-        const float* pb = part + ((int64_t)b * Hq + hq) * NS * (D + 2);
-        float mx = -INFINITY;
-        for (int sp = 0; sp < na; ++sp) mx = fmaxf(mx, in_lds ? ml[(h * 2) * na + sp] : ld_sc1(pb + sp * (D + 2)));
-        float ls = 0.f, os = 0.f;
-        int sp = 0;
-        for (; sp + 4 <= na; sp += 4) {
-            float mv[4], lv[4], ov[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                mv[u] = in_lds ? ml[(h * 2) * na + sp + u] : ld_sc1(pb + (sp + u) * (D + 2));
-                lv[u] = in_lds ? ml[(h * 2 + 1) * na + sp + u] : ld_sc1(pb + (sp + u) * (D + 2) + 1);
-                ov[u] = ld_sc1(pb + (sp + u) * (D + 2) + 2 + d);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const float a = (mv[u] == -INFINITY) ? 0.f : __expf(mv[u] - mx);
-                ls += lv[u] * a;
-                os += ov[u] * a;
-            }
+    if (threadIdx.x < grp) {
+        const int h = threadIdx.x;
+        float M = -INFINITY;
+        for (int sp = 0; sp < na; ++sp) M = fmaxf(M, sm_ml[h][sp][0]);
+        float Ls = 0.f;
+        for (int sp = 0; sp < na; ++sp) {
+            const float w = (sm_ml[h][sp][0] == -INFINITY) ? 0.f : __expf(sm_ml[h][sp][0] - M);
+            sm_ml[h][sp][0] = w;
+            Ls += w * sm_ml[h][sp][1];
         }
-        for (; sp < na; ++sp) {
-            const float mv = in_lds ? ml[(h * 2) * na + sp] : ld_sc1(pb + sp * (D + 2));
-            const float lv = in_lds ? ml[(h * 2 + 1) * na + sp] : ld_sc1(pb + sp * (D + 2) + 1);
-            const float a = (mv == -INFINITY) ? 0.f : __expf(mv - mx);
-            ls += lv * a;
-            os += ld_sc1(pb + sp * (D + 2) + 2 + d) * a;
-        }
-        store_from_f32(out, b * o_sb + (int64_t)hq * o_sh + d, odt, os / ls);
+        sm_ML[h][0] = M;
+        sm_ML[h][1] = Ls;
     }
-    if (threadIdx.x == 0) st_sc1(cnt + b * Hkv + g, 0u);  // re-arm for the next launch
+    __syncthreads();
+    // round 2: weighted sum of the o partials; threads = (h, d4) x nsub split-subsets
+    const int nout = grp * D4;
+    const int nsub = max(1, kAttnThreads / nout);
+    float* red = sm_o[0][0];  // [nsub][nout][4] floats <= NW*G*D
+    if (threadIdx.x < nout * nsub) {
+        const int oi = threadIdx.x % nout, sb = threadIdx.x / nout;
+        const int h = oi / D4, d = (oi - h * D4) * 4;
+        const int64_t rbase = (((int64_t)b * Hq + g * grp + h) * NS) * rec;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int sp0 = sb; sp0 < na; sp0 += 8 * nsub) {
+            float4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int sp = sp0 + u * nsub;
+                v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (sp < na)
+                    v[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                          rs, (int)((rbase + (int64_t)sp * rec) * 4) + 16 + 4 * d, 0, 16));
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int sp = sp0 + u * nsub;
+                if (sp < na) {
+                    const float w = sm_ml[h][sp][0];
+                    acc[0] = fmaf(w, v[u].x, acc[0]);
+                    acc[1] = fmaf(w, v[u].y, acc[1]);
+                    acc[2] = fmaf(w, v[u].z, acc[2]);
+                    acc[3] = fmaf(w, v[u].w, acc[3]);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[(sb * nout + oi) * 4 + j] = acc[j];
+    }
+    __syncthreads();
+    for (int oi = threadIdx.x; oi < nout; oi += kAttnThreads) {
+        const int h = oi / D4, d = (oi - h * D4) * 4;
+        const int hq = g * grp + h;
+        const float inv = 1.0f / sm_ML[h][1];
+        float ov[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float t = 0.f;
+            for (int sb = 0; sb < nsub; ++sb) t += red[(sb * nout + oi) * 4 + j];
+            ov[j] = t * inv;
+        }
+        store_out4(out, b * o_sb + (int64_t)hq * o_sh + d, odt, ov, nx.ticket2 != nullptr);
+    }
+    if (threadIdx.x == 0) st_sc1(cnt + b * Hkv + g, 0u);  // re-arm the ticket for the next launch
+    if (nx.ticket2 && ticket_arrive(nx.ticket2 + b, Hkv, &sh_last)) {
+        NormOut no{nx.q8 + (int64_t)b * nx.q8_stride, nx.sf + b, nx.asum + b, nullptr};
+        norm_quant_row<true>(reinterpret_cast<const uint16_t*>(out) + b * o_sb, nx.nw, Hq * D, nx.eps, no, red_n);
+        ticket_rearm(nx.ticket2 + b);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -314,18 +386,20 @@ __global__ void k_kv_page_copy(uint8_t* __restrict__ pool, const uint8_t* __rest
     }
 }
 
+
 struct AttnArgs {
     const void* q; int qdt; int64_t q_sb, q_sh;
     const void* k; const void* v; int64_t kv_sb, kv_sh, kv_st; float ks, vs;
     int Hq, Hkv, S; const int32_t* sl; float sm; int NS; unsigned* cnt; float* part;
     void* out; int odt; int64_t o_sb, o_sh;
+    AttnNext nx;
 };
 
 template <int D, int G, int KVDT>
 static void launch_attn(dim3 grid, hipStream_t st, const AttnArgs& a) {
     hipLaunchKernelGGL((k_attn_split<D, G, KVDT>), grid, dim3(kAttnThreads), 0, st, a.q, a.qdt, a.q_sb, a.q_sh, a.k,
                        a.v, a.kv_sb, a.kv_sh, a.kv_st, a.ks, a.vs, a.Hq, a.Hkv, a.S, a.sl, a.sm, a.NS, a.cnt, a.part,
-                       a.out, a.odt, a.o_sb, a.o_sh);
+                       a.out, a.odt, a.o_sb, a.o_sh, a.nx);
 }
 
 template <int D, int G>
@@ -353,13 +427,21 @@ static int dispatch_g(int grp, int kvdt, dim3 grid, hipStream_t st, const AttnAr
 int decode_attention_impl(const void* q, int q_dtype, int64_t q_sb, int64_t q_sh, const void* k, const void* v,
                           int kv_dtype, int64_t kv_sb, int64_t kv_sh, int64_t kv_st, float k_scale, float v_scale, int B,
                           int Hq, int Hkv, int D, int S, const int32_t* seq_lens, float sm_scale, void* out,
-                          int out_dtype, int64_t o_sb, int64_t o_sh, void* ws, hipStream_t st) {
+                          int out_dtype, int64_t o_sb, int64_t o_sh, void* ws, hipStream_t st,
+                          const AttnNext* next = nullptr) {
     WF_REQUIRE(D == 16 || D == 32 || D == 64 || D == 128, "decode_attention: head_dim %d unsupported", D);
     const int NS = attn_splits(D, S);
+    WF_REQUIRE(NS <= kAttnMaxSplits, "decode_attention: S=%d exceeds %d keys", S, kAttnMaxSplits * attn_split_len(D));
+    WF_REQUIRE((int64_t)B * Hq * NS * attn_rec_floats(D) * 4 < 0x7fffffff, "decode_attention: workspace > 2 GiB");
     AttnArgs a{q, q_dtype, q_sb, q_sh, k, v, kv_sb, kv_sh, kv_st, k_scale, v_scale, Hq, Hkv, S, seq_lens, sm_scale, NS,
                reinterpret_cast<unsigned*>(ws),
                reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(ws) + attn_cnt_bytes(B, Hkv)), out, out_dtype,
-               o_sb, o_sh};
+               o_sb, o_sh, AttnNext{}};
+    if (next) {
+        WF_REQUIRE(out_dtype == WF_BF16 && o_sh == D && o_sb == (int64_t)Hq * D && Hq * D <= 8192,
+                   "decode_attention: fused follow-up needs a contiguous bf16 [B, Hq*D] output");
+        a.nx = *next;
+    }
     const dim3 grid(NS, Hkv, B);
     const int grp = Hq / Hkv;
     int bad = 1;
@@ -381,7 +463,7 @@ extern "C" {
 
 int64_t wf_decode_attention_ws_bytes(int B, int Hq, int D, int S) {
     if (D <= 0 || D % 8) return 0;
-    return attn_cnt_bytes(B, Hq) + (int64_t)B * Hq * attn_splits(D, S) * (D + 2) * (int64_t)sizeof(float);
+    return attn_cnt_bytes(B, Hq) + (int64_t)B * Hq * attn_splits(D, S) * attn_rec_floats(D) * (int64_t)sizeof(float);
 }
 
 int wf_decode_attention(const void* q, int q_dtype, int64_t q_sb, int64_t q_sh, const void* k, const void* v,

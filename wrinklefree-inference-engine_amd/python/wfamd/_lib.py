@@ -17,8 +17,7 @@ LIB_PATH = Path(os.environ.get("WF_BITNET_LIB", PKG_ROOT / "lib" / "libwfbitnet.
 WF_OK, WF_EINVAL, WF_EHIP, WF_ENOTSUP = 0, 1, 2, 3
 WF_F32, WF_BF16, WF_F16, WF_I8, WF_U8 = 0, 1, 2, 3, 4
 WF_FMT_I2S, WF_FMT_TQ = 0, 1
-(WF_OP_EMBED, WF_OP_QKV, WF_OP_ATTN, WF_OP_O, WF_OP_GATE_UP, WF_OP_DOWN, WF_OP_FINAL_NORM, WF_OP_LM_HEAD,
- WF_OP_ARGMAX) = range(9)
+(WF_OP_EMBED, WF_OP_QKV, WF_OP_ATTN, WF_OP_O, WF_OP_GATE_UP, WF_OP_DOWN, WF_OP_LM_HEAD) = range(7)
 
 vp, i32, i64, f32 = C.c_void_p, C.c_int, C.c_int64, C.c_float
 
@@ -61,7 +60,8 @@ class WFModelDesc(C.Structure):
                [("eps", C.c_float), ("wfmt", C.c_int)] + \
                [(n, C.c_void_p) for n in ("embed", "final_norm", "rope_cos", "rope_sin", "ln_in", "ln_post",
                                           "attn_sub", "ffn_sub", "w_qkv", "w_o", "w_gu", "w_d", "wscale",
-                                          "tokens", "positions", "logits", "k_cache", "v_cache")]
+                                          "tokens", "positions", "logits", "k_cache", "v_cache")] + \
+               [("debug_flags", C.c_int)]
 
 
 class KernelError(RuntimeError):

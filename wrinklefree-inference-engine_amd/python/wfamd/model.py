@@ -164,7 +164,7 @@ class BitNetDecoder:
     """Owns the device layout, the caller-side state tensors and the wf_model handle."""
 
     def __init__(self, cfg: BitNetConfig, weights: Dict[str, torch.Tensor], batch: int = 1,
-                 wfmt: int = WF_FMT_TQ, device="cuda"):
+                 wfmt: int = WF_FMT_TQ, device="cuda", debug_flags: int = 0):
         self.cfg, self.batch, self.wfmt = cfg, batch, wfmt
         self.dev = torch.device(device)
         lay = build_device_layout(cfg, weights, wfmt)
@@ -194,6 +194,7 @@ class BitNetDecoder:
         d.wscale = self.wscale.data_ptr()
         d.tokens, d.positions, d.logits = self.tokens.data_ptr(), self.positions.data_ptr(), self.logits.data_ptr()
         d.k_cache, d.v_cache = self.k_cache.data_ptr(), self.v_cache.data_ptr()
+        d.debug_flags = int(debug_flags)
         self._desc = d
         h = C.c_void_p()
         call("wf_model_create", C.addressof(d), C.addressof(h))
