@@ -126,18 +126,16 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
     float* __restrict__ part, void* __restrict__ out, int odt, int64_t o_sb, int64_t o_sh, AttnNext nx) {
     constexpr int LP = D / 8;                // lanes per key position
     constexpr int NG = kAttnThreads / LP;    // lane groups per block
-    constexpr int NW = kAttnThreads / 64;
     constexpr int T = kAttnU * NG;
     const int s = blockIdx.x, g = blockIdx.y, b = blockIdx.z;
     const int grp = Hq / Hkv;
-    const int wave = threadIdx.x >> 6;
     const int gid = threadIdx.x / LP, li = threadIdx.x % LP;
     const int Sb = seq_lens ? min(seq_lens[b], S) : S;
     const int t0 = s * T;
     const int nact = (Sb + T - 1) / T;       // splits that hold keys for this sequence
 
-    __shared__ float sm_m[NW][G], sm_l[NW][G];
-    __shared__ float sm_o[NW][G][D];
+    __shared__ float sm_m[NG][G], sm_l[NG][G];
+    __shared__ __attribute__((aligned(16))) float sm_o[NG][G][D];
     __shared__ int sh_last;
 
     float m[G], l[G], o[G][8];
@@ -207,28 +205,15 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
             }
         }
     }
-    // merge the GW lane groups of a wave (same li, different gid)
+    // every lane group parks (m, l, o) in LDS; the block merges them per (h, d) below
+    if (li == 0) {
 #pragma unroll
-    for (int off = LP; off < 64; off <<= 1) {
-#pragma unroll
-        for (int h = 0; h < G; ++h) {
-            const float mo = __shfl_xor(m[h], off, 64), lo = __shfl_xor(l[h], off, 64);
-            const float mn = fmaxf(m[h], mo);
-            const float a = (m[h] == -INFINITY) ? 0.f : __expf(m[h] - mn);
-            const float c = (mo == -INFINITY) ? 0.f : __expf(mo - mn);
-            l[h] = l[h] * a + lo * c;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) o[h][j] = o[h][j] * a + __shfl_xor(o[h][j], off, 64) * c;
-            m[h] = mn;
-        }
+        for (int h = 0; h < G; ++h) { sm_m[gid][h] = m[h]; sm_l[gid][h] = l[h]; }
     }
-    if ((threadIdx.x & 63) < LP) {
 #pragma unroll
-        for (int h = 0; h < G; ++h) {
-            if (li == 0) { sm_m[wave][h] = m[h]; sm_l[wave][h] = l[h]; }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) sm_o[wave][h][li * 8 + j] = o[h][j];
-        }
+    for (int h = 0; h < G; ++h) {
+        *reinterpret_cast<float4*>(&sm_o[gid][h][li * 8]) = make_float4(o[h][0], o[h][1], o[h][2], o[h][3]);
+        *reinterpret_cast<float4*>(&sm_o[gid][h][li * 8 + 4]) = make_float4(o[h][4], o[h][5], o[h][6], o[h][7]);
     }
     __syncthreads();
     // block result per (h, 4 consecutive d)
@@ -239,15 +224,15 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
         const int h = idx / D4, d = (idx - h * D4) * 4;
         float mx = -INFINITY;
 #pragma unroll
-        for (int w = 0; w < NW; ++w) mx = fmaxf(mx, sm_m[w][h]);
+        for (int w = 0; w < NG; ++w) mx = fmaxf(mx, sm_m[w][h]);
         float ls = 0.f;
         float os[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int w = 0; w < NW; ++w) {
+        for (int w = 0; w < NG; ++w) {
             const float a = (sm_m[w][h] == -INFINITY) ? 0.f : __expf(sm_m[w][h] - mx);
             ls += sm_l[w][h] * a;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) os[j] += sm_o[w][h][d + j] * a;
+            const float4 ov = *reinterpret_cast<const float4*>(&sm_o[w][h][d]);
+            os[0] += ov.x * a; os[1] += ov.y * a; os[2] += ov.z * a; os[3] += ov.w * a;
         }
         const int hq = g * grp + h;
         if (NS == 1) {
@@ -264,10 +249,10 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
     }
     __shared__ float red_n[48];
     if (NS == 1) {
-        if (nx.ticket2 && ticket_arrive(nx.ticket2 + b, Hkv, &sh_last)) {
+        if (nx.ticket2 && ticket_arrive(nx.ticket2 + b * kTicketWords, Hkv, g, &sh_last)) {
             NormOut no{nx.q8 + (int64_t)b * nx.q8_stride, nx.sf + b, nx.asum + b, nullptr};
             norm_quant_row<true>(reinterpret_cast<const uint16_t*>(out) + b * o_sb, nx.nw, Hq * D, nx.eps, no, red_n);
-            ticket_rearm(nx.ticket2 + b);
+            ticket_rearm(nx.ticket2 + b * kTicketWords);
         }
         return;
     }
@@ -308,16 +293,16 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
     // round 2: weighted sum of the o partials; threads = (h, d4) x nsub split-subsets
     const int nout = grp * D4;
     const int nsub = max(1, kAttnThreads / nout);
-    float* red = sm_o[0][0];  // [nsub][nout][4] floats <= NW*G*D
+    float* red = sm_o[0][0];  // [nsub][nout][4] floats <= NG*G*D
     if (threadIdx.x < nout * nsub) {
         const int oi = threadIdx.x % nout, sb = threadIdx.x / nout;
         const int h = oi / D4, d = (oi - h * D4) * 4;
         const int64_t rbase = (((int64_t)b * Hq + g * grp + h) * NS) * rec;
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int sp0 = sb; sp0 < na; sp0 += 8 * nsub) {
-            float4 v[8];
+        for (int sp0 = sb; sp0 < na; sp0 += 16 * nsub) {
+            float4 v[16];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+            for (int u = 0; u < 16; ++u) {
                 const int sp = sp0 + u * nsub;
                 v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (sp < na)
@@ -325,7 +310,7 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
                                                           rs, (int)((rbase + (int64_t)sp * rec) * 4) + 16 + 4 * d, 0, 16));
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+            for (int u = 0; u < 16; ++u) {
                 const int sp = sp0 + u * nsub;
                 if (sp < na) {
                     const float w = sm_ml[h][sp][0];
@@ -354,10 +339,10 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
         store_out4(out, b * o_sb + (int64_t)hq * o_sh + d, odt, ov, nx.ticket2 != nullptr);
     }
     if (threadIdx.x == 0) st_sc1(cnt + b * Hkv + g, 0u);  // re-arm the ticket for the next launch
-    if (nx.ticket2 && ticket_arrive(nx.ticket2 + b, Hkv, &sh_last)) {
+    if (nx.ticket2 && ticket_arrive(nx.ticket2 + b * kTicketWords, Hkv, g, &sh_last)) {
         NormOut no{nx.q8 + (int64_t)b * nx.q8_stride, nx.sf + b, nx.asum + b, nullptr};
         norm_quant_row<true>(reinterpret_cast<const uint16_t*>(out) + b * o_sb, nx.nw, Hq * D, nx.eps, no, red_n);
-        ticket_rearm(nx.ticket2 + b);
+        ticket_rearm(nx.ticket2 + b * kTicketWords);
     }
 }
 

@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
             const int64_t byte_off = ((int64_t)(b0 + m) * a.out_stride + first) * 2;
             if (first < a.out_stride) st16_sc1(make_rsrc(a.out), (int)byte_off, make_uint4(pk[0], pk[1], pk[2], pk[3]));
         }
-        if (!ticket_arrive(a.ticket, gridDim.x * gridDim.y, &sh_flag)) return;
+        if (!ticket_arrive(a.ticket, gridDim.x * gridDim.y, linear_block_id(), &sh_flag)) return;
         // last block of the launch: rms_norm + quantize (or final norm) of every row for the next op
         const int Kn = (int)a.out_stride;
         for (int b = 0; b < a.B; ++b) {
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(256) void k_lm_head(const uint16_t* __restrict__ E,
         const uint64_t pk = ((uint64_t)(uint32_t)(blockIdx.x * 16 + bi) << 32) | __float_as_uint(best);
         st_sc1(reinterpret_cast<uint64_t*>(part) + (int64_t)(b0 + m) * nblk + blockIdx.x, pk);
     }
-    if (!ticket_arrive(ticket, gridDim.x * gridDim.y, &sh_flag)) return;
+    if (!ticket_arrive(ticket, gridDim.x * gridDim.y, linear_block_id(), &sh_flag)) return;
     for (int b = 0; b < B; ++b) {
         float best = -INFINITY;
         int bi = 0x7fffffff;
@@ -418,7 +418,8 @@ __global__ __launch_bounds__(256) void k_lm_head(const uint16_t* __restrict__ E,
 // =============================================================================================
 // Model runtime
 // =============================================================================================
-enum { TK_O = 0, TK_GU = 1, TK_DN = 2, TK_LM = 3, TK_ATTN2 = 8 };  // ticket slots (ATTN2: + batch row)
+// ticket slots, kTicketWords words each (ATTN2: one per batch row)
+enum { TK_O = 0, TK_GU = 1, TK_DN = 2, TK_LM = 3, TK_ATTN2 = 4 };
 
 struct wf_model {
     wf_model_desc d;
@@ -512,7 +513,7 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             a.out = m->qbuf; a.out_stride = (int64_t)d.n_heads * D;
             return launch_gemv_fmt<MODE_QKV, 16>(d.wfmt, a, st);
         case WF_OP_ATTN: {
-            AttnNext nx{m->tickets + TK_ATTN2, d.attn_sub + (int64_t)l * H, d.eps, m->q8, m->q8_stride, m->act_sf,
+            AttnNext nx{m->tickets + TK_ATTN2 * kTicketWords, d.attn_sub + (int64_t)l * H, d.eps, m->q8, m->q8_stride, m->act_sf,
                         m->act_sum};
             return decode_attention_impl(m->qbuf, WF_BF16, (int64_t)d.n_heads * D, D, a.kc, a.vc, WF_BF16,
                                          a.kv_b_stride, (int64_t)S * D, D, 1.f, 1.f, B, d.n_heads, d.n_kv_heads, D, S,
@@ -522,17 +523,17 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
         case WF_OP_O:  // h_b = h_a + o_proj(attn); last block: rms_norm(post_attention_layernorm)
             a.w = d.w_o + (int64_t)l * H * wrow_bytes(d.wfmt, H); a.N = H; a.K = H; a.ws0 = wsh[3];
             a.resid = m->h_a; a.out = m->h_b; a.out_stride = H;
-            a.ticket = m->tickets + TK_O; a.next_nw = d.ln_post + (int64_t)l * H;
+            a.ticket = m->tickets + TK_O * kTicketWords; a.next_nw = d.ln_post + (int64_t)l * H;
             return launch_gemv_fmt<MODE_O, 16>(d.wfmt, a, st);
         case WF_OP_GATE_UP:  // act = relu(gate)^2 * up; last block: rms_norm(ffn_sub_norm)
             a.w = d.w_gu + (int64_t)l * 2 * I * wrow_bytes(d.wfmt, H); a.N = 2 * I; a.K = H;
             a.ws0 = wsh[4]; a.ws1 = wsh[5]; a.out = m->act; a.out_stride = I;
-            a.ticket = m->tickets + TK_GU; a.next_nw = d.ffn_sub + (int64_t)l * I;
+            a.ticket = m->tickets + TK_GU * kTicketWords; a.next_nw = d.ffn_sub + (int64_t)l * I;
             return launch_gemv_fmt<MODE_GU, 16>(d.wfmt, a, st);
         case WF_OP_DOWN:  // h_a = h_b + down(act); last block: next layer's input norm or the final norm
             a.w = d.w_d + (int64_t)l * H * wrow_bytes(d.wfmt, I); a.N = H; a.K = I; a.ws0 = wsh[6];
             a.resid = m->h_b; a.out = m->h_a; a.out_stride = H;
-            a.ticket = m->tickets + TK_DN;
+            a.ticket = m->tickets + TK_DN * kTicketWords;
             if (l + 1 < d.layers) {
                 a.next_nw = d.ln_in + (int64_t)(l + 1) * H;
             } else {
@@ -544,7 +545,7 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             const size_t sh = (size_t)H * 2;
 #define WF_LM(MBV)                                                                                              \
     hipLaunchKernelGGL((k_lm_head<MBV>), dim3(m->lm_blocks, B / MBV), dim3(256), sh * MBV, st, d.embed, m->hn, \
-                       H, d.vocab, B, m->logits, m->am_part, m->lm_blocks, m->tickets + TK_LM, m->tokens,      \
+                       H, d.vocab, B, m->logits, m->am_part, m->lm_blocks, m->tickets + TK_LM * kTicketWords, m->tokens,      \
                        m->positions, S)
             if (B % 4 == 0) WF_LM(4);
             else if (B % 2 == 0) WF_LM(2);
@@ -620,12 +621,12 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_ALLOC(m->q8, (size_t)B * m->q8_stride);
     WF_ALLOC(m->act_sf, sizeof(float) * B);
     WF_ALLOC(m->act_sum, sizeof(int) * B);
-    WF_ALLOC(m->tickets, sizeof(unsigned) * (TK_ATTN2 + B));
+    WF_ALLOC(m->tickets, sizeof(unsigned) * kTicketWords * (TK_ATTN2 + B));
     WF_ALLOC(m->attn_ws, ws_bytes);
     WF_ALLOC(m->am_part, sizeof(uint2) * B * m->lm_blocks);
 #undef WF_ALLOC
     // tickets start at zero; every launch re-arms the ones it uses
-    if ((e = hipMemset(m->tickets, 0, sizeof(unsigned) * (TK_ATTN2 + B))) != hipSuccess) return fail(e);
+    if ((e = hipMemset(m->tickets, 0, sizeof(unsigned) * kTicketWords * (TK_ATTN2 + B))) != hipSuccess) return fail(e);
     if ((e = hipMemset(m->attn_ws, 0, ws_bytes)) != hipSuccess) return fail(e);
     if ((e = hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking)) != hipSuccess) return fail(e);
     *out = m;

@@ -33,21 +33,41 @@ __device__ __forceinline__ uint4 ld16_sc1(__amdgpu_buffer_rsrc_t r, int byte_off
     return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16));
 }
 
-// Producer side of the ticket: all of this block's sc1 stores must be issued before the call.
-// Returns true in exactly one block of the launch (the last arriver); that block must call
-// ticket_rearm() when done.
-__device__ __forceinline__ bool ticket_arrive(unsigned* ticket, unsigned n_blocks, int* sh_flag) {
+// Producer side of the launch ticket: all of this block's sc1 stores must be issued before the
+// call. Arrivals are spread over kTicketShards counters (one word takes ~88 atomics/us, so 800+
+// arrivals on one word would serialise for ~10 us); the last arriver of each shard re-arms its shard
+// and relays to the top counter. Returns true in exactly one block of the launch (the last
+// arriver), which must call ticket_rearm() when done. `t` points at kTicketShards + 1 words.
+constexpr int kTicketShards = 32;
+constexpr int kTicketWords = 64;  // words reserved per ticket (>= kTicketShards + 1, 256-byte aligned)
+
+// `idx` in [0, n_blocks) names the arriving block within the ticket's arrival set.
+__device__ __forceinline__ bool ticket_arrive(unsigned* t, unsigned n_blocks, unsigned idx, int* sh_flag) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        const unsigned old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *sh_flag = (old == n_blocks - 1u);
+        const unsigned bid = idx;
+        const unsigned nsh = n_blocks < (unsigned)kTicketShards ? n_blocks : (unsigned)kTicketShards;
+        const unsigned sh = bid % nsh;
+        const unsigned members = (n_blocks - sh + nsh - 1) / nsh;  // blocks with bid % nsh == sh
+        bool last = false;
+        const unsigned old = __hip_atomic_fetch_add(t + sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == members - 1u) {
+            st_sc1(t + sh, 0u);  // every member of this shard has arrived: re-arm it
+            const unsigned top =
+                __hip_atomic_fetch_add(t + kTicketShards, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = (top == nsh - 1u);
+        }
+        *sh_flag = last;
     }
     __syncthreads();
     return *sh_flag != 0;
 }
-__device__ __forceinline__ void ticket_rearm(unsigned* ticket) {
-    if (threadIdx.x == 0) st_sc1(ticket, 0u);
+__device__ __forceinline__ unsigned linear_block_id() {
+    return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+}
+__device__ __forceinline__ void ticket_rearm(unsigned* t) {
+    if (threadIdx.x == 0) st_sc1(t + kTicketShards, 0u);
 }
 
 // Where a normalised row goes: int8 codes + float scale + exact code sum (for the next ternary
