@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Ablation timing of the decode ops on the full 2B model: production kernels vs builds without the
-norm/quantize prologue (flag 1) and without weight loads (flag 2). Event-timed per op (30 layers
+int8 activation staging (flag 1), without weight loads (flag 2), without the producer tail
+(ticket + next-op norm, flag 4) or with the ticket but no norm (flag 8). Event-timed per op (30 layers
 back to back after an Infinity-Cache flush), like bench.py. Results of flagged runs are garbage."""
 import json
 import sys
@@ -22,7 +23,7 @@ def main():
     w = synthetic_weights(BITNET_2B, seed=0)
     res = {}
     for fmt_name, fmt in (("tq", WF_FMT_TQ), ("i2s", WF_FMT_I2S)):
-        for flags in (0, 1, 2, 3):
+        for flags in (0, 1, 2, 4, 8, 5):
             if fmt == WF_FMT_I2S and flags:
                 continue
             dec = BitNetDecoder(BITNET_2B, w, batch=1, wfmt=fmt, debug_flags=flags)

@@ -41,7 +41,7 @@ int decode_attention_impl(const void* q, int q_dtype, int64_t q_sb, int64_t q_sh
                           const AttnNext* next = nullptr);
 
 enum { MODE_QKV = 0, MODE_O = 1, MODE_GU = 2, MODE_DN = 3 };
-enum { WF_DBG_NO_PROLOGUE = 1, WF_DBG_NO_WEIGHTS = 2 };  // ablation builds of the same kernel (timing only)
+enum { WF_DBG_NO_PROLOGUE = 1, WF_DBG_NO_WEIGHTS = 2, WF_DBG_NO_TAIL = 4, WF_DBG_TAIL_NO_NORM = 8 };  // timing ablations
 constexpr int kPrefetch = 4;  // 16-byte weight chunks in flight per lane
 
 struct GemvArgs {
@@ -258,9 +258,11 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
             const int64_t byte_off = ((int64_t)(b0 + m) * a.out_stride + first) * 2;
             if (first < a.out_stride) st16_sc1(make_rsrc(a.out), (int)byte_off, make_uint4(pk[0], pk[1], pk[2], pk[3]));
         }
+        if (a.flags & WF_DBG_NO_TAIL) return;
         if (!ticket_arrive(a.ticket, gridDim.x * gridDim.y, linear_block_id(), &sh_flag)) return;
         // last block of the launch: rms_norm + quantize (or final norm) of every row for the next op
         const int Kn = (int)a.out_stride;
+        if (a.flags & WF_DBG_TAIL_NO_NORM) { ticket_rearm(a.ticket); return; }
         for (int b = 0; b < a.B; ++b) {
             NormOut no{a.next_q8 + (int64_t)b * a.q8_stride, a.next_sf + b, a.next_asum + b,
                        a.next_y16 ? a.next_y16 + (int64_t)b * Kn : nullptr};
