@@ -128,8 +128,8 @@ typedef struct {
     uint16_t* logits;             /* [batch, vocab] bf16                                           */
     uint16_t* k_cache;            /* [layers, batch, n_kv_heads, max_seq, head_dim] bf16           */
     uint16_t* v_cache;
-    int debug_flags;              /* 0; ablation switches for timing studies (1: no norm/quantize
-                                     prologue, 2: no weight loads) -- results are then meaningless */
+    int debug_flags;              /* reserved, must be 0 (latency studies use the stamp build,
+                                     tools/stamps.py)                                             */
 } wf_model_desc;
 
 typedef struct wf_model wf_model;

@@ -86,25 +86,11 @@ struct KVRaw {
     }
 };
 
-// Optional fused follow-up (decode step): when every kv group of row b has written its heads
-// (sc1 stores), the last one normalises the full attention row (attn_sub_norm) and quantises it
-// for the O projection (wf_norm.h). ticket2 == nullptr disables it (generic C-ABI use).
-struct AttnNext {
-    unsigned* ticket2;
-    const uint16_t* nw;
-    float eps;
-    int8_t* q8;
-    int64_t q8_stride;
-    float* sf;
-    int* asum;
-};
-
-// store 4 consecutive outputs (write-through bf16x4 when the fused follow-up reads them)
-__device__ __forceinline__ void store_out4(void* out, int64_t off, int odt, const float (&v)[4], bool sc1) {
-    if (sc1) {  // odt == BF16 (checked on the host)
-        const uint64_t pk = (uint64_t)f2bf(v[0]) | ((uint64_t)f2bf(v[1]) << 16) | ((uint64_t)f2bf(v[2]) << 32) |
-                            ((uint64_t)f2bf(v[3]) << 48);
-        st_sc1(reinterpret_cast<uint64_t*>(reinterpret_cast<uint16_t*>(out) + off), pk);
+// store 4 consecutive outputs
+__device__ __forceinline__ void store_out4(void* out, int64_t off, int odt, const float (&v)[4]) {
+    if (odt == DT_BF16) {
+        const uint2 pk = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + off) = pk;
     } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) store_from_f32(out, off + j, odt, v[j]);
@@ -116,14 +102,16 @@ __device__ __forceinline__ void store_out4(void* out, int64_t off, int odt, cons
 // softmax; groups merge by shuffles and through LDS. With NS > 1 the block publishes (m, l, o)
 // partials write-through (sc1) and bumps a per-(b, g) ticket; the last arriver merges the splits
 // and writes the output (MI355X_MICROARCH.md "Valid forms" row 1: sc1 stores, vmcnt(0) in every
-// storing wave, a barrier, one agent-scope atomic add; sc1 loads in the last arriver). The last
-// arriver also re-arms the ticket for the next launch.
+// storing wave, a barrier, one agent-scope atomic add; sc1 loads in the last arriver). Its merge
+// issues every (m, l) and o load of its share of the splits at once (one round trip), folds them
+// with an online max, and combines the thread subsets through LDS. The last arriver also re-arms
+// the ticket for the next launch.
 template <int D, int G, int KVDT>
 __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
     const void* __restrict__ q, int qdt, int64_t q_sb, int64_t q_sh, const void* __restrict__ K,
     const void* __restrict__ V, int64_t kv_sb, int64_t kv_sh, int64_t kv_st, float k_scale, float v_scale, int Hq,
     int Hkv, int S, const int32_t* __restrict__ seq_lens, float sm_scale, int NS, unsigned* __restrict__ cnt,
-    float* __restrict__ part, void* __restrict__ out, int odt, int64_t o_sb, int64_t o_sh, AttnNext nx) {
+    float* __restrict__ part, void* __restrict__ out, int odt, int64_t o_sb, int64_t o_sh) {
     constexpr int LP = D / 8;                // lanes per key position
     constexpr int NG = kAttnThreads / LP;    // lane groups per block
     constexpr int T = kAttnU * NG;
@@ -133,6 +121,7 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
     const int Sb = seq_lens ? min(seq_lens[b], S) : S;
     const int t0 = s * T;
     const int nact = (Sb + T - 1) / T;       // splits that hold keys for this sequence
+    WF_STAMP(0);
 
     __shared__ float sm_m[NG][G], sm_l[NG][G];
     __shared__ __attribute__((aligned(16))) float sm_o[NG][G][D];
@@ -148,13 +137,6 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
     }
     if (t0 < Sb) {
         const int64_t kvb = b * kv_sb + g * kv_sh + li * 8;
-        KVRaw<KVDT> kr[kAttnU], vr[kAttnU];
-#pragma unroll
-        for (int u = 0; u < kAttnU; ++u) {
-            const int t = min(t0 + gid + NG * u, Sb - 1);
-            kr[u].load(K, kvb + t * kv_st);
-            vr[u].load(V, kvb + t * kv_st);
-        }
         float qv[G][8];
 #pragma unroll
         for (int h = 0; h < G; ++h) {
@@ -169,6 +151,13 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
                 for (int j = 0; j < 8; ++j) qv[h][j] = load_as_f32(q, qo + j, qdt);
             }
         }
+        KVRaw<KVDT> kr[kAttnU], vr[kAttnU];
+#pragma unroll
+        for (int u = 0; u < kAttnU; ++u) {
+            const int t = min(t0 + gid + NG * u, Sb - 1);
+            kr[u].load(K, kvb + t * kv_st);
+            vr[u].load(V, kvb + t * kv_st);
+        }
         float sc[kAttnU][G];
 #pragma unroll
         for (int u = 0; u < kAttnU; ++u) {
@@ -180,11 +169,11 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
                 float d = 0.f;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) d = fmaf(qv[h][j], kx[j], d);
-#pragma unroll
-                for (int off = LP / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+                d = group_reduce<LP>(d, OpAdd{});
                 sc[u][h] = valid ? d * sm_scale : -INFINITY;
             }
         }
+        WF_STAMP(1);
 #pragma unroll
         for (int h = 0; h < G; ++h) {
             float mx = sc[0][h];
@@ -216,6 +205,7 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
         *reinterpret_cast<float4*>(&sm_o[gid][h][li * 8 + 4]) = make_float4(o[h][4], o[h][5], o[h][6], o[h][7]);
     }
     __syncthreads();
+    WF_STAMP(2);
     // block result per (h, 4 consecutive d)
     constexpr int D4 = D / 4;
     const int rec = D + 4;  // partial record: m, l, 0, 0, o[D]
@@ -237,7 +227,7 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
         const int hq = g * grp + h;
         if (NS == 1) {
             const float ov[4] = {os[0] / ls, os[1] / ls, os[2] / ls, os[3] / ls};
-            store_out4(out, b * o_sb + (int64_t)hq * o_sh + d, odt, ov, nx.ticket2 != nullptr);
+            store_out4(out, b * o_sb + (int64_t)hq * o_sh + d, odt, ov);
         } else if (t0 < Sb) {
             const int off = (int)((((int64_t)b * Hq + hq) * NS + s) * rec) * 4;  // bytes
             const float4 ov = make_float4(os[0], os[1], os[2], os[3]);
@@ -247,15 +237,7 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
                                                        off, 0, 16);
         }
     }
-    __shared__ float red_n[48];
-    if (NS == 1) {
-        if (nx.ticket2 && ticket_arrive(nx.ticket2 + b * kTicketWords, Hkv, g, &sh_last)) {
-            NormOut no{nx.q8 + (int64_t)b * nx.q8_stride, nx.sf + b, nx.asum + b, nullptr};
-            norm_quant_row<true>(reinterpret_cast<const uint16_t*>(out) + b * o_sb, nx.nw, Hq * D, nx.eps, no, red_n);
-            ticket_rearm(nx.ticket2 + b * kTicketWords);
-        }
-        return;
-    }
+    if (NS == 1) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -263,87 +245,70 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
         sh_last = (old == (unsigned)NS - 1u);
     }
     __syncthreads();
+    WF_STAMP(3);
     if (!sh_last) return;
     // ---- last arriver: merge the active splits of every query head of this kv group ----
     const int na = min(nact, NS);  // <= kAttnMaxSplits (host check)
-    __shared__ float sm_ml[G][kAttnMaxSplits][2];
-    __shared__ float sm_ML[G][2];
-    for (int idx = threadIdx.x; idx < grp * na; idx += kAttnThreads) {  // round 1: (m, l) records
-        const int h = idx / na, sp = idx - h * na;
-        const int off = (int)((((int64_t)b * Hq + g * grp + h) * NS + sp) * rec) * 4;
-        const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
-        sm_ml[h][sp][0] = v.x;
-        sm_ml[h][sp][1] = v.y;
-    }
-    __syncthreads();
-    if (threadIdx.x < grp) {
-        const int h = threadIdx.x;
-        float M = -INFINITY;
-        for (int sp = 0; sp < na; ++sp) M = fmaxf(M, sm_ml[h][sp][0]);
-        float Ls = 0.f;
-        for (int sp = 0; sp < na; ++sp) {
-            const float w = (sm_ml[h][sp][0] == -INFINITY) ? 0.f : __expf(sm_ml[h][sp][0] - M);
-            sm_ml[h][sp][0] = w;
-            Ls += w * sm_ml[h][sp][1];
-        }
-        sm_ML[h][0] = M;
-        sm_ML[h][1] = Ls;
-    }
-    __syncthreads();
-    // round 2: weighted sum of the o partials; threads = (h, d4) x nsub split-subsets
-    const int nout = grp * D4;
-    const int nsub = max(1, kAttnThreads / nout);
-    float* red = sm_o[0][0];  // [nsub][nout][4] floats <= NG*G*D
-    if (threadIdx.x < nout * nsub) {
-        const int oi = threadIdx.x % nout, sb = threadIdx.x / nout;
+    const int nout = grp * D4;     // float4 outputs of this (b, g)
+    const int nsub = max(1, kAttnThreads / nout);  // thread subsets over the splits
+    constexpr int kMU = 8;         // splits in flight per thread per round
+    float M = -INFINITY, Lsum = 0.f, O4[4] = {0.f, 0.f, 0.f, 0.f};
+    const int oi = threadIdx.x % nout, sb = threadIdx.x / nout;
+    if (sb < nsub) {
         const int h = oi / D4, d = (oi - h * D4) * 4;
         const int64_t rbase = (((int64_t)b * Hq + g * grp + h) * NS) * rec;
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int sp0 = sb; sp0 < na; sp0 += 16 * nsub) {
-            float4 v[16];
+        for (int sp0 = sb; sp0 < na; sp0 += kMU * nsub) {
+            float4 ml[kMU], ov[kMU];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int sp = sp0 + u * nsub;
-                v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (sp < na)
-                    v[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                          rs, (int)((rbase + (int64_t)sp * rec) * 4) + 16 + 4 * d, 0, 16));
+            for (int u = 0; u < kMU; ++u) {  // every load of the round in flight at once
+                const int sp = min(sp0 + u * nsub, na - 1);
+                const int off = (int)((rbase + (int64_t)sp * rec) * 4);
+                ml[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
+                ov[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 + 4 * d, 0, 16));
             }
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int sp = sp0 + u * nsub;
-                if (sp < na) {
-                    const float w = sm_ml[h][sp][0];
-                    acc[0] = fmaf(w, v[u].x, acc[0]);
-                    acc[1] = fmaf(w, v[u].y, acc[1]);
-                    acc[2] = fmaf(w, v[u].z, acc[2]);
-                    acc[3] = fmaf(w, v[u].w, acc[3]);
+            for (int u = 0; u < kMU; ++u) {
+                if (sp0 + u * nsub < na) {
+                    const float nm = fmaxf(M, ml[u].x);
+                    const float a = __expf(M - nm), c = __expf(ml[u].x - nm);  // M = -inf -> a = 0
+                    Lsum = Lsum * a + ml[u].y * c;
+                    O4[0] = O4[0] * a + ov[u].x * c;
+                    O4[1] = O4[1] * a + ov[u].y * c;
+                    O4[2] = O4[2] * a + ov[u].z * c;
+                    O4[3] = O4[3] * a + ov[u].w * c;
+                    M = nm;
                 }
             }
         }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) red[(sb * nout + oi) * 4 + j] = acc[j];
+    }
+    // combine the nsub subsets: [nsub][nout] x (M, L, O[4]) in the (now free) sm_o area
+    float* cm = sm_o[0][0];
+    float* cl = cm + nsub * nout;
+    float4* co = reinterpret_cast<float4*>(cl + nsub * nout);
+    if (sb < nsub) {
+        cm[sb * nout + oi] = M;
+        cl[sb * nout + oi] = Lsum;
+        co[sb * nout + oi] = make_float4(O4[0], O4[1], O4[2], O4[3]);
     }
     __syncthreads();
-    for (int oi = threadIdx.x; oi < nout; oi += kAttnThreads) {
-        const int h = oi / D4, d = (oi - h * D4) * 4;
-        const int hq = g * grp + h;
-        const float inv = 1.0f / sm_ML[h][1];
-        float ov[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            float t = 0.f;
-            for (int sb = 0; sb < nsub; ++sb) t += red[(sb * nout + oi) * 4 + j];
-            ov[j] = t * inv;
+    WF_STAMP(4);
+    for (int o2 = threadIdx.x; o2 < nout; o2 += kAttnThreads) {
+        const int h2 = o2 / D4, d2 = (o2 - h2 * D4) * 4;
+        float MM = -INFINITY;
+        for (int t = 0; t < nsub; ++t) MM = fmaxf(MM, cm[t * nout + o2]);
+        float LL = 0.f, OO[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < nsub; ++t) {
+            const float wgt = (cm[t * nout + o2] == -INFINITY) ? 0.f : __expf(cm[t * nout + o2] - MM);
+            LL += cl[t * nout + o2] * wgt;
+            const float4 v4 = co[t * nout + o2];
+            OO[0] += v4.x * wgt; OO[1] += v4.y * wgt; OO[2] += v4.z * wgt; OO[3] += v4.w * wgt;
         }
-        store_out4(out, b * o_sb + (int64_t)hq * o_sh + d, odt, ov, nx.ticket2 != nullptr);
+        const float inv = 1.0f / LL;
+        const float ov4[4] = {OO[0] * inv, OO[1] * inv, OO[2] * inv, OO[3] * inv};
+        store_out4(out, b * o_sb + (int64_t)(g * grp + h2) * o_sh + d2, odt, ov4);
     }
     if (threadIdx.x == 0) st_sc1(cnt + b * Hkv + g, 0u);  // re-arm the ticket for the next launch
-    if (nx.ticket2 && ticket_arrive(nx.ticket2 + b * kTicketWords, Hkv, g, &sh_last)) {
-        NormOut no{nx.q8 + (int64_t)b * nx.q8_stride, nx.sf + b, nx.asum + b, nullptr};
-        norm_quant_row<true>(reinterpret_cast<const uint16_t*>(out) + b * o_sb, nx.nw, Hq * D, nx.eps, no, red_n);
-        ticket_rearm(nx.ticket2 + b * kTicketWords);
-    }
+    WF_STAMP(5);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -377,14 +342,13 @@ struct AttnArgs {
     const void* k; const void* v; int64_t kv_sb, kv_sh, kv_st; float ks, vs;
     int Hq, Hkv, S; const int32_t* sl; float sm; int NS; unsigned* cnt; float* part;
     void* out; int odt; int64_t o_sb, o_sh;
-    AttnNext nx;
 };
 
 template <int D, int G, int KVDT>
 static void launch_attn(dim3 grid, hipStream_t st, const AttnArgs& a) {
     hipLaunchKernelGGL((k_attn_split<D, G, KVDT>), grid, dim3(kAttnThreads), 0, st, a.q, a.qdt, a.q_sb, a.q_sh, a.k,
                        a.v, a.kv_sb, a.kv_sh, a.kv_st, a.ks, a.vs, a.Hq, a.Hkv, a.S, a.sl, a.sm, a.NS, a.cnt, a.part,
-                       a.out, a.odt, a.o_sb, a.o_sh, a.nx);
+                       a.out, a.odt, a.o_sb, a.o_sh);
 }
 
 template <int D, int G>
@@ -412,8 +376,7 @@ static int dispatch_g(int grp, int kvdt, dim3 grid, hipStream_t st, const AttnAr
 int decode_attention_impl(const void* q, int q_dtype, int64_t q_sb, int64_t q_sh, const void* k, const void* v,
                           int kv_dtype, int64_t kv_sb, int64_t kv_sh, int64_t kv_st, float k_scale, float v_scale, int B,
                           int Hq, int Hkv, int D, int S, const int32_t* seq_lens, float sm_scale, void* out,
-                          int out_dtype, int64_t o_sb, int64_t o_sh, void* ws, hipStream_t st,
-                          const AttnNext* next = nullptr) {
+                          int out_dtype, int64_t o_sb, int64_t o_sh, void* ws, hipStream_t st) {
     WF_REQUIRE(D == 16 || D == 32 || D == 64 || D == 128, "decode_attention: head_dim %d unsupported", D);
     const int NS = attn_splits(D, S);
     WF_REQUIRE(NS <= kAttnMaxSplits, "decode_attention: S=%d exceeds %d keys", S, kAttnMaxSplits * attn_split_len(D));
@@ -421,12 +384,7 @@ int decode_attention_impl(const void* q, int q_dtype, int64_t q_sb, int64_t q_sh
     AttnArgs a{q, q_dtype, q_sb, q_sh, k, v, kv_sb, kv_sh, kv_st, k_scale, v_scale, Hq, Hkv, S, seq_lens, sm_scale, NS,
                reinterpret_cast<unsigned*>(ws),
                reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(ws) + attn_cnt_bytes(B, Hkv)), out, out_dtype,
-               o_sb, o_sh, AttnNext{}};
-    if (next) {
-        WF_REQUIRE(out_dtype == WF_BF16 && o_sh == D && o_sb == (int64_t)Hq * D && Hq * D <= 8192,
-                   "decode_attention: fused follow-up needs a contiguous bf16 [B, Hq*D] output");
-        a.nx = *next;
-    }
+               o_sb, o_sh};
     const dim3 grid(NS, Hkv, B);
     const int grp = Hq / Hkv;
     int bad = 1;
@@ -441,6 +399,8 @@ int decode_attention_impl(const void* q, int q_dtype, int64_t q_sb, int64_t q_sh
 }
 
 }  // namespace wf
+
+WF_STAMP_READER(wf_debug_stamps_attn)
 
 using namespace wf;
 

@@ -1,19 +1,19 @@
 // wf_decode.hip -- fused BitNet b1.58 decode step for gfx950.
 //
 // One decode token per sequence, per layer five launches:
-//   QKV : stage int8 image -> ternary GEMV over rows q|k|v -> reference correction, RoPE (θ=5e5,
-//         half-split), q -> qbuf, k/v -> cache[pos]
-//   ATTN: split-K GQA decode attention (wf_attn.hip); its last block normalises attn
-//         (attn_sub_norm) and quantises it for O
-//   O   : GEMV + correction + residual (h_b = h_a + o); last block: rms_norm(post_attention_layernorm)
-//         + quantize for gate/up
-//   GU  : GEMV over gate/up rows interleaved in 8-row tiles; relu(gate)^2 * up; last block:
-//         rms_norm(ffn_sub_norm) + quantize for down
-//   DN  : GEMV (K = 6912) + correction + residual (h_a = h_b + d); last block: next layer's
-//         rms_norm(input_layernorm) + quantize for QKV, or the final norm for the LM head
-// plus embed (+ layer-0 norm/quantize) and the tied bf16 LM head with a fused greedy argmax.
-// "rms_norm -> quantize" therefore runs once per op (in the producer's last-arriving block, see
-// wf_norm.h) instead of in every GEMV block. Every float op follows
+//   QKV : rms_norm(input_layernorm) + quantize (block prologue) -> ternary GEMV over rows q|k|v ->
+//         reference correction, RoPE (θ=5e5, half-split), q -> qbuf, k/v -> cache[pos]
+//   ATTN: split-K GQA decode attention (wf_attn.hip), single launch, last-arriver merge
+//   O   : rms_norm(attn_sub_norm) + quantize (prologue) -> GEMV + correction + residual
+//         (h_b = h_a + o)
+//   GU  : rms_norm(post_attention_layernorm) + quantize (prologue) -> GEMV over gate/up rows
+//         interleaved in 8-row tiles; relu(gate)^2 * up
+//   DN  : rms_norm(ffn_sub_norm) + quantize (prologue) -> GEMV (K = 6912) + correction + residual
+//         (h_a = h_b + d)
+// plus embed and the tied bf16 LM head (after the final norm) with a fused greedy argmax.
+// At batch 1 every GEMV block normalises + quantises its input row itself (wf_norm.h) while its
+// first weight chunks are in flight, so no launch carries a serial norm tail; at batch > 1 one
+// k_rownorm launch per op produces the int8 codes instead. Every float op follows
 // scripts/direct_inference_full.py:181-302 (bf16 tensors between ops); results match the oracle
 // up to fp32 reduction order.
 #include <hip/hip_runtime.h>
@@ -25,27 +25,22 @@
 #include "wf_norm.h"
 
 namespace wf {
-struct AttnNext {          // mirror of wf_attn.hip (per-row level-2 ticket + attn_sub_norm/quantize)
-    unsigned* ticket2;
-    const uint16_t* nw;
-    float eps;
-    int8_t* q8;
-    int64_t q8_stride;
-    float* sf;
-    int* asum;
-};
 int decode_attention_impl(const void* q, int q_dtype, int64_t q_sb, int64_t q_sh, const void* k, const void* v,
                           int kv_dtype, int64_t kv_sb, int64_t kv_sh, int64_t kv_st, float k_scale, float v_scale, int B,
                           int Hq, int Hkv, int D, int S, const int32_t* seq_lens, float sm_scale, void* out,
-                          int out_dtype, int64_t o_sb, int64_t o_sh, void* ws, hipStream_t st,
-                          const AttnNext* next = nullptr);
+                          int out_dtype, int64_t o_sb, int64_t o_sh, void* ws, hipStream_t st);
 
 enum { MODE_QKV = 0, MODE_O = 1, MODE_GU = 2, MODE_DN = 3 };
-enum { WF_DBG_NO_PROLOGUE = 1, WF_DBG_NO_WEIGHTS = 2, WF_DBG_NO_TAIL = 4, WF_DBG_TAIL_NO_NORM = 8 };  // timing ablations
 constexpr int kPrefetch = 4;  // 16-byte weight chunks in flight per lane
 
 struct GemvArgs {
-    const int8_t* q8;          // [B, q8_stride] int8 activations of this op (published by the producer)
+    // input row(s): bf16 x + norm weight (PPT > 0: normalised + quantised in the block prologue)
+    const uint16_t* x;
+    int64_t x_stride;
+    const uint16_t* nw;
+    float eps;
+    // or int8 codes from k_rownorm (PPT == 0)
+    const int8_t* q8;          // [B, q8_stride]
     int64_t q8_stride;
     const float* act_sf;       // [B] float(act scale)
     const int* act_sum;        // [B] sum of codes
@@ -64,15 +59,6 @@ struct GemvArgs {
     uint16_t* kc;
     uint16_t* vc;
     int64_t kv_b_stride;
-    // next op's norm (O/GU/DN): last block normalises `out` rows
-    unsigned* ticket;
-    const uint16_t* next_nw;
-    float eps;
-    int8_t* next_q8;           // shared activation buffer (stride q8_stride)
-    float* next_sf;
-    int* next_asum;
-    uint16_t* next_y16;        // final norm output (bf16 [B, out_stride]) instead of int8, or nullptr
-    int flags;
 };
 
 // Reference correction (direct_inference_full.py:201-208) for one output:
@@ -83,21 +69,18 @@ __device__ __forceinline__ float corrected(int S, float ws, int asum, float sf) 
     return (raw - c) * sf;
 }
 
-template <int LPR>
-__device__ __forceinline__ int group_sum_i(int v) {
-#pragma unroll
-    for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
 // Block = 256 threads; LPR lanes per weight row -> 256/LPR rows per block; MB activation rows.
-template <class F, int MODE, int LPR, int MB>
+// PPT > 0 (MB == 1): the block normalises + quantises its input row itself (wf_norm.h) while its
+// first weight chunks stream in; PPT = 8-element pieces per thread (padded K <= 2048 * PPT).
+// PPT == 0: the codes come from k_rownorm (batch > 1).
+template <class F, int MODE, int LPR, int MB, int PPT>
 __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
+    static_assert(PPT == 0 || MB == 1, "the norm prologue handles one activation row");
     constexpr int RPB = 256 / LPR;
     extern __shared__ __attribute__((aligned(16))) int8_t smem[];
-    __shared__ float red[48];
+    __shared__ float red[8];
+    __shared__ int red_i[4];
     __shared__ float s_out[MB][RPB];
-    __shared__ int sh_flag;
 
     const int K = a.K, N = a.N;
     const int img = lds_image_bytes<F>(K);
@@ -105,28 +88,31 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     const int lrow = threadIdx.x / LPR, sub = threadIdx.x % LPR;
     const int row = blockIdx.x * RPB + lrow;
     const int C = F::chunks(K);
-    const bool no_w = a.flags & WF_DBG_NO_WEIGHTS;
+    WF_STAMP(0);
 
-    // 1) int8 activation pieces (issued first: vmcnt retires in order), 2) the weight stream
-    const int pieces = F::k_pad(K) / 16;
-    constexpr int kMaxPiecesPerThread = 2;  // K_pad <= 8192
+    // 1) the input row (issued first: vmcnt retires in order), 2) the weight stream, 3) residual
+    NormRow<PPT == 0 ? 1 : PPT> nr;
+    constexpr int kMaxPiecesPerThread = 2;  // staged int8: K_pad <= 8192
     uint4 apre[MB][kMaxPiecesPerThread];
+    const int pieces16 = F::k_pad(K) / 16;
+    if constexpr (PPT > 0) {
+        nr.issue(a.x + (int64_t)b0 * a.x_stride, a.nw, K);
+    } else {
 #pragma unroll
-    for (int m = 0; m < MB; ++m)
+        for (int m = 0; m < MB; ++m)
 #pragma unroll
-        for (int i = 0; i < kMaxPiecesPerThread; ++i) {
-            const int p = threadIdx.x + 256 * i;
-            apre[m][i] = (p < pieces && 16 * p < K && !(a.flags & WF_DBG_NO_PROLOGUE))
-                             ? *reinterpret_cast<const uint4*>(a.q8 + (int64_t)(b0 + m) * a.q8_stride + 16 * p)
-                             : make_uint4(0, 0, 0, 0);
-        }
-    const uint8_t* wr = a.w + (int64_t)min(row, N - 1) * F::row_bytes(K) + sub * 16;
+            for (int i = 0; i < kMaxPiecesPerThread; ++i) {
+                const int p = threadIdx.x + 256 * i;
+                apre[m][i] = (p < pieces16 && 16 * p < K)
+                                 ? *reinterpret_cast<const uint4*>(a.q8 + (int64_t)(b0 + m) * a.q8_stride + 16 * p)
+                                 : make_uint4(0, 0, 0, 0);
+            }
+    }
+    const uint8_t* wr = a.w + (int64_t)min(row, N - 1) * F::row_bytes(K);
     uint4 wpre[kPrefetch];
 #pragma unroll
-    for (int u = 0; u < kPrefetch; ++u) {
-        const int c = LPR * u + sub;
-        wpre[u] = (c < C && !no_w) ? ldg_nt(wr + (int64_t)(LPR * u) * 16) : make_uint4(0, 0, 0, 0);
-    }
+    for (int u = 0; u < kPrefetch; ++u)  // clamped (no branch): lanes past the row re-read its last chunk
+        wpre[u] = ldg_nt(wr + (int64_t)min(LPR * u + sub, C - 1) * 16);
     float resid[MB];
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
@@ -134,21 +120,31 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
         if constexpr (MODE == MODE_O || MODE == MODE_DN)
             if (sub == 0 && row < N) resid[m] = bf2f(a.resid[(int64_t)(b0 + m) * a.out_stride + row]);
     }
-#pragma unroll
-    for (int m = 0; m < MB; ++m)
-#pragma unroll
-        for (int i = 0; i < kMaxPiecesPerThread; ++i) {
-            const int p = threadIdx.x + 256 * i;
-            if (p < pieces) *reinterpret_cast<uint4*>(smem + m * img + F::lds_off(16 * p)) = apre[m][i];
-        }
     float sf[MB];
     int asum[MB];
+    if constexpr (PPT > 0) {
+        float y[PPT][8];
+        sf[0] = norm_row<PPT>(nr, K, a.eps, y, red);
+        int as = quant_row<PPT>(y, sf[0], F::k_pad(K) / 8, smem, [](int p) { return F::lds_off(8 * p); });
+        as = wave_sum_i(as);
+        if ((threadIdx.x & 63) == 0) red_i[threadIdx.x >> 6] = as;
+    } else {
 #pragma unroll
-    for (int m = 0; m < MB; ++m) {
-        sf[m] = a.act_sf[b0 + m];
-        asum[m] = a.act_sum[b0 + m];
+        for (int m = 0; m < MB; ++m)
+#pragma unroll
+            for (int i = 0; i < kMaxPiecesPerThread; ++i) {
+                const int p = threadIdx.x + 256 * i;
+                if (p < pieces16) *reinterpret_cast<uint4*>(smem + m * img + F::lds_off(16 * p)) = apre[m][i];
+            }
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+            sf[m] = a.act_sf[b0 + m];
+            asum[m] = a.act_sum[b0 + m];
+        }
     }
     __syncthreads();
+    if constexpr (PPT > 0) asum[0] = (red_i[0] + red_i[1]) + (red_i[2] + red_i[3]);
+    WF_STAMP(1);
 
     int acc[MB];
 #pragma unroll
@@ -167,10 +163,8 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     for (int c0 = LPR * kPrefetch; c0 < C; c0 += LPR * kPrefetch) {
         uint4 w[kPrefetch];
 #pragma unroll
-        for (int u = 0; u < kPrefetch; ++u) {
-            const int c = c0 + LPR * u + sub;
-            w[u] = (c < C && !no_w) ? ldg_nt(wr + (int64_t)(c0 + LPR * u) * 16) : make_uint4(0, 0, 0, 0);
-        }
+        for (int u = 0; u < kPrefetch; ++u)
+            w[u] = ldg_nt(wr + (int64_t)min(c0 + LPR * u + sub, C - 1) * 16);
 #pragma unroll
         for (int u = 0; u < kPrefetch; ++u) {
             const int c = c0 + LPR * u + sub;
@@ -183,8 +177,9 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
             }
         }
     }
+    WF_STAMP(2);
 #pragma unroll
-    for (int m = 0; m < MB; ++m) acc[m] = group_sum_i<LPR>(acc[m]);
+    for (int m = 0; m < MB; ++m) acc[m] = group_reduce<LPR>(acc[m], OpAdd{});
 
     if constexpr (MODE == MODE_QKV) {
         // rows per head permuted: block t of head h = dims {8t..8t+7, 64+8t..64+8t+7} (RPB == 16)
@@ -222,6 +217,7 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                 cache[d0 + 64] = f2bf(x2);
             }
         }
+        WF_STAMP(7);
         return;
     } else {
         // O/DN: out[row] = bf16(resid + bf16(o)); GU: act[8t+i] = bf16(bf16(relu(g)^2) * u)
@@ -235,9 +231,8 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
             }
         }
         __syncthreads();
-        // publish this block's slice of the output vector write-through (16-byte sc1 stores)
         constexpr int NOUT = (MODE == MODE_GU) ? 8 : RPB;  // outputs per block per row
-        static_assert(NOUT % 8 == 0, "16-byte publishing granules");
+        static_assert(NOUT % 8 == 0, "16-byte output granules");
         if (threadIdx.x < MB * (NOUT / 8)) {
             const int m = threadIdx.x / (NOUT / 8), j = threadIdx.x % (NOUT / 8);
             uint32_t pk[4];
@@ -252,43 +247,64 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                     lo = s_out[m][8 * j + 2 * t];
                     hi = s_out[m][8 * j + 2 * t + 1];
                 }
-                pk[t] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+                pk[t] = pk_bf16(lo, hi);
             }
             const int64_t first = (int64_t)blockIdx.x * NOUT + 8 * j;
-            const int64_t byte_off = ((int64_t)(b0 + m) * a.out_stride + first) * 2;
-            if (first < a.out_stride) st16_sc1(make_rsrc(a.out), (int)byte_off, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+            if (first < a.out_stride)
+                *reinterpret_cast<uint4*>(a.out + (int64_t)(b0 + m) * a.out_stride + first) =
+                    make_uint4(pk[0], pk[1], pk[2], pk[3]);
         }
-        if (a.flags & WF_DBG_NO_TAIL) return;
-        if (!ticket_arrive(a.ticket, gridDim.x * gridDim.y, linear_block_id(), &sh_flag)) return;
-        // last block of the launch: rms_norm + quantize (or final norm) of every row for the next op
-        const int Kn = (int)a.out_stride;
-        if (a.flags & WF_DBG_TAIL_NO_NORM) { ticket_rearm(a.ticket); return; }
-        for (int b = 0; b < a.B; ++b) {
-            NormOut no{a.next_q8 + (int64_t)b * a.q8_stride, a.next_sf + b, a.next_asum + b,
-                       a.next_y16 ? a.next_y16 + (int64_t)b * Kn : nullptr};
-            norm_quant_row<true>(a.out + (int64_t)b * a.out_stride, a.next_nw, Kn, a.eps, no, red);
-        }
-        ticket_rearm(a.ticket);
+        WF_STAMP(3);
     }
 }
 
 // ---------------------------------------------------------------------------------------------
-// embed (+ layer-0 rms_norm/quantize), LM head with fused greedy argmax
+// embed, standalone row norm (batch > 1 codes; final norm), LM head with fused greedy argmax
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_embed_norm(const uint16_t* __restrict__ embed, const int32_t* __restrict__ tokens,
-                                                    int H, int V, uint16_t* __restrict__ h,
-                                                    const int32_t* __restrict__ positions, int32_t* __restrict__ seq_lens,
-                                                    const uint16_t* __restrict__ nw, float eps, int8_t* q8,
-                                                    int64_t q8_stride, float* sf, int* asum) {
-    __shared__ float red[48];
+__global__ __launch_bounds__(256) void k_embed(const uint16_t* __restrict__ embed, const int32_t* __restrict__ tokens,
+                                               int H, int V, uint16_t* __restrict__ h,
+                                               const int32_t* __restrict__ positions, int32_t* __restrict__ seq_lens) {
     const int b = blockIdx.x;
     const int tok = min(max(tokens[b], 0), V - 1);  // never read outside the table
     const uint16_t* src = embed + (int64_t)tok * H;
     for (int i = threadIdx.x; i < H / 8; i += blockDim.x)
         reinterpret_cast<uint4*>(h + (int64_t)b * H)[i] = reinterpret_cast<const uint4*>(src)[i];
     if (threadIdx.x == 0) seq_lens[b] = positions[b] + 1;
-    NormOut no{q8 + (int64_t)b * q8_stride, sf + b, asum + b, nullptr};
-    norm_quant_row<false>(src, nw, H, eps, no, red);
+}
+
+// One block per row: rms_norm + quantize -> q8/sf/asum (Y16 = false), or the final norm -> bf16.
+template <int PPT, bool Y16>
+__global__ __launch_bounds__(256) void k_rownorm(const uint16_t* __restrict__ x, int64_t xs,
+                                                 const uint16_t* __restrict__ nw, int K, float eps,
+                                                 int8_t* __restrict__ q8, int64_t q8s, float* __restrict__ sf,
+                                                 int* __restrict__ asum, uint16_t* __restrict__ y16, int64_t ys) {
+    __shared__ float red[8];
+    __shared__ int red_i[4];
+    const int b = blockIdx.x;
+    NormRow<PPT> nr;
+    nr.issue(x + (int64_t)b * xs, nw, K);
+    float y[PPT][8];
+    if constexpr (Y16) {
+        (void)norm_row<PPT>(nr, K, eps, y, red, false);
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) {
+            const int p = threadIdx.x + kNT * i;
+            if (p < K / 8)
+                *reinterpret_cast<uint4*>(y16 + (int64_t)b * ys + 8 * p) =
+                    make_uint4(pk_bf16(y[i][0], y[i][1]), pk_bf16(y[i][2], y[i][3]), pk_bf16(y[i][4], y[i][5]),
+                               pk_bf16(y[i][6], y[i][7]));
+        }
+    } else {
+        const float s = norm_row<PPT>(nr, K, eps, y, red);
+        int as = quant_row<PPT>(y, s, K / 8, q8 + (int64_t)b * q8s, [](int p) { return 8 * p; });
+        as = wave_sum_i(as);
+        if ((threadIdx.x & 63) == 0) red_i[threadIdx.x >> 6] = as;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            asum[b] = (red_i[0] + red_i[1]) + (red_i[2] + red_i[3]);
+            sf[b] = s;
+        }
+    }
 }
 
 // logits[b, v] = bf16(sum_k hn[b,k] * E[v,k]) (F.linear, fp32 accumulation); 16 lanes per vocab
@@ -311,6 +327,7 @@ __global__ __launch_bounds__(256) void k_lm_head(const uint16_t* __restrict__ E,
     const int row = blockIdx.x * 16 + lrow;
     const int C = H / 8;
     const uint16_t* er = E + (int64_t)min(row, V - 1) * H;
+    WF_STAMP(0);
     uint4 w[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {  // first weight chunks in flight before the activation staging
@@ -322,6 +339,7 @@ __global__ __launch_bounds__(256) void k_lm_head(const uint16_t* __restrict__ E,
         reinterpret_cast<uint4*>(sh + m * H)[j] = reinterpret_cast<const uint4*>(hn + (int64_t)(b0 + m) * H)[j];
     }
     __syncthreads();
+    WF_STAMP(1);
     float acc[MB];
 #pragma unroll
     for (int m = 0; m < MB; ++m) acc[m] = 0.f;
@@ -351,13 +369,11 @@ __global__ __launch_bounds__(256) void k_lm_head(const uint16_t* __restrict__ E,
             }
         }
     }
+    WF_STAMP(2);
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
         float v = acc[m];
-        v += __shfl_xor(v, 8, 64);
-        v += __shfl_xor(v, 4, 64);
-        v += __shfl_xor(v, 2, 64);
-        v += __shfl_xor(v, 1, 64);
+        v = group_reduce<16>(v, OpAdd{});
         if (sub == 0) {
             const uint16_t lb = f2bf(v);
             if (row < V) logits[(int64_t)(b0 + m) * V + row] = lb;
@@ -374,22 +390,23 @@ __global__ __launch_bounds__(256) void k_lm_head(const uint16_t* __restrict__ E,
         const uint64_t pk = ((uint64_t)(uint32_t)(blockIdx.x * 16 + bi) << 32) | __float_as_uint(best);
         st_sc1(reinterpret_cast<uint64_t*>(part) + (int64_t)(b0 + m) * nblk + blockIdx.x, pk);
     }
-    if (!ticket_arrive(ticket, gridDim.x * gridDim.y, linear_block_id(), &sh_flag)) return;
+    const bool last = ticket_arrive(ticket, gridDim.x * gridDim.y, linear_block_id(), &sh_flag);
+    WF_STAMP(3);
+    if (!last) return;
+    constexpr int kAM = 32;  // partial records in flight per thread
     for (int b = 0; b < B; ++b) {
         float best = -INFINITY;
         int bi = 0x7fffffff;
         const uint64_t* pb = reinterpret_cast<const uint64_t*>(part) + (int64_t)b * nblk;
-        for (int i0 = threadIdx.x; i0 < nblk; i0 += 256 * 8) {
-            uint64_t v[8];
+        for (int i0 = threadIdx.x; i0 < nblk; i0 += 256 * kAM) {
+            uint64_t v[kAM];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = (i0 + 256 * u < nblk) ? ld_sc1(pb + i0 + 256 * u) : 0ull;
+            for (int u = 0; u < kAM; ++u) v[u] = ld_sc1(pb + min(i0 + 256 * u, nblk - 1));  // clamped: repeats are harmless
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                if (i0 + 256 * u < nblk) {
-                    const float fv = __uint_as_float((uint32_t)v[u]);
-                    const int id = (int)(v[u] >> 32);
-                    if (fv > best || (fv == best && id < bi)) { best = fv; bi = id; }
-                }
+            for (int u = 0; u < kAM; ++u) {
+                const float fv = __uint_as_float((uint32_t)v[u]);
+                const int id = (int)(v[u] >> 32);
+                if (fv > best || (fv == best && id < bi)) { best = fv; bi = id; }
             }
         }
         r_val[threadIdx.x] = best;
@@ -413,15 +430,18 @@ __global__ __launch_bounds__(256) void k_lm_head(const uint16_t* __restrict__ E,
         __syncthreads();
     }
     ticket_rearm(ticket);
+    WF_STAMP(4);
 }
 
 }  // namespace wf
 
+WF_STAMP_READER(wf_debug_stamps_decode)
+
 // =============================================================================================
 // Model runtime
 // =============================================================================================
-// ticket slots, kTicketWords words each (ATTN2: one per batch row)
-enum { TK_O = 0, TK_GU = 1, TK_DN = 2, TK_LM = 3, TK_ATTN2 = 4 };
+// ticket slots, kTicketWords words each
+enum { TK_LM = 0, TK_COUNT = 1 };
 
 struct wf_model {
     wf_model_desc d;
@@ -432,7 +452,7 @@ struct wf_model {
     uint16_t *k_cache = nullptr, *v_cache = nullptr;  // caller-owned (desc)
     int32_t* seq_lens = nullptr;
     uint16_t *h_a = nullptr, *h_b = nullptr, *qbuf = nullptr, *attn = nullptr, *act = nullptr, *hn = nullptr;
-    int8_t* q8 = nullptr;   // activation codes of the next GEMV [B, q8_stride]
+    int8_t* q8 = nullptr;   // batch > 1: activation codes of the next GEMV [B, q8_stride]
     float* act_sf = nullptr;
     int* act_sum = nullptr;
     unsigned* tickets = nullptr;
@@ -450,6 +470,9 @@ using namespace wf;
 namespace {
 
 int64_t wrow_bytes(int fmt, int K) { return fmt == WF_FMT_TQ ? FmtTQ::row_bytes(K) : FmtI2S::row_bytes(K); }
+int k_pad(int fmt, int K) { return fmt == WF_FMT_TQ ? FmtTQ::k_pad(K) : FmtI2S::k_pad(K); }
+// 8-element pieces per thread of the norm prologue / k_rownorm
+int norm_ppt(int kpad) { return kpad <= 2 * 8 * kNT ? 2 : 4; }
 
 template <class F, int MODE, int LPR>
 int launch_gemv(const GemvArgs& ga, hipStream_t st) {
@@ -457,11 +480,15 @@ int launch_gemv(const GemvArgs& ga, hipStream_t st) {
     const int img = lds_image_bytes<F>(ga.K);
     const int gx = (ga.N + RPB - 1) / RPB;
     const int B = ga.B;
-#define WF_G(MBV) hipLaunchKernelGGL((k_gemv<F, MODE, LPR, MBV>), dim3(gx, B / MBV), dim3(256), (size_t)img * MBV, st, ga)
-    if (B % 8 == 0) WF_G(8);
-    else if (B % 4 == 0) WF_G(4);
-    else if (B % 2 == 0) WF_G(2);
-    else WF_G(1);
+#define WF_G(MBV, PPTV) \
+    hipLaunchKernelGGL((k_gemv<F, MODE, LPR, MBV, PPTV>), dim3(gx, B / MBV), dim3(256), (size_t)img * MBV, st, ga)
+    if (B == 1) {
+        if (norm_ppt(F::k_pad(ga.K)) == 2) WF_G(1, 2);
+        else WF_G(1, 4);
+    } else if (B % 8 == 0) WF_G(8, 0);
+    else if (B % 4 == 0) WF_G(4, 0);
+    else if (B % 2 == 0) WF_G(2, 0);
+    else WF_G(1, 0);
 #undef WF_G
     return check_launch("gemv");
 }
@@ -472,19 +499,33 @@ int launch_gemv_fmt(int fmt, const GemvArgs& ga, hipStream_t st) {
     return launch_gemv<FmtI2S, MODE, LPR>(ga, st);
 }
 
+// rows of x [B, xs] -> int8 codes in m->q8 (batch > 1), or bf16 into y16 (final norm)
+void launch_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, const uint16_t* nw, int K, uint16_t* y16,
+                    hipStream_t st) {
+    const wf_model_desc& d = m->d;
+    const bool big = norm_ppt(K) != 2;
+#define WF_RN(PPTV, Y)                                                                                            \
+    hipLaunchKernelGGL((k_rownorm<PPTV, Y>), dim3(d.batch), dim3(256), 0, st, x, xs, nw, K, d.eps, m->q8, m->q8_stride, \
+                       m->act_sf, m->act_sum, y16, (int64_t)K)
+    if (y16) {
+        if (big) WF_RN(4, true);
+        else WF_RN(2, true);
+    } else {
+        if (big) WF_RN(4, false);
+        else WF_RN(2, false);
+    }
+#undef WF_RN
+}
+
 GemvArgs base_args(const wf_model* m, int l) {
     const wf_model_desc& d = m->d;
     GemvArgs a{};
-    a.flags = d.debug_flags;
     a.eps = d.eps;
     a.B = d.batch;
     a.q8 = m->q8;
     a.q8_stride = m->q8_stride;
     a.act_sf = m->act_sf;
     a.act_sum = m->act_sum;
-    a.next_q8 = m->q8;
-    a.next_sf = m->act_sf;
-    a.next_asum = m->act_sum;
     a.Hq = d.n_heads;
     a.Hkv = d.n_kv_heads;
     a.S = d.max_seq;
@@ -498,52 +539,59 @@ GemvArgs base_args(const wf_model* m, int l) {
     return a;
 }
 
+// input row + norm weight of a GEMV; batch > 1 normalises them in a k_rownorm launch first
+int gemv_input(wf_model* m, GemvArgs& a, const uint16_t* x, int64_t xs, const uint16_t* nw, hipStream_t st) {
+    a.x = x;
+    a.x_stride = xs;
+    a.nw = nw;
+    if (m->d.batch > 1) {
+        launch_rownorm(m, x, xs, nw, a.K, nullptr, st);
+        return check_launch("rownorm");
+    }
+    return WF_OK;
+}
+
 // One op of the decode step (WF_OP_* in include/wf_bitnet.h).
 int run_op(wf_model* m, int l, int op, hipStream_t st) {
     const wf_model_desc& d = m->d;
     const int B = d.batch, H = d.hidden, I = d.inter, D = d.head_dim, S = d.max_seq;
     const float* wsh = d.wscale + 7 * l;  // host copy made at create time
     GemvArgs a = base_args(m, l);
+    int rc = WF_OK;
     switch (op) {
         case WF_OP_EMBED:
-            hipLaunchKernelGGL(k_embed_norm, dim3(B), dim3(256), 0, st, d.embed, m->tokens, H, d.vocab, m->h_a,
-                               m->positions, m->seq_lens, d.ln_in, d.eps, m->q8, m->q8_stride, m->act_sf, m->act_sum);
+            hipLaunchKernelGGL(k_embed, dim3(B), dim3(256), 0, st, d.embed, m->tokens, H, d.vocab, m->h_a, m->positions,
+                               m->seq_lens);
             break;
-        case WF_OP_QKV:
+        case WF_OP_QKV:  // rms_norm(input_layernorm)(h_a) -> q|k|v, RoPE, cache
             a.w = d.w_qkv + (int64_t)l * m->qkv_rows * wrow_bytes(d.wfmt, H);
             a.N = m->qkv_rows; a.K = H; a.ws0 = wsh[0]; a.ws1 = wsh[1]; a.ws2 = wsh[2];
             a.out = m->qbuf; a.out_stride = (int64_t)d.n_heads * D;
+            if ((rc = gemv_input(m, a, m->h_a, H, d.ln_in + (int64_t)l * H, st))) return rc;
             return launch_gemv_fmt<MODE_QKV, 16>(d.wfmt, a, st);
-        case WF_OP_ATTN: {
-            AttnNext nx{m->tickets + TK_ATTN2 * kTicketWords, d.attn_sub + (int64_t)l * H, d.eps, m->q8, m->q8_stride, m->act_sf,
-                        m->act_sum};
+        case WF_OP_ATTN:
             return decode_attention_impl(m->qbuf, WF_BF16, (int64_t)d.n_heads * D, D, a.kc, a.vc, WF_BF16,
                                          a.kv_b_stride, (int64_t)S * D, D, 1.f, 1.f, B, d.n_heads, d.n_kv_heads, D, S,
                                          m->seq_lens, 1.0f / sqrtf((float)D), m->attn, WF_BF16,
-                                         (int64_t)d.n_heads * D, D, m->attn_ws, st, &nx);
-        }
-        case WF_OP_O:  // h_b = h_a + o_proj(attn); last block: rms_norm(post_attention_layernorm)
+                                         (int64_t)d.n_heads * D, D, m->attn_ws, st);
+        case WF_OP_O:  // h_b = h_a + o_proj(rms_norm(attn_sub_norm)(attn))
             a.w = d.w_o + (int64_t)l * H * wrow_bytes(d.wfmt, H); a.N = H; a.K = H; a.ws0 = wsh[3];
             a.resid = m->h_a; a.out = m->h_b; a.out_stride = H;
-            a.ticket = m->tickets + TK_O * kTicketWords; a.next_nw = d.ln_post + (int64_t)l * H;
+            if ((rc = gemv_input(m, a, m->attn, H, d.attn_sub + (int64_t)l * H, st))) return rc;
             return launch_gemv_fmt<MODE_O, 16>(d.wfmt, a, st);
-        case WF_OP_GATE_UP:  // act = relu(gate)^2 * up; last block: rms_norm(ffn_sub_norm)
+        case WF_OP_GATE_UP:  // act = relu(gate)^2 * up of rms_norm(post_attention_layernorm)(h_b)
             a.w = d.w_gu + (int64_t)l * 2 * I * wrow_bytes(d.wfmt, H); a.N = 2 * I; a.K = H;
             a.ws0 = wsh[4]; a.ws1 = wsh[5]; a.out = m->act; a.out_stride = I;
-            a.ticket = m->tickets + TK_GU * kTicketWords; a.next_nw = d.ffn_sub + (int64_t)l * I;
+            if ((rc = gemv_input(m, a, m->h_b, H, d.ln_post + (int64_t)l * H, st))) return rc;
             return launch_gemv_fmt<MODE_GU, 16>(d.wfmt, a, st);
-        case WF_OP_DOWN:  // h_a = h_b + down(act); last block: next layer's input norm or the final norm
+        case WF_OP_DOWN:  // h_a = h_b + down(rms_norm(ffn_sub_norm)(act))
             a.w = d.w_d + (int64_t)l * H * wrow_bytes(d.wfmt, I); a.N = H; a.K = I; a.ws0 = wsh[6];
             a.resid = m->h_b; a.out = m->h_a; a.out_stride = H;
-            a.ticket = m->tickets + TK_DN * kTicketWords;
-            if (l + 1 < d.layers) {
-                a.next_nw = d.ln_in + (int64_t)(l + 1) * H;
-            } else {
-                a.next_nw = d.final_norm;
-                a.next_y16 = m->hn;
-            }
+            if ((rc = gemv_input(m, a, m->act, I, d.ffn_sub + (int64_t)l * I, st))) return rc;
             return launch_gemv_fmt<MODE_DN, 32>(d.wfmt, a, st);
-        case WF_OP_LM_HEAD: {
+        case WF_OP_LM_HEAD: {  // final norm -> hn, logits = hn @ embed^T, greedy token
+            launch_rownorm(m, m->h_a, H, d.final_norm, H, m->hn, st);
+            if ((rc = check_launch("final_norm"))) return rc;
             const size_t sh = (size_t)H * 2;
 #define WF_LM(MBV)                                                                                              \
     hipLaunchKernelGGL((k_lm_head<MBV>), dim3(m->lm_blocks, B / MBV), dim3(256), sh * MBV, st, d.embed, m->hn, \
@@ -581,7 +629,8 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_REQUIRE(d.hidden == d.n_heads * d.head_dim, "model_create: hidden != n_heads * head_dim");
     WF_REQUIRE(d.n_kv_heads > 0 && d.n_heads % d.n_kv_heads == 0 && d.n_heads / d.n_kv_heads <= 8, "model_create: bad GQA");
     WF_REQUIRE(d.hidden % 128 == 0 && d.inter % 128 == 0, "model_create: hidden/inter must be multiples of 128");
-    WF_REQUIRE(d.hidden <= 8192 && d.inter <= 8192, "model_create: hidden/inter > 8192 not supported");
+    WF_REQUIRE(k_pad(d.wfmt, d.hidden) <= 8192 && k_pad(d.wfmt, d.inter) <= 8192,
+               "model_create: hidden/inter (padded to the weight format) > 8192 not supported");
     WF_REQUIRE(d.batch >= 1 && d.batch <= 64 && d.max_seq >= 1 && d.vocab >= 1 && d.layers >= 1,
                "model_create: bad sizes (batch 1..64)");
     WF_REQUIRE(d.wfmt == WF_FMT_I2S || d.wfmt == WF_FMT_TQ, "model_create: bad weight format");
@@ -623,12 +672,12 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_ALLOC(m->q8, (size_t)B * m->q8_stride);
     WF_ALLOC(m->act_sf, sizeof(float) * B);
     WF_ALLOC(m->act_sum, sizeof(int) * B);
-    WF_ALLOC(m->tickets, sizeof(unsigned) * kTicketWords * (TK_ATTN2 + B));
+    WF_ALLOC(m->tickets, sizeof(unsigned) * kTicketWords * TK_COUNT);
     WF_ALLOC(m->attn_ws, ws_bytes);
     WF_ALLOC(m->am_part, sizeof(uint2) * B * m->lm_blocks);
 #undef WF_ALLOC
     // tickets start at zero; every launch re-arms the ones it uses
-    if ((e = hipMemset(m->tickets, 0, sizeof(unsigned) * kTicketWords * (TK_ATTN2 + B))) != hipSuccess) return fail(e);
+    if ((e = hipMemset(m->tickets, 0, sizeof(unsigned) * kTicketWords * TK_COUNT)) != hipSuccess) return fail(e);
     if ((e = hipMemset(m->attn_ws, 0, ws_bytes)) != hipSuccess) return fail(e);
     if ((e = hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking)) != hipSuccess) return fail(e);
     *out = m;

@@ -17,16 +17,20 @@ namespace wf {
 constexpr int kWave = 64;
 
 // ---------------------------------------------------------------------------------------------
-// bf16 <-> f32 (bit exact, round-to-nearest-even; NaN stays NaN like torch .to(bfloat16))
+// bf16 <-> f32 (bit exact, round-to-nearest-even like torch .to(bfloat16); NaN stays NaN).
+// gfx950 converts in hardware (v_cvt_pk_bf16_f32): no per-element branch for the NaN case.
 // ---------------------------------------------------------------------------------------------
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
-__device__ __forceinline__ uint16_t f2bf(float f) {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return (uint16_t)(u >> 16);
+__device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+// two floats -> packed bf16x2 (lo in bits 0..15), one instruction
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+    const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(uint32_t, v);
 }
 __device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 __device__ __forceinline__ float h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
 __device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
 
@@ -45,31 +49,60 @@ __device__ __forceinline__ void store_from_f32(void* p, int64_t i, int dt, float
 }
 
 // ---------------------------------------------------------------------------------------------
-// wave / block reductions (wave64)
+// wave / lane-group reductions (wave64) on DPP: quad_perm, row_half_mirror and row_mirror combine
+// lanes inside a 16-lane row (every lane ends with the same bits: each step adds two equal-order
+// partials), row_bcast:15/31 carry rows into lane 63 for a full-wave result (then v_readlane).
+// ~8 cycles per step instead of an LDS-latency ds_bpermute per step.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+enum : int { DPP_QP_1032 = 0xB1, DPP_QP_2301 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140,
+             DPP_BCAST15 = 0x142, DPP_BCAST31 = 0x143 };
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ int dpp_i(int v, int old = 0) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, ROW_MASK, 0xF, false);
+}
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dpp_f(float v, float old = 0.f) {
+    return __int_as_float(dpp_i<CTRL, ROW_MASK>(__float_as_int(v), __float_as_int(old)));
+}
+template <int CTRL, int ROW_MASK = 0xF, class T>
+__device__ __forceinline__ T dpp_cast(T v, T old = T(0)) {
+    if constexpr (__is_same(T, float)) return dpp_f<CTRL, ROW_MASK>(v, old);
+    else return dpp_i<CTRL, ROW_MASK>(v, old);
+}
+struct OpAdd {
+    template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return a + b; }
+};
+struct OpMax {
+    __device__ __forceinline__ float operator()(float a, float b) const { return fmaxf(a, b); }
+};
+// Reduce over aligned groups of G lanes (G in 1..64); every lane of the group gets the result.
+template <int G, class T, class Op>
+__device__ __forceinline__ T group_reduce(T v, Op op) {
+    static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "group size");
+    if constexpr (G >= 2) v = op(v, dpp_cast<DPP_QP_1032>(v));
+    if constexpr (G >= 4) v = op(v, dpp_cast<DPP_QP_2301>(v));
+    if constexpr (G >= 8) v = op(v, dpp_cast<DPP_HALF_MIRROR>(v));
+    if constexpr (G >= 16) v = op(v, dpp_cast<DPP_MIRROR>(v));
+    if constexpr (G >= 32) v = op(v, __shfl_xor(v, 16, 64));
+    if constexpr (G >= 64) v = op(v, __shfl_xor(v, 32, 64));
     return v;
 }
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+// Full-wave reduction, result uniform (scalar) in every lane: rows -> lane 63 -> readlane.
+template <class T, class Op>
+__device__ __forceinline__ T wave_reduce(T v, Op op, T ident) {
+    v = group_reduce<16>(v, op);
+    v = op(v, dpp_cast<DPP_BCAST15, 0xA>(v, ident));
+    v = op(v, dpp_cast<DPP_BCAST31, 0xC>(v, ident));
+    if constexpr (sizeof(T) == 4 && __is_same(T, float))
+        return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+    else
+        return __builtin_amdgcn_readlane(v, 63);
 }
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
+__device__ __forceinline__ float wave_max(float v) { return wave_reduce(v, OpMax{}, -INFINITY); }
+__device__ __forceinline__ float wave_sum(float v) { return wave_reduce(v, OpAdd{}, 0.f); }
+__device__ __forceinline__ int wave_sum_i(int v) { return wave_reduce(v, OpAdd{}, 0); }
 // Reduce across the 16 lanes of a 16-lane group.
-__device__ __forceinline__ int group16_sum_i(int v) {
-    v += __shfl_xor(v, 8, 64);
-    v += __shfl_xor(v, 4, 64);
-    v += __shfl_xor(v, 2, 64);
-    v += __shfl_xor(v, 1, 64);
-    return v;
-}
+__device__ __forceinline__ int group16_sum_i(int v) { return group_reduce<16>(v, OpAdd{}); }
 
 // Block-wide reductions over blockDim.x (multiple of 64, <= 1024). `red` is >= 16 floats of LDS.
 __device__ __forceinline__ float block_max(float v, float* red) {
@@ -118,6 +151,33 @@ __device__ __forceinline__ int8_t quant_one(float x, float sf) {
     float v = rintf(x / sf);
     v = fminf(fmaxf(v, -128.f), 127.f);
     return (int8_t)(int)v;
+}
+// Eight codes at once, bit-identical to quant_one: t = x * (1/s) is within 3 * 2^-17 of the
+// correctly rounded quotient for |x/s| <= 128, so rint(t) is the reference code unless t lies
+// within 2^-13 of a half-integer; only then (p ~ 2.4e-4 per element) the lane redoes the
+// IEEE divide. Returns the 8 codes packed little-endian; adds them to `asum`.
+__device__ __forceinline__ uint2 quant8(const float (&x)[8], float sf, float inv, int& asum) {
+    float q[8];
+    bool risky = false;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float t = x[j] * inv;
+        q[j] = rintf(t);
+        risky |= fabsf(t - q[j]) > 0.4998779296875f;  // 0.5 - 2^-13
+    }
+    if (risky) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) q[j] = rintf(x[j] / sf);
+    }
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int c = (int)fminf(fmaxf(q[j], -128.f), 127.f);
+        asum += c;
+        if (j < 4) lo |= ((uint32_t)c & 0xffu) << (8 * j);
+        else hi |= ((uint32_t)c & 0xffu) << (8 * (j - 4));
+    }
+    return make_uint2(lo, hi);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -1,13 +1,12 @@
-// wf_norm.h -- block-level RMSNorm + int8 activation quantizer and the in-launch hand-off helpers
-// used by the fused decode step (gfx950).
+// wf_norm.h -- block-level RMSNorm + int8 activation quantizer, the in-launch hand-off helpers
+// (launch tickets) and the diagnostic stamp facility of the fused decode step (gfx950).
 //
-// The decode step runs each op's "rms_norm -> quantize" exactly once per token: the LAST block of
-// the producing kernel (per-launch ticket) normalises the full output vector and publishes
-// int8 codes + scale + code sum for the consumer GEMV, which then only stages the int8 image.
-// Hand-off protocol (MI355X_MICROARCH.md, Valid forms row 1): every block stores its slice of the
-// vector write-through (sc1), drains (s_waitcnt vmcnt(0)) in every storing wave, meets at a
-// barrier, one lane bumps an agent-scope ticket; the block whose add returns n-1 reads the vector
-// with sc1 loads, computes, and re-arms the ticket for the next launch.
+// At batch 1 every GEMV block normalises + quantises its input row itself, straight into its LDS
+// activation image, while its first weight chunks are in flight (k_gemv's prologue); at larger
+// batch one k_rownorm launch does it once per row. Hand-off protocol of the launch tickets
+// (MI355X_MICROARCH.md, Valid forms row 1): every block stores write-through (sc1), drains
+// (s_waitcnt vmcnt(0)) in every storing wave, meets at a barrier, one lane bumps an agent-scope
+// ticket; the block whose add returns n-1 reads with sc1 loads and re-arms the ticket.
 #pragma once
 #include "wf_device.h"
 
@@ -70,113 +69,125 @@ __device__ __forceinline__ void ticket_rearm(unsigned* t) {
     if (threadIdx.x == 0) st_sc1(t + kTicketShards, 0u);
 }
 
-// Where a normalised row goes: int8 codes + float scale + exact code sum (for the next ternary
-// GEMV), or bf16 (final norm feeding the LM head).
-struct NormOut {
-    int8_t* q8;      // [K] int8, or nullptr
-    float* sf;       // float(s), s = double(max|y|)/127
-    int* asum;       // sum of the codes
-    uint16_t* y16;   // [K] bf16 normalised row (final norm), or nullptr
-};
+// Diagnostic build only (make stamps -> lib/libwfbitnet_stamps.so): thread 0 of every block records
+// the 100 MHz wall clock (s_memrealtime) at named points; read back with wf_debug_stamps_<tu>().
+// In the product build WF_STAMP compiles to nothing.
+#ifdef WF_STAMPS
+constexpr int kStampSlots = 16;
+constexpr int kStampBlocks = 16384;
+static __device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
+#define WF_STAMP(i)                                                                         \
+    do {                                                                                    \
+        if (threadIdx.x == 0) {                                                             \
+            const unsigned sb_ = ::wf::linear_block_id();                                    \
+            if (sb_ < (unsigned)::wf::kStampBlocks)                                          \
+                ::wf::g_stamps[sb_ * ::wf::kStampSlots + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                                   \
+    } while (0)
+#define WF_STAMP_READER(NAME)                                                                     \
+    extern "C" int NAME(void* host, int n_words, int reset) {                                     \
+        const size_t nb = sizeof(unsigned long long) * (size_t)::wf::kStampBlocks * ::wf::kStampSlots; \
+        if (reset) return (int)hipMemset(::wf::g_stamps_addr(), 0, nb);                           \
+        size_t b = sizeof(unsigned long long) * (size_t)n_words;                                   \
+        if (b > nb) b = nb;                                                                        \
+        return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(::wf::g_stamps), b, 0, hipMemcpyDeviceToHost); \
+    }
+inline void* g_stamps_addr() {
+    void* p = nullptr;
+    (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamps));
+    return p;
+}
+#else
+#define WF_STAMP(i) \
+    do {            \
+    } while (0)
+#define WF_STAMP_READER(NAME)
+#endif
 
-constexpr int kNormMaxPieces = 4;  // 8-element pieces per thread: K <= 4 * 8 * 256 = 8192
+// ---------------------------------------------------------------------------------------------
+// rms_norm -> int8 activation quantizer for one row, 256 threads, 8-element pieces
+// (p = threadIdx.x + 256 * i, i < PPT). Float sequence of the reference
+// (scripts/direct_inference_full.py:181-184, tests/test_bitnet_core.py:139-146):
+//   r = bf16(1 / sqrt(mean(x^2) + eps)); y = bf16(bf16(x * r) * w)
+//   s = double(max|y|) / 127 (1/127 if max < 1e-6); q = clamp(rne(y / float(s)), -128, 127)
+// Loads are issued unconditionally (clamped index, masked in the arithmetic) so the caller can
+// put its own loads behind them and hipcc counts vmcnt exactly.
+// ---------------------------------------------------------------------------------------------
+constexpr int kNT = 256;  // threads per block of every decode-step kernel
 
-// One block (256 threads) normalises one row: y = bf16(bf16(x * r) * w), r = bf16(1/sqrt(mean(x^2)
-// + eps)) (scripts/direct_inference_full.py:181-184), then q = clamp(rne(y / float(s)), -128, 127)
-// with s = max|y| / 127 in double (tests/test_bitnet_core.py:139-146). `red` >= 48 floats of LDS.
-// SC1: read x with sc1 loads (x was written by other blocks of this launch).
-template <bool SC1>
-__device__ void norm_quant_row(const uint16_t* __restrict__ x, const uint16_t* __restrict__ nw, int K, float eps,
-                               NormOut o, float* red) {
-    const int nwv = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int np = K / 8;
-    uint4 xr[kNormMaxPieces], wr[kNormMaxPieces];
-    __amdgpu_buffer_rsrc_t rs = make_rsrc(x);
+template <int PPT>
+struct NormRow {
+    uint4 x[PPT], w[PPT];
+    __device__ __forceinline__ void issue(const uint16_t* __restrict__ xrow, const uint16_t* __restrict__ nw, int K) {
+        const int npk = K >> 3;
 #pragma unroll
-    for (int i = 0; i < kNormMaxPieces; ++i) {
-        const int p = threadIdx.x + i * blockDim.x;
-        xr[i] = make_uint4(0, 0, 0, 0);
-        wr[i] = make_uint4(0, 0, 0, 0);
-        if (p < np) {
-            xr[i] = SC1 ? ld16_sc1(rs, p * 16) : *reinterpret_cast<const uint4*>(x + 8 * p);
-            wr[i] = *reinterpret_cast<const uint4*>(nw + 8 * p);
+        for (int i = 0; i < PPT; ++i) {
+            const int p = min((int)threadIdx.x + kNT * i, npk - 1);
+            x[i] = *reinterpret_cast<const uint4*>(xrow + 8 * p);
+            w[i] = *reinterpret_cast<const uint4*>(nw + 8 * p);
         }
     }
-    float xv[kNormMaxPieces][8];
+};
+
+// Normalises the row held in `r`; returns the bf16-rounded y values in `y` (0 for pieces >= K/8)
+// and the quantizer's float scale. `red` = 8 floats of LDS (two barriers inside).
+template <int PPT>
+__device__ __forceinline__ float norm_row(const NormRow<PPT>& r, int K, float eps, float (&y)[PPT][8], float* red,
+                                          bool want_scale = true) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int npk = K >> 3;
     float ss = 0.f;
 #pragma unroll
-    for (int i = 0; i < kNormMaxPieces; ++i) {
-        const uint32_t w4[4] = {xr[i].x, xr[i].y, xr[i].z, xr[i].w};
+    for (int i = 0; i < PPT; ++i) {
+        const bool valid = (int)threadIdx.x + kNT * i < npk;
+        const uint32_t w4[4] = {r.x[i].x, r.x[i].y, r.x[i].z, r.x[i].w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            xv[i][2 * j] = __uint_as_float(w4[j] << 16);
-            xv[i][2 * j + 1] = __uint_as_float(w4[j] & 0xffff0000u);
+            y[i][2 * j] = valid ? bf_lo(w4[j]) : 0.f;
+            y[i][2 * j + 1] = valid ? bf_hi(w4[j]) : 0.f;
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ss = fmaf(xv[i][j], xv[i][j], ss);
+        for (int j = 0; j < 8; ++j) ss = fmaf(y[i][j], y[i][j], ss);
     }
     ss = wave_sum(ss);
     if (lane == 0) red[wave] = ss;
     __syncthreads();
-    ss = red[0];
-    for (int i = 1; i < nwv; ++i) ss += red[i];
-    const float r = rbf(1.0f / sqrtf(ss / (float)K + eps));
+    ss = (red[0] + red[1]) + (red[2] + red[3]);
+    const float rr = rbf(1.0f / sqrtf(ss / (float)K + eps));
     float mx = 0.f;
 #pragma unroll
-    for (int i = 0; i < kNormMaxPieces; ++i) {
-        const uint32_t n4[4] = {wr[i].x, wr[i].y, wr[i].z, wr[i].w};
+    for (int i = 0; i < PPT; ++i) {
+        const uint32_t n4[4] = {r.w[i].x, r.w[i].y, r.w[i].z, r.w[i].w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float wv = (j & 1) ? __uint_as_float(n4[j >> 1] & 0xffff0000u) : __uint_as_float(n4[j >> 1] << 16);
-            xv[i][j] = rbf(rbf(xv[i][j] * r) * wv);
-            mx = fmaxf(mx, fabsf(xv[i][j]));
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t a = pk_bf16(y[i][2 * j] * rr, y[i][2 * j + 1] * rr);
+            const uint32_t b = pk_bf16(bf_lo(a) * bf_lo(n4[j]), bf_hi(a) * bf_hi(n4[j]));
+            y[i][2 * j] = bf_lo(b);
+            y[i][2 * j + 1] = bf_hi(b);
+            mx = fmaxf(mx, fmaxf(fabsf(y[i][2 * j]), fabsf(y[i][2 * j + 1])));
         }
     }
-    if (o.y16) {  // final norm: bf16 row out, no quantization
-#pragma unroll
-        for (int i = 0; i < kNormMaxPieces; ++i) {
-            const int p = threadIdx.x + i * blockDim.x;
-            if (p < np) {
-                uint32_t pk[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) pk[j] = (uint32_t)f2bf(xv[i][2 * j]) | ((uint32_t)f2bf(xv[i][2 * j + 1]) << 16);
-                *reinterpret_cast<uint4*>(o.y16 + 8 * p) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-            }
-        }
-        __syncthreads();  // red[] is reused by the caller's next row
-        return;
-    }
+    if (!want_scale) return 0.f;
     mx = wave_max(mx);
-    if (lane == 0) red[16 + wave] = mx;
+    if (lane == 0) red[4 + wave] = mx;
     __syncthreads();
-    mx = red[16];
-    for (int i = 1; i < nwv; ++i) mx = fmaxf(mx, red[16 + i]);
-    const float sf = (float)act_scale_from_max(mx);
+    mx = fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7]));
+    return (float)act_scale_from_max(mx);
+}
+
+// Quantizes the normalised pieces; piece p (< npad = padded K / 8) goes to dst + off(p). Returns
+// this thread's code sum (the caller reduces it).
+template <int PPT, class Off>
+__device__ __forceinline__ int quant_row(const float (&y)[PPT][8], float sf, int npad, int8_t* dst, Off off) {
+    const float inv = 1.0f / sf;
     int asum = 0;
 #pragma unroll
-    for (int i = 0; i < kNormMaxPieces; ++i) {
-        const int p = threadIdx.x + i * blockDim.x;
-        if (p < np) {
-            uint32_t pk[2] = {0u, 0u};
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int8_t q = quant_one(xv[i][j], sf);
-                asum += q;
-                pk[j >> 2] |= (uint32_t)(uint8_t)q << (8 * (j & 3));
-            }
-            *reinterpret_cast<uint2*>(o.q8 + 8 * p) = make_uint2(pk[0], pk[1]);
-        }
+    for (int i = 0; i < PPT; ++i) {
+        const int p = (int)threadIdx.x + kNT * i;
+        const uint2 q = quant8(y[i], sf, inv, asum);
+        if (p < npad) *reinterpret_cast<uint2*>(dst + off(p)) = q;
     }
-    asum = wave_sum_i(asum);
-    int* redi = reinterpret_cast<int*>(red + 32);
-    if (lane == 0) redi[wave] = asum;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int t = 0;
-        for (int i = 0; i < nwv; ++i) t += redi[i];
-        *o.asum = t;
-        *o.sf = sf;
-    }
+    return asum;
 }
 
 }  // namespace wf
