@@ -140,6 +140,31 @@ def test_quantize_golden_bitexact():
         assert np.array_equal(qb.cpu().numpy(), qo) and sb == so
 
 
+def test_quantize_half_integer_boundaries(orc):
+    """The fast quantizer (quant8: x * (1/s) with an exact-divide fallback near x.5, used by every
+    decode-step GEMV prologue) against the oracle's IEEE divide on inputs packed around the
+    rounding boundaries x/s = k + 0.5 (tests/test_bitnet_core.py:139-146 semantics), bit-exact."""
+    from wfamd import ops
+    m = np.float32(3.7)
+    sf = np.float32(np.float64(m) / 127.0)
+    k = np.arange(-127, 127, dtype=np.float64) + 0.5
+    vals = [np.float32(m), -np.float32(m)]
+    for rel in (-3, -2, -1, 0, 1, 2, 3):
+        base = (k * np.float64(sf)).astype(np.float32)
+        vals.append(np.nextafter(base, np.float32(np.inf) * np.sign(rel)) if rel else base)
+        for _ in range(abs(rel) - 1):
+            vals[-1] = np.nextafter(vals[-1], np.float32(np.inf) * np.sign(rel))
+    x = np.concatenate([np.atleast_1d(v) for v in vals]).astype(np.float32)
+    x = x[np.abs(x) <= m]
+    pad = (-x.size) % 8
+    x = np.concatenate([x, np.zeros(pad + 8, np.float32)])  # 8-wide body + scalar tail both run
+    x = np.concatenate([x, np.float32([0.25, -0.5, 1.0])])
+    q, s = ops.quantize_activations_i8(cu(x))
+    qo, so = orc.quantize_i8(x)
+    assert s == so
+    assert np.array_equal(q.cpu().numpy(), qo)
+
+
 def test_quantize_rows_vs_oracle(orc):
     from wfamd import ops
     x = np.random.default_rng(3).standard_normal((7, 2560)).astype(np.float32) * 5

@@ -26,10 +26,11 @@ import torch  # noqa: E402
 from wfamd import WF_FMT_I2S, WF_FMT_TQ, _lib  # noqa: E402
 from wfamd.model import BITNET_2B, BitNetDecoder, synthetic_weights  # noqa: E402
 
-SLOTS, NBLK = 16, 16384
+SLOTS, NBLK = 80, 16384  # wave 0 uses columns 0..15 (wf_norm.h)
 NAMES = {  # slot names per kernel kind (WF_STAMP(i) in csrc/)
-    "gemv": ["entry", "image", "dot", "out", "-", "-", "-", "qkv_out"] + ["-"] * 8,
-    "attn": ["entry", "scores", "merged", "ticket", "fold", "out", "-", "-"] + ["-"] * 8,
+    "gemv": ["entry", "image", "dot", "out", "-", "-", "-", "qkv_out", "p_ss", "p_r", "p_y", "p_sf", "p_q", "w_landed",
+             "-", "-"],
+    "attn": ["entry", "kv_done", "out", "-", "-", "-", "-", "-"] + ["-"] * 8,
     "lm": ["entry", "staged", "dot", "ticket", "argmax", "-", "-", "-"] + ["-"] * 8,
 }
 
@@ -47,12 +48,13 @@ def reset(lib):
 
 
 def summarize(st, kind, tail_slot):
+    """st: [NBLK, SLOTS]; block (x, y, z) of a launch sits in row x + 2048 y + 8192 z (wf_norm.h)."""
     live = st[:, 0] > 0
     st = st[live].astype(np.int64)
     t0 = st[:, 0].min()
     rel = (st - t0) * 0.01  # 100 MHz -> us
     out = {"blocks": int(live.sum())}
-    for s, name in enumerate(NAMES[kind]):
+    for s, name in enumerate(NAMES[kind][:16]):
         if name == "-":
             continue
         col = rel[st[:, s] > 0, s]
@@ -62,7 +64,7 @@ def summarize(st, kind, tail_slot):
     tails = np.nonzero(st[:, tail_slot] > 0)[0]
     if tails.size:
         i = tails[0]
-        out["tail_block"] = {NAMES[kind][s]: round(float(rel[i, s]), 2) for s in range(SLOTS)
+        out["tail_block"] = {NAMES[kind][s]: round(float(rel[i, s]), 2) for s in range(16)
                              if st[i, s] > 0 and NAMES[kind][s] != "-"}
     return out
 
@@ -74,6 +76,8 @@ def main():
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--layer", type=int, default=5)
+    ap.add_argument("--warm", action="store_true",
+                    help="launch the same op of layer-1 right before (code and inputs warm, weights cold)")
     args = ap.parse_args()
     lib = _lib.load()
     for fn in ("wf_debug_stamps_decode", "wf_debug_stamps_attn"):
@@ -89,7 +93,7 @@ def main():
         dec.step(graph=False)
     torch.cuda.synchronize()
     flush = torch.empty(384 << 20, dtype=torch.uint8, device="cuda")
-    ops = [(_lib.WF_OP_QKV, "qkv", "gemv", "decode", 7), (_lib.WF_OP_ATTN, "attn", "attn", "attn", 5),
+    ops = [(_lib.WF_OP_QKV, "qkv", "gemv", "decode", 7), (_lib.WF_OP_ATTN, "attn", "attn", "attn", 2),
            (_lib.WF_OP_O, "o_proj", "gemv", "decode", 3), (_lib.WF_OP_GATE_UP, "gate_up", "gemv", "decode", 3),
            (_lib.WF_OP_DOWN, "down", "gemv", "decode", 3), (_lib.WF_OP_LM_HEAD, "lm_head", "lm", "decode", 4)]
     res = {}
@@ -100,6 +104,8 @@ def main():
             reset(lib)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            if args.warm:
+                dec.launch_op(args.layer - 1, op)
             e0.record()
             dec.launch_op(args.layer, op)
             e1.record()

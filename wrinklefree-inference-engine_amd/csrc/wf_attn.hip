@@ -106,7 +106,7 @@ __device__ __forceinline__ void store_out4(void* out, int64_t off, int odt, cons
 // issues every (m, l) and o load of its share of the splits at once (one round trip), folds them
 // with an online max, and combines the thread subsets through LDS. The last arriver also re-arms
 // the ticket for the next launch.
-template <int D, int G, int KVDT>
+template <int D, int G, int KVDT, int U = kAttnU>
 __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
     const void* __restrict__ q, int qdt, int64_t q_sb, int64_t q_sh, const void* __restrict__ K,
     const void* __restrict__ V, int64_t kv_sb, int64_t kv_sh, int64_t kv_st, float k_scale, float v_scale, int Hq,
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
     float* __restrict__ part, void* __restrict__ out, int odt, int64_t o_sb, int64_t o_sh) {
     constexpr int LP = D / 8;                // lanes per key position
     constexpr int NG = kAttnThreads / LP;    // lane groups per block
-    constexpr int T = kAttnU * NG;
+    constexpr int T = U * NG;
     const int s = blockIdx.x, g = blockIdx.y, b = blockIdx.z;
     const int grp = Hq / Hkv;
     const int gid = threadIdx.x / LP, li = threadIdx.x % LP;
@@ -151,16 +151,16 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
                 for (int j = 0; j < 8; ++j) qv[h][j] = load_as_f32(q, qo + j, qdt);
             }
         }
-        KVRaw<KVDT> kr[kAttnU], vr[kAttnU];
+        KVRaw<KVDT> kr[U], vr[U];
 #pragma unroll
-        for (int u = 0; u < kAttnU; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int t = min(t0 + gid + NG * u, Sb - 1);
             kr[u].load(K, kvb + t * kv_st);
             vr[u].load(V, kvb + t * kv_st);
         }
-        float sc[kAttnU][G];
+        float sc[U][G];
 #pragma unroll
-        for (int u = 0; u < kAttnU; ++u) {
+        for (int u = 0; u < U; ++u) {
             float kx[8];
             kr[u].decode(k_scale, kx);
             const bool valid = t0 + gid + NG * u < Sb;
@@ -178,11 +178,11 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
         for (int h = 0; h < G; ++h) {
             float mx = sc[0][h];
 #pragma unroll
-            for (int u = 1; u < kAttnU; ++u) mx = fmaxf(mx, sc[u][h]);
+            for (int u = 1; u < U; ++u) mx = fmaxf(mx, sc[u][h]);
             m[h] = mx;
         }
 #pragma unroll
-        for (int u = 0; u < kAttnU; ++u) {
+        for (int u = 0; u < U; ++u) {
             float vx[8];
             vr[u].decode(v_scale, vx);
 #pragma unroll
@@ -309,6 +309,155 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
     }
     if (threadIdx.x == 0) st_sc1(cnt + b * Hkv + g, 0u);  // re-arm the ticket for the next launch
     WF_STAMP(5);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Decode-step attention partials: bf16 q/K/V, D = 128, kAttnPartSplits splits per (b, kv head)
+// whatever the context: split s of a sequence with Sb keys covers [s*T, min((s+1)*T, Sb)) with
+// T = round_up(ceil(Sb / kAttnPartSplits), 16), walked in chunks of 128 keys (8 per lane group,
+// every load of a chunk in flight at once) with an online softmax. The block writes, per query
+// head of its group, (m, l) to ml[b][hq][s] and the unnormalised o to o[b][hq][s][D]; an empty
+// split writes (-inf, 0) and zeros. The consumer (wf_norm.h AttnRow, the O projection's
+// prologue or k_rownorm_attn) reads a fixed number of records, so it needs no sequence length
+// and issues every load before its weight stream.
+// ---------------------------------------------------------------------------------------------
+template <int G>
+__global__ __launch_bounds__(kAttnThreads) void k_attn_part(const uint16_t* __restrict__ q, int64_t q_sb,
+                                                            const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+                                                            int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv, int S,
+                                                            const int32_t* __restrict__ seq_lens, float sm_scale,
+                                                            float2* __restrict__ ml_out, float* __restrict__ o_out) {
+    constexpr int D = 128, LP = D / 8, NG = kAttnThreads / LP, U = 8, CH = U * NG;  // 128 keys per chunk
+    const int s = blockIdx.x, g = blockIdx.y, b = blockIdx.z;
+    const int grp = Hq / Hkv;
+    const int gid = threadIdx.x / LP, li = threadIdx.x % LP;
+    const int Sb = min(seq_lens[b], S);
+    const int T = ((Sb + kAttnPartSplits - 1) / kAttnPartSplits + 15) / 16 * 16;
+    const int t0 = s * T, t1 = min(t0 + T, Sb);
+    WF_STAMP(0);
+    __shared__ float sm_m[NG][G], sm_l[NG][G];
+    __shared__ __attribute__((aligned(16))) float sm_o[NG][G][D];
+
+    float m[G], l[G], o[G][8];
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+        m[h] = -INFINITY;
+        l[h] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[h][j] = 0.f;
+    }
+    if (t0 < t1) {
+        float qv[G][8];
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            const uint4 r = *reinterpret_cast<const uint4*>(q + b * q_sb + (int64_t)(g * grp + min(h, grp - 1)) * D + li * 8);
+            const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { qv[h][2 * i] = bf_lo(w[i]); qv[h][2 * i + 1] = bf_hi(w[i]); }
+        }
+        const int64_t kvb = b * kv_sb + g * kv_sh + li * 8;
+        for (int c0 = t0; c0 < t1; c0 += CH) {
+            uint4 kr[U], vr[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = min(c0 + gid + NG * u, t1 - 1);
+                kr[u] = *reinterpret_cast<const uint4*>(K + kvb + (int64_t)t * D);
+                vr[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)t * D);
+            }
+            float sc[U][G];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t w[4] = {kr[u].x, kr[u].y, kr[u].z, kr[u].w};
+                const bool valid = c0 + gid + NG * u < t1;
+#pragma unroll
+                for (int h = 0; h < G; ++h) {
+                    float d = 0.f;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        d = fmaf(qv[h][2 * i], bf_lo(w[i]), d);
+                        d = fmaf(qv[h][2 * i + 1], bf_hi(w[i]), d);
+                    }
+                    d = group_reduce<LP>(d, OpAdd{});
+                    sc[u][h] = valid ? d * sm_scale : -INFINITY;
+                }
+            }
+#pragma unroll
+            for (int h = 0; h < G; ++h) {
+                float mx = m[h];
+#pragma unroll
+                for (int u = 0; u < U; ++u) mx = fmaxf(mx, sc[u][h]);
+                const float a = (mx == -INFINITY) ? 1.f : __expf(m[h] - mx);  // no key yet: nothing to rescale
+                l[h] *= a;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o[h][j] *= a;
+                m[h] = mx;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t w[4] = {vr[u].x, vr[u].y, vr[u].z, vr[u].w};
+                float vx[8];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) { vx[2 * i] = bf_lo(w[i]); vx[2 * i + 1] = bf_hi(w[i]); }
+#pragma unroll
+                for (int h = 0; h < G; ++h) {
+                    const float p = (sc[u][h] == -INFINITY) ? 0.f : __expf(sc[u][h] - m[h]);
+                    l[h] += p;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) o[h][j] = fmaf(p, vx[j], o[h][j]);
+                }
+            }
+        }
+    }
+    WF_STAMP(1);
+    if (li == 0) {
+#pragma unroll
+        for (int h = 0; h < G; ++h) { sm_m[gid][h] = m[h]; sm_l[gid][h] = l[h]; }
+    }
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+        *reinterpret_cast<float4*>(&sm_o[gid][h][li * 8]) = make_float4(o[h][0], o[h][1], o[h][2], o[h][3]);
+        *reinterpret_cast<float4*>(&sm_o[gid][h][li * 8 + 4]) = make_float4(o[h][4], o[h][5], o[h][6], o[h][7]);
+    }
+    __syncthreads();
+    constexpr int D4 = D / 4;
+    for (int idx = threadIdx.x; idx < grp * D4; idx += kAttnThreads) {
+        const int h = idx / D4, d = (idx - h * D4) * 4;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < NG; ++w) mx = fmaxf(mx, sm_m[w][h]);
+        float ls = 0.f, os[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int w = 0; w < NG; ++w) {
+            const float a = (sm_m[w][h] == -INFINITY) ? 0.f : __expf(sm_m[w][h] - mx);
+            ls += sm_l[w][h] * a;
+            const float4 ov = *reinterpret_cast<const float4*>(&sm_o[w][h][d]);
+            os[0] += ov.x * a; os[1] += ov.y * a; os[2] += ov.z * a; os[3] += ov.w * a;
+        }
+        const int64_t rec = (int64_t)(b * Hq + g * grp + h) * kAttnPartSplits + s;
+        *reinterpret_cast<float4*>(o_out + rec * D + d) = make_float4(os[0], os[1], os[2], os[3]);
+        if (d == 0) ml_out[rec] = make_float2(mx, ls);
+    }
+    WF_STAMP(2);
+}
+
+int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
+                              int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
+                              float2* ml, float* o, hipStream_t st) {
+    const dim3 grid(kAttnPartSplits, Hkv, B);
+    const int grp = Hq / Hkv;
+#define WF_AP(GV)                                                                                                   \
+    hipLaunchKernelGGL((k_attn_part<GV>), grid, dim3(kAttnThreads), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, \
+                       seq_lens, sm_scale, ml, o)
+    if (grp == 1) WF_AP(1);
+    else if (grp == 2) WF_AP(2);
+    else if (grp <= 4) WF_AP(4);
+    else if (grp <= 8) WF_AP(8);
+    else {
+        set_error("decode_attention_partials: GQA group %d > 8", grp);
+        return WF_EINVAL;
+    }
+#undef WF_AP
+    return check_launch("decode_attention_partials");
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -25,13 +25,11 @@
 #include "wf_norm.h"
 
 namespace wf {
-int decode_attention_impl(const void* q, int q_dtype, int64_t q_sb, int64_t q_sh, const void* k, const void* v,
-                          int kv_dtype, int64_t kv_sb, int64_t kv_sh, int64_t kv_st, float k_scale, float v_scale, int B,
-                          int Hq, int Hkv, int D, int S, const int32_t* seq_lens, float sm_scale, void* out,
-                          int out_dtype, int64_t o_sb, int64_t o_sh, void* ws, hipStream_t st);
+int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
+                              int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
+                              float2* ml, float* o, hipStream_t st);
 
 enum { MODE_QKV = 0, MODE_O = 1, MODE_GU = 2, MODE_DN = 3 };
-constexpr int kPrefetch = 4;  // 16-byte weight chunks in flight per lane
 
 struct GemvArgs {
     // input row(s): bf16 x + norm weight (PPT > 0: normalised + quantised in the block prologue)
@@ -39,6 +37,9 @@ struct GemvArgs {
     int64_t x_stride;
     const uint16_t* nw;
     float eps;
+    // MODE_O: the attention row comes from the decode-attention partials (wf_norm.h AttnRow)
+    const float2* part_ml;
+    const float* part_o;
     // or int8 codes from k_rownorm (PPT == 0)
     const int8_t* q8;          // [B, q8_stride]
     int64_t q8_stride;
@@ -77,6 +78,9 @@ template <class F, int MODE, int LPR, int MB, int PPT>
 __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     static_assert(PPT == 0 || MB == 1, "the norm prologue handles one activation row");
     constexpr int RPB = 256 / LPR;
+    // 16-byte weight chunks in flight per lane (K = 2560: 2 per lane at LPR 16, 4 at LPR 8;
+    // K = 6912 at LPR 16: 6)
+    constexpr int kPrefetch = (MODE == MODE_DN || LPR <= 8) ? 8 : 4;
     extern __shared__ __attribute__((aligned(16))) int8_t smem[];
     __shared__ float red[8];
     __shared__ int red_i[4];
@@ -92,10 +96,15 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
 
     // 1) the input row (issued first: vmcnt retires in order), 2) the weight stream, 3) residual
     NormRow<PPT == 0 ? 1 : PPT> nr;
+    constexpr bool kAttnIn = (MODE == MODE_O && PPT > 0);
+    AttnRow<kAttnIn ? PPT : 1> ar;
     constexpr int kMaxPiecesPerThread = 2;  // staged int8: K_pad <= 8192
     uint4 apre[MB][kMaxPiecesPerThread];
     const int pieces16 = F::k_pad(K) / 16;
-    if constexpr (PPT > 0) {
+    if constexpr (kAttnIn) {
+        ar.issue(a.part_ml, a.part_o, b0, a.Hq, 128);
+        nr.issue_w(a.nw, K);
+    } else if constexpr (PPT > 0) {
         nr.issue(a.x + (int64_t)b0 * a.x_stride, a.nw, K);
     } else {
 #pragma unroll
@@ -113,18 +122,34 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
 #pragma unroll
     for (int u = 0; u < kPrefetch; ++u)  // clamped (no branch): lanes past the row re-read its last chunk
         wpre[u] = ldg_nt(wr + (int64_t)min(LPR * u + sub, C - 1) * 16);
-    float resid[MB];
+    // residual: unconditional (clamped) load -- a load under a lane condition makes hipcc wait
+    // vmcnt(0) right there, i.e. for the whole weight prefetch before the prologue can start
+    uint16_t resid_raw[MB];
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
-        resid[m] = 0.f;
+        resid_raw[m] = 0;
         if constexpr (MODE == MODE_O || MODE == MODE_DN)
-            if (sub == 0 && row < N) resid[m] = bf2f(a.resid[(int64_t)(b0 + m) * a.out_stride + row]);
+            resid_raw[m] = a.resid[(int64_t)(b0 + m) * a.out_stride + min(row, N - 1)];
     }
+    // every load above is in flight before any input-stage arithmetic (hipcc would otherwise hoist
+    // that math above the weight stream to save registers)
+    if constexpr (kAttnIn) {
+        ar.fence();
+        nr.fence(false);
+    } else if constexpr (PPT > 0) {
+        nr.fence();
+    }
+    __builtin_amdgcn_sched_barrier(0);
     float sf[MB];
     int asum[MB];
     if constexpr (PPT > 0) {
         float y[PPT][8];
-        sf[0] = norm_row<PPT>(nr, K, a.eps, y, red);
+        if constexpr (kAttnIn) {
+            ar.finish(a.Hq, 128, y);
+            sf[0] = norm_core<PPT>(nr, K, a.eps, y, red);
+        } else {
+            sf[0] = norm_row<PPT>(nr, K, a.eps, y, red);
+        }
         int as = quant_row<PPT>(y, sf[0], F::k_pad(K) / 8, smem, [](int p) { return F::lds_off(8 * p); });
         as = wave_sum_i(as);
         if ((threadIdx.x & 63) == 0) red_i[threadIdx.x >> 6] = as;
@@ -145,6 +170,7 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     __syncthreads();
     if constexpr (PPT > 0) asum[0] = (red_i[0] + red_i[1]) + (red_i[2] + red_i[3]);
     WF_STAMP(1);
+    WF_STAMP_DRAIN(13);
 
     int acc[MB];
 #pragma unroll
@@ -225,13 +251,13 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
 #pragma unroll
             for (int m = 0; m < MB; ++m) {
                 if constexpr (MODE == MODE_GU)
-                    s_out[m][lrow] = rbf(corrected(acc[m], lrow < 8 ? a.ws0 : a.ws1, asum[m], sf[m]));
+                    s_out[m][lrow] = rbf(corrected(acc[m], (lrow & 15) < 8 ? a.ws0 : a.ws1, asum[m], sf[m]));
                 else
-                    s_out[m][lrow] = rbf(resid[m] + rbf(corrected(acc[m], a.ws0, asum[m], sf[m])));
+                    s_out[m][lrow] = rbf(bf2f(resid_raw[m]) + rbf(corrected(acc[m], a.ws0, asum[m], sf[m])));
             }
         }
         __syncthreads();
-        constexpr int NOUT = (MODE == MODE_GU) ? 8 : RPB;  // outputs per block per row
+        constexpr int NOUT = (MODE == MODE_GU) ? RPB / 2 : RPB;  // outputs per block per row
         static_assert(NOUT % 8 == 0, "16-byte output granules");
         if (threadIdx.x < MB * (NOUT / 8)) {
             const int m = threadIdx.x / (NOUT / 8), j = threadIdx.x % (NOUT / 8);
@@ -240,9 +266,11 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
             for (int t = 0; t < 4; ++t) {
                 float lo, hi;
                 if constexpr (MODE == MODE_GU) {
-                    const float g0 = fmaxf(s_out[m][2 * t], 0.f), g1 = fmaxf(s_out[m][2 * t + 1], 0.f);
-                    lo = rbf(rbf(g0 * g0) * s_out[m][8 + 2 * t]);
-                    hi = rbf(rbf(g1 * g1) * s_out[m][8 + 2 * t + 1]);
+                    // 8-row tile j of the block: gate rows 16j..16j+7, up rows 16j+8..16j+15
+                    const float* tg = &s_out[m][16 * j];
+                    const float g0 = fmaxf(tg[2 * t], 0.f), g1 = fmaxf(tg[2 * t + 1], 0.f);
+                    lo = rbf(rbf(g0 * g0) * tg[8 + 2 * t]);
+                    hi = rbf(rbf(g1 * g1) * tg[8 + 2 * t + 1]);
                 } else {
                     lo = s_out[m][8 * j + 2 * t];
                     hi = s_out[m][8 * j + 2 * t + 1];
@@ -304,6 +332,31 @@ __global__ __launch_bounds__(256) void k_rownorm(const uint16_t* __restrict__ x,
             asum[b] = (red_i[0] + red_i[1]) + (red_i[2] + red_i[3]);
             sf[b] = s;
         }
+    }
+}
+
+// Batch > 1 O-projection input: attention row from the partials -> rms_norm -> int8 codes.
+template <int PPT>
+__global__ __launch_bounds__(256) void k_rownorm_attn(const float2* __restrict__ ml, const float* __restrict__ o, int Hq,
+                                                      const uint16_t* __restrict__ nw, float eps, int8_t* __restrict__ q8,
+                                                      int64_t q8s, float* __restrict__ sf, int* __restrict__ asum) {
+    __shared__ float red[8];
+    __shared__ int red_i[4];
+    const int b = blockIdx.x, K = Hq * 128;
+    AttnRow<PPT> ar;
+    ar.issue(ml, o, b, Hq, 128);
+    NormRow<PPT> nr;
+    nr.issue_w(nw, K);
+    float y[PPT][8];
+    ar.finish(Hq, 128, y);
+    const float s = norm_core<PPT>(nr, K, eps, y, red);
+    int as = quant_row<PPT>(y, s, K / 8, q8 + (int64_t)b * q8s, [](int p) { return 8 * p; });
+    as = wave_sum_i(as);
+    if ((threadIdx.x & 63) == 0) red_i[threadIdx.x >> 6] = as;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        asum[b] = (red_i[0] + red_i[1]) + (red_i[2] + red_i[3]);
+        sf[b] = s;
     }
 }
 
@@ -451,12 +504,13 @@ struct wf_model {
     uint16_t* logits = nullptr;    // caller-owned (desc)
     uint16_t *k_cache = nullptr, *v_cache = nullptr;  // caller-owned (desc)
     int32_t* seq_lens = nullptr;
-    uint16_t *h_a = nullptr, *h_b = nullptr, *qbuf = nullptr, *attn = nullptr, *act = nullptr, *hn = nullptr;
+    uint16_t *h_a = nullptr, *h_b = nullptr, *qbuf = nullptr, *act = nullptr, *hn = nullptr;
+    float2* part_ml = nullptr;  // attention partials [B, Hq, kAttnPartSplits] (m, l)
+    float* part_o = nullptr;    // [B, Hq, kAttnPartSplits, head_dim] unnormalised o
     int8_t* q8 = nullptr;   // batch > 1: activation codes of the next GEMV [B, q8_stride]
     float* act_sf = nullptr;
     int* act_sum = nullptr;
     unsigned* tickets = nullptr;
-    float* attn_ws = nullptr;
     uint2* am_part = nullptr;
     int lm_blocks = 0;
     int64_t q8_stride = 0;
@@ -468,6 +522,10 @@ struct wf_model {
 using namespace wf;
 
 namespace {
+
+// lanes per weight row (16 rows per 256-thread block at 16; QKV needs 16 for its RoPE pairing)
+constexpr int kLprGU = 8;   // 32 rows = two gate/up tiles per block: 432 blocks at I = 6912
+constexpr int kLprDN = 16;  // 160 blocks at H = 2560
 
 int64_t wrow_bytes(int fmt, int K) { return fmt == WF_FMT_TQ ? FmtTQ::row_bytes(K) : FmtI2S::row_bytes(K); }
 int k_pad(int fmt, int K) { return fmt == WF_FMT_TQ ? FmtTQ::k_pad(K) : FmtI2S::k_pad(K); }
@@ -569,26 +627,36 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             a.out = m->qbuf; a.out_stride = (int64_t)d.n_heads * D;
             if ((rc = gemv_input(m, a, m->h_a, H, d.ln_in + (int64_t)l * H, st))) return rc;
             return launch_gemv_fmt<MODE_QKV, 16>(d.wfmt, a, st);
-        case WF_OP_ATTN:
-            return decode_attention_impl(m->qbuf, WF_BF16, (int64_t)d.n_heads * D, D, a.kc, a.vc, WF_BF16,
-                                         a.kv_b_stride, (int64_t)S * D, D, 1.f, 1.f, B, d.n_heads, d.n_kv_heads, D, S,
-                                         m->seq_lens, 1.0f / sqrtf((float)D), m->attn, WF_BF16,
-                                         (int64_t)d.n_heads * D, D, m->attn_ws, st);
+        case WF_OP_ATTN:  // split partials; merged by the O projection's input stage
+            return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, a.kv_b_stride, (int64_t)S * D,
+                                             B, d.n_heads, d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D),
+                                             m->part_ml, m->part_o, st);
         case WF_OP_O:  // h_b = h_a + o_proj(rms_norm(attn_sub_norm)(attn))
             a.w = d.w_o + (int64_t)l * H * wrow_bytes(d.wfmt, H); a.N = H; a.K = H; a.ws0 = wsh[3];
             a.resid = m->h_a; a.out = m->h_b; a.out_stride = H;
-            if ((rc = gemv_input(m, a, m->attn, H, d.attn_sub + (int64_t)l * H, st))) return rc;
+            a.nw = d.attn_sub + (int64_t)l * H;
+            a.part_ml = m->part_ml;
+            a.part_o = m->part_o;
+            if (B > 1) {
+#define WF_RA(PPTV)                                                                                                  \
+    hipLaunchKernelGGL((k_rownorm_attn<PPTV>), dim3(B), dim3(256), 0, st, m->part_ml, m->part_o, d.n_heads, a.nw, d.eps, \
+                       m->q8, m->q8_stride, m->act_sf, m->act_sum)
+                if (norm_ppt(H) == 2) WF_RA(2);
+                else WF_RA(4);
+#undef WF_RA
+                if ((rc = check_launch("rownorm_attn"))) return rc;
+            }
             return launch_gemv_fmt<MODE_O, 16>(d.wfmt, a, st);
         case WF_OP_GATE_UP:  // act = relu(gate)^2 * up of rms_norm(post_attention_layernorm)(h_b)
             a.w = d.w_gu + (int64_t)l * 2 * I * wrow_bytes(d.wfmt, H); a.N = 2 * I; a.K = H;
             a.ws0 = wsh[4]; a.ws1 = wsh[5]; a.out = m->act; a.out_stride = I;
             if ((rc = gemv_input(m, a, m->h_b, H, d.ln_post + (int64_t)l * H, st))) return rc;
-            return launch_gemv_fmt<MODE_GU, 16>(d.wfmt, a, st);
+            return launch_gemv_fmt<MODE_GU, kLprGU>(d.wfmt, a, st);
         case WF_OP_DOWN:  // h_a = h_b + down(rms_norm(ffn_sub_norm)(act))
             a.w = d.w_d + (int64_t)l * H * wrow_bytes(d.wfmt, I); a.N = H; a.K = I; a.ws0 = wsh[6];
             a.resid = m->h_b; a.out = m->h_a; a.out_stride = H;
             if ((rc = gemv_input(m, a, m->act, I, d.ffn_sub + (int64_t)l * I, st))) return rc;
-            return launch_gemv_fmt<MODE_DN, 32>(d.wfmt, a, st);
+            return launch_gemv_fmt<MODE_DN, kLprDN>(d.wfmt, a, st);
         case WF_OP_LM_HEAD: {  // final norm -> hn, logits = hn @ embed^T, greedy token
             launch_rownorm(m, m->h_a, H, d.final_norm, H, m->hn, st);
             if ((rc = check_launch("final_norm"))) return rc;
@@ -659,26 +727,24 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
         return WF_EHIP;
     };
     hipError_t e;
-    const size_t ws_bytes = (size_t)wf_decode_attention_ws_bytes(B, d.n_heads, d.head_dim, d.max_seq);
 #define WF_ALLOC(ptr, bytes) \
     if ((e = hipMalloc((void**)&(ptr), (bytes))) != hipSuccess) return fail(e)
     WF_ALLOC(m->seq_lens, sizeof(int32_t) * B);
     WF_ALLOC(m->h_a, 2 * (size_t)B * d.hidden);
     WF_ALLOC(m->h_b, 2 * (size_t)B * d.hidden);
     WF_ALLOC(m->qbuf, 2 * (size_t)B * d.hidden);
-    WF_ALLOC(m->attn, 2 * (size_t)B * d.hidden);
+    WF_ALLOC(m->part_ml, sizeof(float2) * (size_t)B * d.n_heads * kAttnPartSplits);
+    WF_ALLOC(m->part_o, sizeof(float) * (size_t)B * d.n_heads * kAttnPartSplits * d.head_dim);
     WF_ALLOC(m->hn, 2 * (size_t)B * d.hidden);
     WF_ALLOC(m->act, 2 * (size_t)B * d.inter);
     WF_ALLOC(m->q8, (size_t)B * m->q8_stride);
     WF_ALLOC(m->act_sf, sizeof(float) * B);
     WF_ALLOC(m->act_sum, sizeof(int) * B);
     WF_ALLOC(m->tickets, sizeof(unsigned) * kTicketWords * TK_COUNT);
-    WF_ALLOC(m->attn_ws, ws_bytes);
     WF_ALLOC(m->am_part, sizeof(uint2) * B * m->lm_blocks);
 #undef WF_ALLOC
     // tickets start at zero; every launch re-arms the ones it uses
     if ((e = hipMemset(m->tickets, 0, sizeof(unsigned) * kTicketWords * TK_COUNT)) != hipSuccess) return fail(e);
-    if ((e = hipMemset(m->attn_ws, 0, ws_bytes)) != hipSuccess) return fail(e);
     if ((e = hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking)) != hipSuccess) return fail(e);
     *out = m;
     return WF_OK;
@@ -689,8 +755,8 @@ int wf_model_destroy(wf_model* m) {
     if (m->exec) (void)hipGraphExecDestroy(m->exec);
     if (m->graph) (void)hipGraphDestroy(m->graph);
     if (m->cap) (void)hipStreamDestroy(m->cap);
-    void* ptrs[] = {m->seq_lens, m->h_a, m->h_b, m->qbuf, m->attn, m->hn, m->act, m->q8,
-                    m->act_sf, m->act_sum, m->tickets, m->attn_ws, m->am_part};
+    void* ptrs[] = {m->seq_lens, m->h_a, m->h_b, m->qbuf, m->part_ml, m->part_o, m->hn, m->act, m->q8,
+                    m->act_sf, m->act_sum, m->tickets, m->am_part};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete[] m->d.wscale;

@@ -142,6 +142,8 @@ __device__ __forceinline__ int block_sum_i(int v, int* red) {
 // m < 1e-6); q = clamp(rne(x / float(s)), -128, 127). Division is IEEE (hipcc's default
 // correctly-rounded fp32 divide), rint() is round-half-even.
 // ---------------------------------------------------------------------------------------------
+// sum of the four signed bytes of `a` (+ c)
+__device__ __forceinline__ int sdot4_ones(uint32_t a, int c) { return __builtin_amdgcn_sdot4((int)a, 0x01010101, c, false); }
 __device__ __forceinline__ double act_scale_from_max(float m) {
     double md = (double)m;
     if (md < 1e-6) md = 1.0;
@@ -152,31 +154,31 @@ __device__ __forceinline__ int8_t quant_one(float x, float sf) {
     v = fminf(fmaxf(v, -128.f), 127.f);
     return (int8_t)(int)v;
 }
-// Eight codes at once, bit-identical to quant_one: t = x * (1/s) is within 3 * 2^-17 of the
-// correctly rounded quotient for |x/s| <= 128, so rint(t) is the reference code unless t lies
-// within 2^-13 of a half-integer; only then (p ~ 2.4e-4 per element) the lane redoes the
-// IEEE divide. Returns the 8 codes packed little-endian; adds them to `asum`.
+// Eight codes at once, bit-identical to quant_one. The exact product x * inv (inv = 1/s rounded)
+// is within 2^-17 of x/s for |x/s| <= 128, so rne(x/s) = rne(x * inv) unless x * inv lies within
+// 2^-13 of a half-integer; only then (p ~ 2.4e-4 per element) the lane redoes the IEEE divide.
+// rne comes from the fma's own rounding: fma(x, inv, 1.5 * 2^23) keeps rne(x * inv) in the low
+// mantissa bits (low byte = the int8 code), fma(x, inv, -q) is the exact remainder. No clamp is
+// needed: s = max|x| / 127 bounds |x * inv| by 127 (1 + 2^-23). Returns the 8 codes packed
+// little-endian; adds them to `asum`.
 __device__ __forceinline__ uint2 quant8(const float (&x)[8], float sf, float inv, int& asum) {
-    float q[8];
+    constexpr float kMagic = 12582912.0f;  // 1.5 * 2^23
+    uint32_t b[8];
     bool risky = false;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const float t = x[j] * inv;
-        q[j] = rintf(t);
-        risky |= fabsf(t - q[j]) > 0.4998779296875f;  // 0.5 - 2^-13
+        const float sm = fmaf(x[j], inv, kMagic);
+        const float q = sm - kMagic;
+        risky |= fabsf(fmaf(x[j], inv, -q)) > 0.4998779296875f;  // 0.5 - 2^-13
+        b[j] = __float_as_uint(sm);
     }
     if (risky) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) q[j] = rintf(x[j] / sf);
+        for (int j = 0; j < 8; ++j) b[j] = __float_as_uint(fminf(fmaxf(rintf(x[j] / sf), -128.f), 127.f) + kMagic);
     }
-    uint32_t lo = 0, hi = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int c = (int)fminf(fmaxf(q[j], -128.f), 127.f);
-        asum += c;
-        if (j < 4) lo |= ((uint32_t)c & 0xffu) << (8 * j);
-        else hi |= ((uint32_t)c & 0xffu) << (8 * (j - 4));
-    }
+    const uint32_t lo = __builtin_amdgcn_perm(b[1], b[0], 0x0c0c0400u) | __builtin_amdgcn_perm(b[3], b[2], 0x04000c0cu);
+    const uint32_t hi = __builtin_amdgcn_perm(b[5], b[4], 0x0c0c0400u) | __builtin_amdgcn_perm(b[7], b[6], 0x04000c0cu);
+    asum = sdot4_ones(lo, sdot4_ones(hi, asum));
     return make_uint2(lo, hi);
 }
 

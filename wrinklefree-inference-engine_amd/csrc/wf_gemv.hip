@@ -156,6 +156,22 @@ __global__ __launch_bounds__(256) void k_quant_apply(const void* __restrict__ x,
     if (mode == 0) sf = (float)act_scale_from_max(m);
     else if (mode == 1) sf = (m > 1e-6f) ? (float)((double)m / 127.0) : 1.0f;
     else sf = (float)(127.0 / ((double)m < 1e-6 ? 1.0 : (double)m));
+    if (mode == 0) {  // 8 codes per thread through quant8 (the decode step's quantizer), scalar tail
+        const float inv = 1.0f / sf;
+        const int64_t n8 = n / 8;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = load_as_f32(x, 8 * i + j, dt);
+            int dummy = 0;
+            const uint2 pk = quant8(v, sf, inv, dummy);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) q[8 * i + j] = (int8_t)(((j < 4 ? pk.x : pk.y) >> (8 * (j & 3))) & 0xff);
+        }
+        for (int64_t i = 8 * n8 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+            q[i] = quant_one(load_as_f32(x, i, dt), sf);
+        return;
+    }
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const float v = load_as_f32(x, i, dt);
         int8_t r;

@@ -73,16 +73,31 @@ __device__ __forceinline__ void ticket_rearm(unsigned* t) {
 // the 100 MHz wall clock (s_memrealtime) at named points; read back with wf_debug_stamps_<tu>().
 // In the product build WF_STAMP compiles to nothing.
 #ifdef WF_STAMPS
-constexpr int kStampSlots = 16;
+constexpr int kStampSlots = 80;  // 4 waves x 16 realtime slots + 16 shader-clock slots
 constexpr int kStampBlocks = 16384;
-static __device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
-#define WF_STAMP(i)                                                                         \
-    do {                                                                                    \
-        if (threadIdx.x == 0) {                                                             \
-            const unsigned sb_ = ::wf::linear_block_id();                                    \
-            if (sb_ < (unsigned)::wf::kStampBlocks)                                          \
-                ::wf::g_stamps[sb_ * ::wf::kStampSlots + (i)] = __builtin_amdgcn_s_memrealtime(); \
-        }                                                                                   \
+// hidden visibility: PC-relative address (no GOT load per stamp); slot index from blockIdx only
+// (no gridDim load): block (x, y, z) -> x + 2048 y + 8192 z
+__attribute__((visibility("hidden"))) static __device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
+// slot i of wave w lives at column 16 w + i; wave 0 also records the shader clock (s_memtime) of
+// slot i in column 64 + i (clock rate = d(memtime) / d(memrealtime) * 100 MHz)
+#define WF_STAMP(i)                                                                                 \
+    do {                                                                                            \
+        __builtin_amdgcn_sched_barrier(0);                                                          \
+        if ((threadIdx.x & 63) == 0) {                                                              \
+            const unsigned sb_ = blockIdx.x + 2048u * blockIdx.y + 8192u * blockIdx.z;               \
+            if (sb_ < (unsigned)::wf::kStampBlocks) {                                                \
+                unsigned long long* row_ = ::wf::g_stamps + (size_t)sb_ * ::wf::kStampSlots;          \
+                row_[16 * (threadIdx.x >> 6) + (i)] = __builtin_amdgcn_s_memrealtime();              \
+                if (threadIdx.x == 0) row_[64 + (i)] = __builtin_amdgcn_s_memtime();                  \
+            }                                                                                       \
+        }                                                                                           \
+        __builtin_amdgcn_sched_barrier(0);                                                          \
+    } while (0)
+// stamp after draining this wave's outstanding loads (when its data has landed)
+#define WF_STAMP_DRAIN(i)                                   \
+    do {                                                    \
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   \
+        WF_STAMP(i);                                        \
     } while (0)
 #define WF_STAMP_READER(NAME)                                                                     \
     extern "C" int NAME(void* host, int n_words, int reset) {                                     \
@@ -101,6 +116,9 @@ inline void* g_stamps_addr() {
 #define WF_STAMP(i) \
     do {            \
     } while (0)
+#define WF_STAMP_DRAIN(i) \
+    do {                  \
+    } while (0)
 #define WF_STAMP_READER(NAME)
 #endif
 
@@ -115,6 +133,11 @@ inline void* g_stamps_addr() {
 // ---------------------------------------------------------------------------------------------
 constexpr int kNT = 256;  // threads per block of every decode-step kernel
 
+// Register fence: the value must exist here and nothing computed from it can move above this point
+// (hipcc otherwise hoists the input-stage math above a later weight stream, delaying its issue).
+__device__ __forceinline__ void reg_fence(uint4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+__device__ __forceinline__ void reg_fence(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+
 template <int PPT>
 struct NormRow {
     uint4 x[PPT], w[PPT];
@@ -127,31 +150,52 @@ struct NormRow {
             w[i] = *reinterpret_cast<const uint4*>(nw + 8 * p);
         }
     }
+    // norm weight only (the row itself is computed in registers, e.g. AttnRow)
+    __device__ __forceinline__ void issue_w(const uint16_t* __restrict__ nw, int K) {
+        const int npk = K >> 3;
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) w[i] = *reinterpret_cast<const uint4*>(nw + 8 * min((int)threadIdx.x + kNT * i, npk - 1));
+    }
+    __device__ __forceinline__ void fence(bool with_x = true) {
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) {
+            if (with_x) reg_fence(x[i]);
+            reg_fence(w[i]);
+        }
+    }
 };
 
-// Normalises the row held in `r`; returns the bf16-rounded y values in `y` (0 for pieces >= K/8)
-// and the quantizer's float scale. `red` = 8 floats of LDS (two barriers inside).
+// bf16 pieces of `r.x` -> floats (0 for pieces >= K/8)
 template <int PPT>
-__device__ __forceinline__ float norm_row(const NormRow<PPT>& r, int K, float eps, float (&y)[PPT][8], float* red,
-                                          bool want_scale = true) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int npk = K >> 3;
-    float ss = 0.f;
+__device__ __forceinline__ void unpack_row(const NormRow<PPT>& r, int K, float (&y)[PPT][8]) {
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
-        const bool valid = (int)threadIdx.x + kNT * i < npk;
+        const bool valid = (int)threadIdx.x + kNT * i < (K >> 3);
         const uint32_t w4[4] = {r.x[i].x, r.x[i].y, r.x[i].z, r.x[i].w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             y[i][2 * j] = valid ? bf_lo(w4[j]) : 0.f;
             y[i][2 * j + 1] = valid ? bf_hi(w4[j]) : 0.f;
         }
+    }
+}
+
+// Normalises the row held in `y` (x values, 0 for pieces >= K/8) in place with the norm weight in
+// `r.w`; returns the quantizer's float scale. `red` = 8 floats of LDS (two barriers inside).
+template <int PPT>
+__device__ __forceinline__ float norm_core(const NormRow<PPT>& r, int K, float eps, float (&y)[PPT][8], float* red,
+                                           bool want_scale = true) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i)
 #pragma unroll
         for (int j = 0; j < 8; ++j) ss = fmaf(y[i][j], y[i][j], ss);
-    }
+    WF_STAMP(8);
     ss = wave_sum(ss);
     if (lane == 0) red[wave] = ss;
     __syncthreads();
+    WF_STAMP(9);
     ss = (red[0] + red[1]) + (red[2] + red[3]);
     const float rr = rbf(1.0f / sqrtf(ss / (float)K + eps));
     float mx = 0.f;
@@ -168,13 +212,30 @@ __device__ __forceinline__ float norm_row(const NormRow<PPT>& r, int K, float ep
         }
     }
     if (!want_scale) return 0.f;
+    WF_STAMP(10);
     mx = wave_max(mx);
     if (lane == 0) red[4 + wave] = mx;
     __syncthreads();
+    WF_STAMP(11);
     mx = fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7]));
     return (float)act_scale_from_max(mx);
 }
+// unpack_row + norm_core
+template <int PPT>
+__device__ __forceinline__ float norm_row(const NormRow<PPT>& r, int K, float eps, float (&y)[PPT][8], float* red,
+                                          bool want_scale = true) {
+    unpack_row<PPT>(r, K, y);
+    return norm_core<PPT>(r, K, eps, y, red, want_scale);
+}
 
+// ---------------------------------------------------------------------------------------------
+// Attention row of sequence b from the decode-step attention partials (wf_attn.hip k_attn_part:
+// kAttnPartSplits records per (b, head): ml = (m, l), o unnormalised). Piece p (outputs
+// 8p..8p+7, head h = 8p / D) merges the splits of its head,
+//   out = sum_s e^(m_s - M) o_s / sum_s e^(m_s - M) l_s   (M = max_s m_s; empty splits: m = -inf),
+// rounded to bf16 like the reference's attention output tensor. issue() puts every load in flight
+// (the caller then issues its weight stream); finish() merges. Zero for pieces >= Hq*D/8.
+// ---------------------------------------------------------------------------------------------
 // Quantizes the normalised pieces; piece p (< npad = padded K / 8) goes to dst + off(p). Returns
 // this thread's code sum (the caller reduces it).
 template <int PPT, class Off>
@@ -187,7 +248,75 @@ __device__ __forceinline__ int quant_row(const float (&y)[PPT][8], float sf, int
         const uint2 q = quant8(y[i], sf, inv, asum);
         if (p < npad) *reinterpret_cast<uint2*>(dst + off(p)) = q;
     }
+    WF_STAMP(12);
     return asum;
 }
+
+constexpr int kAttnPartSplits = 8;
+
+template <int PPT>
+struct AttnRow {
+    float4 ml[PPT][kAttnPartSplits / 2];  // (m0, l0, m1, l1) pairs
+    float4 oa[PPT][kAttnPartSplits], ob[PPT][kAttnPartSplits];
+    __device__ __forceinline__ void issue(const float2* __restrict__ ml_in, const float* __restrict__ o_in, int b, int Hq,
+                                          int D) {
+        const int npk = Hq * D / 8;
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) {
+            const int pc = min((int)threadIdx.x + kNT * i, npk - 1);
+            const int h = (8 * pc) / D, d0 = 8 * pc - h * D;
+            const int64_t rec = (int64_t)(b * Hq + h) * kAttnPartSplits;
+#pragma unroll
+            for (int u = 0; u < kAttnPartSplits / 2; ++u) ml[i][u] = reinterpret_cast<const float4*>(ml_in + rec)[u];
+#pragma unroll
+            for (int u = 0; u < kAttnPartSplits; ++u) {
+                const float* r = o_in + (rec + u) * D + d0;
+                oa[i][u] = *reinterpret_cast<const float4*>(r);
+                ob[i][u] = *reinterpret_cast<const float4*>(r + 4);
+            }
+        }
+    }
+    __device__ __forceinline__ void fence() {
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) {
+#pragma unroll
+            for (int u = 0; u < kAttnPartSplits / 2; ++u) reg_fence(ml[i][u]);
+#pragma unroll
+            for (int u = 0; u < kAttnPartSplits; ++u) {
+                reg_fence(oa[i][u]);
+                reg_fence(ob[i][u]);
+            }
+        }
+    }
+    __device__ __forceinline__ void finish(int Hq, int D, float (&y)[PPT][8]) const {
+        const int npk = Hq * D / 8;
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) {
+            float mm[kAttnPartSplits], ll[kAttnPartSplits];
+#pragma unroll
+            for (int u = 0; u < kAttnPartSplits / 2; ++u) {
+                mm[2 * u] = ml[i][u].x; ll[2 * u] = ml[i][u].y;
+                mm[2 * u + 1] = ml[i][u].z; ll[2 * u + 1] = ml[i][u].w;
+            }
+            float M = mm[0];
+#pragma unroll
+            for (int u = 1; u < kAttnPartSplits; ++u) M = fmaxf(M, mm[u]);
+            float L = 0.f, O[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int u = 0; u < kAttnPartSplits; ++u) {
+                const float w = (mm[u] == -INFINITY) ? 0.f : __expf(mm[u] - M);
+                L = fmaf(w, ll[u], L);
+                const float ov[8] = {oa[i][u].x, oa[i][u].y, oa[i][u].z, oa[i][u].w,
+                                     ob[i][u].x, ob[i][u].y, ob[i][u].z, ob[i][u].w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) O[j] = fmaf(w, ov[j], O[j]);
+            }
+            const float inv = 1.0f / L;
+            const bool valid = (int)threadIdx.x + kNT * i < npk;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) y[i][j] = valid ? rbf(O[j] * inv) : 0.f;
+        }
+    }
+};
 
 }  // namespace wf
