@@ -314,22 +314,31 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
 // ---------------------------------------------------------------------------------------------
 // Decode-step attention partials: bf16 q/K/V, D = 128, kAttnPartSplits splits per (b, kv head)
 // whatever the context: split s of a sequence with Sb keys covers [s*T, min((s+1)*T, Sb)) with
-// T = round_up(ceil(Sb / kAttnPartSplits), 16), walked in chunks of 128 keys (8 per lane group,
-// every load of a chunk in flight at once) with an online softmax. The block writes, per query
-// head of its group, (m, l) to ml[b][hq][s] and the unnormalised o to o[b][hq][s][D]; an empty
-// split writes (-inf, 0) and zeros. The consumer (wf_norm.h AttnRow, the O projection's
-// prologue or k_rownorm_attn) reads a fixed number of records, so it needs no sequence length
-// and issues every load before its weight stream.
+// T = round_up(ceil(Sb / kAttnPartSplits), 16), walked in chunks of 128 keys (16 lane groups x 8
+// keys) with an online softmax; chunk loads are double-buffered (the next chunk's loads are in
+// flight while the current one is computed; a split of up to 256 keys -- 2048 keys of context --
+// has all of its loads in flight at once). The block writes, per query head of its group, (m, l) to
+// ml[b][hq][s] and the unnormalised o to o[b][hq][s][D]; an empty split writes (-inf, 0) and
+// zeros. The consumer (wf_norm.h AttnRow, the O projection's prologue or k_rownorm_attn) reads a
+// fixed number of records, so it needs no sequence length and issues every load before its
+// weight stream.
 // ---------------------------------------------------------------------------------------------
+constexpr int kAttnPartThreads = 256;
 template <int G>
-__global__ __launch_bounds__(kAttnThreads) void k_attn_part(const uint16_t* __restrict__ q, int64_t q_sb,
-                                                            const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
-                                                            int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv, int S,
-                                                            const int32_t* __restrict__ seq_lens, float sm_scale,
-                                                            float2* __restrict__ ml_out, float* __restrict__ o_out) {
-    constexpr int D = 128, LP = D / 8, NG = kAttnThreads / LP, U = 8, CH = U * NG;  // 128 keys per chunk
-    const int s = blockIdx.x, g = blockIdx.y, b = blockIdx.z;
+__global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* __restrict__ q, int64_t q_sb,
+                                                                const uint16_t* __restrict__ K,
+                                                                const uint16_t* __restrict__ V, int64_t kv_sb,
+                                                                int64_t kv_sh, int Hq, int Hkv, int S,
+                                                                const int32_t* __restrict__ seq_lens, float sm_scale,
+                                                                float2* __restrict__ ml_out, float* __restrict__ o_out) {
+    constexpr int D = 128, LP = D / 8, NG = kAttnPartThreads / LP, U = 8, CH = U * NG;  // 128 keys per chunk
+    // block (s, y, b): query heads hq0 .. hq0 + G - 1 (G = whole GQA group, or 1: one block per query
+    // head, 4x the blocks for a group of 4 -- the K/V re-reads hit the caches)
+    const int s = blockIdx.x, b = blockIdx.z;
     const int grp = Hq / Hkv;
+    const int hq0 = (G == 1) ? (int)blockIdx.y : (int)blockIdx.y * grp;
+    const int g = hq0 / grp;
+    const int nh = (G == 1) ? 1 : grp;  // query heads of this block
     const int gid = threadIdx.x / LP, li = threadIdx.x % LP;
     const int Sb = min(seq_lens[b], S);
     const int T = ((Sb + kAttnPartSplits - 1) / kAttnPartSplits + 15) / 16 * 16;
@@ -347,38 +356,38 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_part(const uint16_t* __re
         for (int j = 0; j < 8; ++j) o[h][j] = 0.f;
     }
     if (t0 < t1) {
-        float qv[G][8];
-#pragma unroll
-        for (int h = 0; h < G; ++h) {
-            const uint4 r = *reinterpret_cast<const uint4*>(q + b * q_sb + (int64_t)(g * grp + min(h, grp - 1)) * D + li * 8);
-            const uint32_t w[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) { qv[h][2 * i] = bf_lo(w[i]); qv[h][2 * i + 1] = bf_hi(w[i]); }
-        }
         const int64_t kvb = b * kv_sb + g * kv_sh + li * 8;
-        for (int c0 = t0; c0 < t1; c0 += CH) {
-            uint4 kr[U], vr[U];
+        // chunk loads: clamped to the split (no branch around loads: hipcc counts vmcnt exactly)
+        auto load = [&](uint4 (&kr)[U], uint4 (&vr)[U], int c0) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int t = min(c0 + gid + NG * u, t1 - 1);
                 kr[u] = *reinterpret_cast<const uint4*>(K + kvb + (int64_t)t * D);
                 vr[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)t * D);
             }
+        };
+        uint4 qv[G];  // bf16 pairs
+        uint4 kA[U], vA[U], kB[U], vB[U];
+#pragma unroll
+        for (int h = 0; h < G; ++h)
+            qv[h] = *reinterpret_cast<const uint4*>(q + b * q_sb + (int64_t)(hq0 + min(h, nh - 1)) * D + li * 8);
+        load(kA, vA, t0);
+        auto compute = [&](const uint4 (&kr)[U], const uint4 (&vr)[U], int c0) {
             float sc[U][G];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t w[4] = {kr[u].x, kr[u].y, kr[u].z, kr[u].w};
-                const bool valid = c0 + gid + NG * u < t1;
 #pragma unroll
                 for (int h = 0; h < G; ++h) {
+                    const uint32_t qw[4] = {qv[h].x, qv[h].y, qv[h].z, qv[h].w};
                     float d = 0.f;
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        d = fmaf(qv[h][2 * i], bf_lo(w[i]), d);
-                        d = fmaf(qv[h][2 * i + 1], bf_hi(w[i]), d);
+                        d = fmaf(bf_lo(qw[i]), bf_lo(w[i]), d);
+                        d = fmaf(bf_hi(qw[i]), bf_hi(w[i]), d);
                     }
                     d = group_reduce<LP>(d, OpAdd{});
-                    sc[u][h] = valid ? d * sm_scale : -INFINITY;
+                    sc[u][h] = (c0 + gid + NG * u < t1) ? d * sm_scale : -INFINITY;
                 }
             }
 #pragma unroll
@@ -406,6 +415,12 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_part(const uint16_t* __re
                     for (int j = 0; j < 8; ++j) o[h][j] = fmaf(p, vx[j], o[h][j]);
                 }
             }
+        };
+        for (int c0 = t0; c0 < t1; c0 += 2 * CH) {
+            load(kB, vB, c0 + CH);  // next chunk in flight while this one is computed
+            compute(kA, vA, c0);
+            load(kA, vA, c0 + 2 * CH);
+            if (c0 + CH < t1) compute(kB, vB, c0 + CH);
         }
     }
     WF_STAMP(1);
@@ -420,20 +435,20 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_part(const uint16_t* __re
     }
     __syncthreads();
     constexpr int D4 = D / 4;
-    for (int idx = threadIdx.x; idx < grp * D4; idx += kAttnThreads) {
+    for (int idx = threadIdx.x; idx < nh * D4; idx += kAttnPartThreads) {
         const int h = idx / D4, d = (idx - h * D4) * 4;
         float mx = -INFINITY;
 #pragma unroll
         for (int w = 0; w < NG; ++w) mx = fmaxf(mx, sm_m[w][h]);
         float ls = 0.f, os[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
+#pragma unroll 4
         for (int w = 0; w < NG; ++w) {
             const float a = (sm_m[w][h] == -INFINITY) ? 0.f : __expf(sm_m[w][h] - mx);
             ls += sm_l[w][h] * a;
             const float4 ov = *reinterpret_cast<const float4*>(&sm_o[w][h][d]);
             os[0] += ov.x * a; os[1] += ov.y * a; os[2] += ov.z * a; os[3] += ov.w * a;
         }
-        const int64_t rec = (int64_t)(b * Hq + g * grp + h) * kAttnPartSplits + s;
+        const int64_t rec = (int64_t)(b * Hq + hq0 + h) * kAttnPartSplits + s;
         *reinterpret_cast<float4*>(o_out + rec * D + d) = make_float4(os[0], os[1], os[2], os[3]);
         if (d == 0) ml_out[rec] = make_float2(mx, ls);
     }
@@ -443,10 +458,17 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_part(const uint16_t* __re
 int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
                               float2* ml, float* o, hipStream_t st) {
-    const dim3 grid(kAttnPartSplits, Hkv, B);
+    // one block per query head (G = 1): 4x the blocks of one per kv head at Hq/Hkv = 4, a quarter of
+    // the per-lane arithmetic (the kernel is latency-bound on its score/softmax chain at 1 wave/SIMD)
+    const dim3 grid(kAttnPartSplits, Hq, B);
     const int grp = Hq / Hkv;
+    if (grp <= 8) {
+        hipLaunchKernelGGL((k_attn_part<1>), grid, dim3(kAttnPartThreads), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S,
+                           seq_lens, sm_scale, ml, o);
+        return check_launch("decode_attention_partials");
+    }
 #define WF_AP(GV)                                                                                                   \
-    hipLaunchKernelGGL((k_attn_part<GV>), grid, dim3(kAttnThreads), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, \
+    hipLaunchKernelGGL((k_attn_part<GV>), grid, dim3(kAttnPartThreads), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, \
                        seq_lens, sm_scale, ml, o)
     if (grp == 1) WF_AP(1);
     else if (grp == 2) WF_AP(2);

@@ -70,6 +70,23 @@ __device__ __forceinline__ float corrected(int S, float ws, int asum, float sf) 
     return (raw - c) * sf;
 }
 
+// KV-history prefetch block j (of 2 * Hkv * kPfParts) of the QKV launch: reads its share of keys
+// [0, pos) of K or V of one kv head (the values are dropped; the point is the cache fill).
+constexpr int kPfParts = 4;
+__device__ __forceinline__ void kv_prefetch(const GemvArgs& a, int j, int b) {
+    const int kv = j / (a.Hkv * kPfParts), g = (j / kPfParts) % a.Hkv, part = j % kPfParts;
+    const int Sb = min(max(a.positions[b], 0), a.S);
+    const int k0 = part * Sb / kPfParts, k1 = (part + 1) * Sb / kPfParts;
+    const uint8_t* base = reinterpret_cast<const uint8_t*>((kv ? a.vc : a.kc) + (int64_t)b * a.kv_b_stride +
+                                                          (int64_t)g * a.S * 128);
+    uint32_t acc = 0;
+    const int64_t e = (int64_t)k1 * 256;
+#pragma unroll 8
+    for (int64_t off = (int64_t)k0 * 256 + threadIdx.x * 16; off < e; off += 256 * 16)
+        acc ^= reinterpret_cast<const uint4*>(base + off)->x;
+    if (acc == 0x9e3779b9u && a.S < 0) a.kc[0] = 0;  // never true: keeps the loads
+}
+
 // Block = 256 threads; LPR lanes per weight row -> 256/LPR rows per block; MB activation rows.
 // PPT > 0 (MB == 1): the block normalises + quantises its input row itself (wf_norm.h) while its
 // first weight chunks stream in; PPT = 8-element pieces per thread (padded K <= 2048 * PPT).
@@ -89,6 +106,14 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     const int K = a.K, N = a.N;
     const int img = lds_image_bytes<F>(K);
     const int b0 = blockIdx.y * MB;
+    if constexpr (MODE == MODE_QKV && PPT > 0) {
+        // blocks past the weight rows warm the Infinity Cache (and TLB) with this layer's cached K/V
+        // history for the attention launch that follows (it reads them from HBM otherwise)
+        if ((int)blockIdx.x >= (N + RPB - 1) / RPB) {
+            kv_prefetch(a, blockIdx.x - (N + RPB - 1) / RPB, b0);
+            return;
+        }
+    }
     const int lrow = threadIdx.x / LPR, sub = threadIdx.x % LPR;
     const int row = blockIdx.x * RPB + lrow;
     const int C = F::chunks(K);
@@ -538,8 +563,10 @@ int launch_gemv(const GemvArgs& ga, hipStream_t st) {
     const int img = lds_image_bytes<F>(ga.K);
     const int gx = (ga.N + RPB - 1) / RPB;
     const int B = ga.B;
-#define WF_G(MBV, PPTV) \
-    hipLaunchKernelGGL((k_gemv<F, MODE, LPR, MBV, PPTV>), dim3(gx, B / MBV), dim3(256), (size_t)img * MBV, st, ga)
+#define WF_G(MBV, PPTV)                                                                                         \
+    hipLaunchKernelGGL((k_gemv<F, MODE, LPR, MBV, PPTV>), dim3(gx + (B == 1 ? pf : 0), B / MBV), dim3(256),     \
+                       (size_t)img * MBV, st, ga)
+    const int pf = MODE == MODE_QKV ? 2 * ga.Hkv * kPfParts : 0;  // KV prefetch blocks (batch 1)
     if (B == 1) {
         if (norm_ppt(F::k_pad(ga.K)) == 2) WF_G(1, 2);
         else WF_G(1, 4);
