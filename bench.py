@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--ctx", type=int, default=1024)
-    ap.add_argument("--wfmt", choices=["tq", "i2s"], default="tq")
+    ap.add_argument("--wfmt", choices=["tq", "i2s"], default="i2s")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-op-timing", action="store_true")

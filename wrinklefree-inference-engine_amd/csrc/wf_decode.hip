@@ -30,6 +30,7 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
                               float2* ml, float* o, hipStream_t st);
 
 enum { MODE_QKV = 0, MODE_O = 1, MODE_GU = 2, MODE_DN = 3 };
+constexpr int kNT = 512;  // threads per GEMV / row-norm block (8 waves: 2 per SIMD hide the input-stage latency)
 
 struct GemvArgs {
     // input row(s): bf16 x + norm weight (PPT > 0: normalised + quantised in the block prologue)
@@ -70,60 +71,35 @@ __device__ __forceinline__ float corrected(int S, float ws, int asum, float sf) 
     return (raw - c) * sf;
 }
 
-// KV-history prefetch block j (of 2 * Hkv * kPfParts) of the QKV launch: reads its share of keys
-// [0, pos) of K or V of one kv head (the values are dropped; the point is the cache fill).
-constexpr int kPfParts = 4;
-__device__ __forceinline__ void kv_prefetch(const GemvArgs& a, int j, int b) {
-    const int kv = j / (a.Hkv * kPfParts), g = (j / kPfParts) % a.Hkv, part = j % kPfParts;
-    const int Sb = min(max(a.positions[b], 0), a.S);
-    const int k0 = part * Sb / kPfParts, k1 = (part + 1) * Sb / kPfParts;
-    const uint8_t* base = reinterpret_cast<const uint8_t*>((kv ? a.vc : a.kc) + (int64_t)b * a.kv_b_stride +
-                                                          (int64_t)g * a.S * 128);
-    uint32_t acc = 0;
-    const int64_t e = (int64_t)k1 * 256;
-#pragma unroll 8
-    for (int64_t off = (int64_t)k0 * 256 + threadIdx.x * 16; off < e; off += 256 * 16)
-        acc ^= reinterpret_cast<const uint4*>(base + off)->x;
-    if (acc == 0x9e3779b9u && a.S < 0) a.kc[0] = 0;  // never true: keeps the loads
-}
-
-// Block = 256 threads; LPR lanes per weight row -> 256/LPR rows per block; MB activation rows.
+// Block = kNT threads; LPR lanes per weight row -> kNT/LPR rows per block; MB activation rows.
 // PPT > 0 (MB == 1): the block normalises + quantises its input row itself (wf_norm.h) while its
 // first weight chunks stream in; PPT = 8-element pieces per thread (padded K <= 2048 * PPT).
 // PPT == 0: the codes come from k_rownorm (batch > 1).
 template <class F, int MODE, int LPR, int MB, int PPT>
-__global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
+__global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
     static_assert(PPT == 0 || MB == 1, "the norm prologue handles one activation row");
-    constexpr int RPB = 256 / LPR;
-    // 16-byte weight chunks in flight per lane (K = 2560: 2 per lane at LPR 16, 4 at LPR 8;
-    // K = 6912 at LPR 16: 6)
-    constexpr int kPrefetch = (MODE == MODE_DN || LPR <= 8) ? 8 : 4;
+    constexpr int RPB = kNT / LPR;
+    // 16-byte weight chunks in flight per lane (K = 2560 TQ: 1 per lane at LPR 32, 4 at LPR 8;
+    // K = 6912 at LPR 32: 3)
+    constexpr int kPrefetch = LPR >= 32 ? 4 : (LPR == 16 ? 4 : 8);
     extern __shared__ __attribute__((aligned(16))) int8_t smem[];
-    __shared__ float red[8];
-    __shared__ int red_i[4];
+    __shared__ float red[2 * kNT / 64];
+    __shared__ int red_i[kNT / 64];
     __shared__ float s_out[MB][RPB];
 
     const int K = a.K, N = a.N;
     const int img = lds_image_bytes<F>(K);
     const int b0 = blockIdx.y * MB;
-    if constexpr (MODE == MODE_QKV && PPT > 0) {
-        // blocks past the weight rows warm the Infinity Cache (and TLB) with this layer's cached K/V
-        // history for the attention launch that follows (it reads them from HBM otherwise)
-        if ((int)blockIdx.x >= (N + RPB - 1) / RPB) {
-            kv_prefetch(a, blockIdx.x - (N + RPB - 1) / RPB, b0);
-            return;
-        }
-    }
     const int lrow = threadIdx.x / LPR, sub = threadIdx.x % LPR;
     const int row = blockIdx.x * RPB + lrow;
     const int C = F::chunks(K);
     WF_STAMP(0);
 
     // 1) the input row (issued first: vmcnt retires in order), 2) the weight stream, 3) residual
-    NormRow<PPT == 0 ? 1 : PPT> nr;
+    NormRow<PPT == 0 ? 1 : PPT, kNT> nr;
     constexpr bool kAttnIn = (MODE == MODE_O && PPT > 0);
-    AttnRow<kAttnIn ? PPT : 1> ar;
-    constexpr int kMaxPiecesPerThread = 2;  // staged int8: K_pad <= 8192
+    AttnRow<kAttnIn ? PPT : 1, kNT> ar;
+    constexpr int kMaxPiecesPerThread = 8192 / 16 / kNT;  // staged int8: K_pad <= 8192
     uint4 apre[MB][kMaxPiecesPerThread];
     const int pieces16 = F::k_pad(K) / 16;
     if constexpr (kAttnIn) {
@@ -136,7 +112,7 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
         for (int m = 0; m < MB; ++m)
 #pragma unroll
             for (int i = 0; i < kMaxPiecesPerThread; ++i) {
-                const int p = threadIdx.x + 256 * i;
+                const int p = threadIdx.x + kNT * i;
                 apre[m][i] = (p < pieces16 && 16 * p < K)
                                  ? *reinterpret_cast<const uint4*>(a.q8 + (int64_t)(b0 + m) * a.q8_stride + 16 * p)
                                  : make_uint4(0, 0, 0, 0);
@@ -171,11 +147,11 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
         float y[PPT][8];
         if constexpr (kAttnIn) {
             ar.finish(a.Hq, 128, y);
-            sf[0] = norm_core<PPT>(nr, K, a.eps, y, red);
+            sf[0] = norm_core(nr, K, a.eps, y, red);
         } else {
-            sf[0] = norm_row<PPT>(nr, K, a.eps, y, red);
+            sf[0] = norm_row(nr, K, a.eps, y, red);
         }
-        int as = quant_row<PPT>(y, sf[0], F::k_pad(K) / 8, smem, [](int p) { return F::lds_off(8 * p); });
+        int as = quant_row<PPT, kNT>(y, sf[0], F::k_pad(K) / 8, smem, [](int p) { return F::lds_off(8 * p); });
         as = wave_sum_i(as);
         if ((threadIdx.x & 63) == 0) red_i[threadIdx.x >> 6] = as;
     } else {
@@ -183,7 +159,7 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
         for (int m = 0; m < MB; ++m)
 #pragma unroll
             for (int i = 0; i < kMaxPiecesPerThread; ++i) {
-                const int p = threadIdx.x + 256 * i;
+                const int p = threadIdx.x + kNT * i;
                 if (p < pieces16) *reinterpret_cast<uint4*>(smem + m * img + F::lds_off(16 * p)) = apre[m][i];
             }
 #pragma unroll
@@ -193,7 +169,11 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
         }
     }
     __syncthreads();
-    if constexpr (PPT > 0) asum[0] = (red_i[0] + red_i[1]) + (red_i[2] + red_i[3]);
+    if constexpr (PPT > 0) {
+        asum[0] = 0;
+#pragma unroll
+        for (int i = 0; i < kNT / 64; ++i) asum[0] += red_i[i];
+    }
     WF_STAMP(1);
     WF_STAMP_DRAIN(13);
 
@@ -327,18 +307,18 @@ __global__ __launch_bounds__(256) void k_embed(const uint16_t* __restrict__ embe
 
 // One block per row: rms_norm + quantize -> q8/sf/asum (Y16 = false), or the final norm -> bf16.
 template <int PPT, bool Y16>
-__global__ __launch_bounds__(256) void k_rownorm(const uint16_t* __restrict__ x, int64_t xs,
+__global__ __launch_bounds__(kNT) void k_rownorm(const uint16_t* __restrict__ x, int64_t xs,
                                                  const uint16_t* __restrict__ nw, int K, float eps,
                                                  int8_t* __restrict__ q8, int64_t q8s, float* __restrict__ sf,
                                                  int* __restrict__ asum, uint16_t* __restrict__ y16, int64_t ys) {
-    __shared__ float red[8];
-    __shared__ int red_i[4];
+    __shared__ float red[2 * kNT / 64];
+    __shared__ int red_i[kNT / 64];
     const int b = blockIdx.x;
-    NormRow<PPT> nr;
+    NormRow<PPT, kNT> nr;
     nr.issue(x + (int64_t)b * xs, nw, K);
     float y[PPT][8];
     if constexpr (Y16) {
-        (void)norm_row<PPT>(nr, K, eps, y, red, false);
+        (void)norm_row(nr, K, eps, y, red, false);
 #pragma unroll
         for (int i = 0; i < PPT; ++i) {
             const int p = threadIdx.x + kNT * i;
@@ -348,13 +328,15 @@ __global__ __launch_bounds__(256) void k_rownorm(const uint16_t* __restrict__ x,
                                pk_bf16(y[i][6], y[i][7]));
         }
     } else {
-        const float s = norm_row<PPT>(nr, K, eps, y, red);
-        int as = quant_row<PPT>(y, s, K / 8, q8 + (int64_t)b * q8s, [](int p) { return 8 * p; });
+        const float s = norm_row(nr, K, eps, y, red);
+        int as = quant_row<PPT, kNT>(y, s, K / 8, q8 + (int64_t)b * q8s, [](int p) { return 8 * p; });
         as = wave_sum_i(as);
         if ((threadIdx.x & 63) == 0) red_i[threadIdx.x >> 6] = as;
         __syncthreads();
         if (threadIdx.x == 0) {
-            asum[b] = (red_i[0] + red_i[1]) + (red_i[2] + red_i[3]);
+            int t = 0;
+            for (int i = 0; i < kNT / 64; ++i) t += red_i[i];
+            asum[b] = t;
             sf[b] = s;
         }
     }
@@ -362,20 +344,20 @@ __global__ __launch_bounds__(256) void k_rownorm(const uint16_t* __restrict__ x,
 
 // Batch > 1 O-projection input: attention row from the partials -> rms_norm -> int8 codes.
 template <int PPT>
-__global__ __launch_bounds__(256) void k_rownorm_attn(const float2* __restrict__ ml, const float* __restrict__ o, int Hq,
+__global__ __launch_bounds__(kNT) void k_rownorm_attn(const float2* __restrict__ ml, const float* __restrict__ o, int Hq,
                                                       const uint16_t* __restrict__ nw, float eps, int8_t* __restrict__ q8,
                                                       int64_t q8s, float* __restrict__ sf, int* __restrict__ asum) {
-    __shared__ float red[8];
-    __shared__ int red_i[4];
+    __shared__ float red[2 * kNT / 64];
+    __shared__ int red_i[kNT / 64];
     const int b = blockIdx.x, K = Hq * 128;
-    AttnRow<PPT> ar;
+    AttnRow<PPT, kNT> ar;
     ar.issue(ml, o, b, Hq, 128);
-    NormRow<PPT> nr;
+    NormRow<PPT, kNT> nr;
     nr.issue_w(nw, K);
     float y[PPT][8];
     ar.finish(Hq, 128, y);
-    const float s = norm_core<PPT>(nr, K, eps, y, red);
-    int as = quant_row<PPT>(y, s, K / 8, q8 + (int64_t)b * q8s, [](int p) { return 8 * p; });
+    const float s = norm_core(nr, K, eps, y, red);
+    int as = quant_row<PPT, kNT>(y, s, K / 8, q8 + (int64_t)b * q8s, [](int p) { return 8 * p; });
     as = wave_sum_i(as);
     if ((threadIdx.x & 63) == 0) red_i[threadIdx.x >> 6] = as;
     __syncthreads();
@@ -548,28 +530,30 @@ using namespace wf;
 
 namespace {
 
-// lanes per weight row (16 rows per 256-thread block at 16; QKV needs 16 for its RoPE pairing)
-constexpr int kLprGU = 8;   // 32 rows = two gate/up tiles per block: 432 blocks at I = 6912
-constexpr int kLprDN = 16;  // 160 blocks at H = 2560
+// lanes per weight row of the kNT-thread GEMV blocks (QKV needs 16 rows per block for its RoPE
+// pairing)
+constexpr int kLprQKV = kNT / 16;  // 240 blocks at 2B
+constexpr int kLprO = kNT / 16;    // 160 blocks
+constexpr int kLprGU = 8;          // 64 rows = four gate/up tiles per block: 216 blocks at I = 6912
+constexpr int kLprDN = kNT / 16;   // 160 blocks
 
 int64_t wrow_bytes(int fmt, int K) { return fmt == WF_FMT_TQ ? FmtTQ::row_bytes(K) : FmtI2S::row_bytes(K); }
 int k_pad(int fmt, int K) { return fmt == WF_FMT_TQ ? FmtTQ::k_pad(K) : FmtI2S::k_pad(K); }
 // 8-element pieces per thread of the norm prologue / k_rownorm
-int norm_ppt(int kpad) { return kpad <= 2 * 8 * kNT ? 2 : 4; }
+int norm_ppt(int kpad) { return kpad <= 8 * kNT ? 1 : 2; }
 
 template <class F, int MODE, int LPR>
 int launch_gemv(const GemvArgs& ga, hipStream_t st) {
-    constexpr int RPB = 256 / LPR;
+    constexpr int RPB = kNT / LPR;
     const int img = lds_image_bytes<F>(ga.K);
     const int gx = (ga.N + RPB - 1) / RPB;
     const int B = ga.B;
 #define WF_G(MBV, PPTV)                                                                                         \
-    hipLaunchKernelGGL((k_gemv<F, MODE, LPR, MBV, PPTV>), dim3(gx + (B == 1 ? pf : 0), B / MBV), dim3(256),     \
+    hipLaunchKernelGGL((k_gemv<F, MODE, LPR, MBV, PPTV>), dim3(gx, B / MBV), dim3(kNT),     \
                        (size_t)img * MBV, st, ga)
-    const int pf = MODE == MODE_QKV ? 2 * ga.Hkv * kPfParts : 0;  // KV prefetch blocks (batch 1)
     if (B == 1) {
-        if (norm_ppt(F::k_pad(ga.K)) == 2) WF_G(1, 2);
-        else WF_G(1, 4);
+        if (norm_ppt(F::k_pad(ga.K)) == 1) WF_G(1, 1);
+        else WF_G(1, 2);
     } else if (B % 8 == 0) WF_G(8, 0);
     else if (B % 4 == 0) WF_G(4, 0);
     else if (B % 2 == 0) WF_G(2, 0);
@@ -588,16 +572,16 @@ int launch_gemv_fmt(int fmt, const GemvArgs& ga, hipStream_t st) {
 void launch_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, const uint16_t* nw, int K, uint16_t* y16,
                     hipStream_t st) {
     const wf_model_desc& d = m->d;
-    const bool big = norm_ppt(K) != 2;
+    const bool big = norm_ppt(K) != 1;
 #define WF_RN(PPTV, Y)                                                                                            \
-    hipLaunchKernelGGL((k_rownorm<PPTV, Y>), dim3(d.batch), dim3(256), 0, st, x, xs, nw, K, d.eps, m->q8, m->q8_stride, \
+    hipLaunchKernelGGL((k_rownorm<PPTV, Y>), dim3(d.batch), dim3(kNT), 0, st, x, xs, nw, K, d.eps, m->q8, m->q8_stride, \
                        m->act_sf, m->act_sum, y16, (int64_t)K)
     if (y16) {
-        if (big) WF_RN(4, true);
-        else WF_RN(2, true);
+        if (big) WF_RN(2, true);
+        else WF_RN(1, true);
     } else {
-        if (big) WF_RN(4, false);
-        else WF_RN(2, false);
+        if (big) WF_RN(2, false);
+        else WF_RN(1, false);
     }
 #undef WF_RN
 }
@@ -653,7 +637,7 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             a.N = m->qkv_rows; a.K = H; a.ws0 = wsh[0]; a.ws1 = wsh[1]; a.ws2 = wsh[2];
             a.out = m->qbuf; a.out_stride = (int64_t)d.n_heads * D;
             if ((rc = gemv_input(m, a, m->h_a, H, d.ln_in + (int64_t)l * H, st))) return rc;
-            return launch_gemv_fmt<MODE_QKV, 16>(d.wfmt, a, st);
+            return launch_gemv_fmt<MODE_QKV, kLprQKV>(d.wfmt, a, st);
         case WF_OP_ATTN:  // split partials; merged by the O projection's input stage
             return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, a.kv_b_stride, (int64_t)S * D,
                                              B, d.n_heads, d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D),
@@ -666,14 +650,14 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             a.part_o = m->part_o;
             if (B > 1) {
 #define WF_RA(PPTV)                                                                                                  \
-    hipLaunchKernelGGL((k_rownorm_attn<PPTV>), dim3(B), dim3(256), 0, st, m->part_ml, m->part_o, d.n_heads, a.nw, d.eps, \
+    hipLaunchKernelGGL((k_rownorm_attn<PPTV>), dim3(B), dim3(kNT), 0, st, m->part_ml, m->part_o, d.n_heads, a.nw, d.eps, \
                        m->q8, m->q8_stride, m->act_sf, m->act_sum)
-                if (norm_ppt(H) == 2) WF_RA(2);
-                else WF_RA(4);
+                if (norm_ppt(H) == 1) WF_RA(1);
+                else WF_RA(2);
 #undef WF_RA
                 if ((rc = check_launch("rownorm_attn"))) return rc;
             }
-            return launch_gemv_fmt<MODE_O, 16>(d.wfmt, a, st);
+            return launch_gemv_fmt<MODE_O, kLprO>(d.wfmt, a, st);
         case WF_OP_GATE_UP:  // act = relu(gate)^2 * up of rms_norm(post_attention_layernorm)(h_b)
             a.w = d.w_gu + (int64_t)l * 2 * I * wrow_bytes(d.wfmt, H); a.N = 2 * I; a.K = H;
             a.ws0 = wsh[4]; a.ws1 = wsh[5]; a.out = m->act; a.out_stride = I;

@@ -123,29 +123,28 @@ inline void* g_stamps_addr() {
 #endif
 
 // ---------------------------------------------------------------------------------------------
-// rms_norm -> int8 activation quantizer for one row, 256 threads, 8-element pieces
-// (p = threadIdx.x + 256 * i, i < PPT). Float sequence of the reference
+// rms_norm -> int8 activation quantizer for one row, NT threads (256 or 512), 8-element pieces
+// (p = threadIdx.x + NT * i, i < PPT). Float sequence of the reference
 // (scripts/direct_inference_full.py:181-184, tests/test_bitnet_core.py:139-146):
 //   r = bf16(1 / sqrt(mean(x^2) + eps)); y = bf16(bf16(x * r) * w)
 //   s = double(max|y|) / 127 (1/127 if max < 1e-6); q = clamp(rne(y / float(s)), -128, 127)
 // Loads are issued unconditionally (clamped index, masked in the arithmetic) so the caller can
 // put its own loads behind them and hipcc counts vmcnt exactly.
 // ---------------------------------------------------------------------------------------------
-constexpr int kNT = 256;  // threads per block of every decode-step kernel
 
 // Register fence: the value must exist here and nothing computed from it can move above this point
 // (hipcc otherwise hoists the input-stage math above a later weight stream, delaying its issue).
 __device__ __forceinline__ void reg_fence(uint4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
 __device__ __forceinline__ void reg_fence(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
 
-template <int PPT>
+template <int PPT, int NT>
 struct NormRow {
     uint4 x[PPT], w[PPT];
     __device__ __forceinline__ void issue(const uint16_t* __restrict__ xrow, const uint16_t* __restrict__ nw, int K) {
         const int npk = K >> 3;
 #pragma unroll
         for (int i = 0; i < PPT; ++i) {
-            const int p = min((int)threadIdx.x + kNT * i, npk - 1);
+            const int p = min((int)threadIdx.x + NT * i, npk - 1);
             x[i] = *reinterpret_cast<const uint4*>(xrow + 8 * p);
             w[i] = *reinterpret_cast<const uint4*>(nw + 8 * p);
         }
@@ -154,7 +153,7 @@ struct NormRow {
     __device__ __forceinline__ void issue_w(const uint16_t* __restrict__ nw, int K) {
         const int npk = K >> 3;
 #pragma unroll
-        for (int i = 0; i < PPT; ++i) w[i] = *reinterpret_cast<const uint4*>(nw + 8 * min((int)threadIdx.x + kNT * i, npk - 1));
+        for (int i = 0; i < PPT; ++i) w[i] = *reinterpret_cast<const uint4*>(nw + 8 * min((int)threadIdx.x + NT * i, npk - 1));
     }
     __device__ __forceinline__ void fence(bool with_x = true) {
 #pragma unroll
@@ -166,11 +165,11 @@ struct NormRow {
 };
 
 // bf16 pieces of `r.x` -> floats (0 for pieces >= K/8)
-template <int PPT>
-__device__ __forceinline__ void unpack_row(const NormRow<PPT>& r, int K, float (&y)[PPT][8]) {
+template <int PPT, int NT>
+__device__ __forceinline__ void unpack_row(const NormRow<PPT, NT>& r, int K, float (&y)[PPT][8]) {
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
-        const bool valid = (int)threadIdx.x + kNT * i < (K >> 3);
+        const bool valid = (int)threadIdx.x + NT * i < (K >> 3);
         const uint32_t w4[4] = {r.x[i].x, r.x[i].y, r.x[i].z, r.x[i].w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -181,10 +180,17 @@ __device__ __forceinline__ void unpack_row(const NormRow<PPT>& r, int K, float (
 }
 
 // Normalises the row held in `y` (x values, 0 for pieces >= K/8) in place with the norm weight in
-// `r.w`; returns the quantizer's float scale. `red` = 8 floats of LDS (two barriers inside).
-template <int PPT>
-__device__ __forceinline__ float norm_core(const NormRow<PPT>& r, int K, float eps, float (&y)[PPT][8], float* red,
+// `r.w`; returns the quantizer's float scale. `red` = 2 * NT / 64 floats of LDS (two barriers
+// inside). The cross-wave sum order is a fixed tree, so kernels with the same NT agree bit for bit.
+template <int W>
+__device__ __forceinline__ float tree_sum(const float* r) {
+    if constexpr (W == 1) return r[0];
+    else return tree_sum<W / 2>(r) + tree_sum<W / 2>(r + W / 2);
+}
+template <int PPT, int NT>
+__device__ __forceinline__ float norm_core(const NormRow<PPT, NT>& r, int K, float eps, float (&y)[PPT][8], float* red,
                                            bool want_scale = true) {
+    constexpr int NW = NT / 64;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float ss = 0.f;
 #pragma unroll
@@ -196,7 +202,7 @@ __device__ __forceinline__ float norm_core(const NormRow<PPT>& r, int K, float e
     if (lane == 0) red[wave] = ss;
     __syncthreads();
     WF_STAMP(9);
-    ss = (red[0] + red[1]) + (red[2] + red[3]);
+    ss = tree_sum<NW>(red);
     const float rr = rbf(1.0f / sqrtf(ss / (float)K + eps));
     float mx = 0.f;
 #pragma unroll
@@ -214,18 +220,20 @@ __device__ __forceinline__ float norm_core(const NormRow<PPT>& r, int K, float e
     if (!want_scale) return 0.f;
     WF_STAMP(10);
     mx = wave_max(mx);
-    if (lane == 0) red[4 + wave] = mx;
+    if (lane == 0) red[NW + wave] = mx;
     __syncthreads();
     WF_STAMP(11);
-    mx = fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7]));
+    mx = red[NW];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) mx = fmaxf(mx, red[NW + i]);
     return (float)act_scale_from_max(mx);
 }
 // unpack_row + norm_core
-template <int PPT>
-__device__ __forceinline__ float norm_row(const NormRow<PPT>& r, int K, float eps, float (&y)[PPT][8], float* red,
+template <int PPT, int NT>
+__device__ __forceinline__ float norm_row(const NormRow<PPT, NT>& r, int K, float eps, float (&y)[PPT][8], float* red,
                                           bool want_scale = true) {
-    unpack_row<PPT>(r, K, y);
-    return norm_core<PPT>(r, K, eps, y, red, want_scale);
+    unpack_row(r, K, y);
+    return norm_core(r, K, eps, y, red, want_scale);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -238,13 +246,13 @@ __device__ __forceinline__ float norm_row(const NormRow<PPT>& r, int K, float ep
 // ---------------------------------------------------------------------------------------------
 // Quantizes the normalised pieces; piece p (< npad = padded K / 8) goes to dst + off(p). Returns
 // this thread's code sum (the caller reduces it).
-template <int PPT, class Off>
+template <int PPT, int NT, class Off>
 __device__ __forceinline__ int quant_row(const float (&y)[PPT][8], float sf, int npad, int8_t* dst, Off off) {
     const float inv = 1.0f / sf;
     int asum = 0;
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
-        const int p = (int)threadIdx.x + kNT * i;
+        const int p = (int)threadIdx.x + NT * i;
         const uint2 q = quant8(y[i], sf, inv, asum);
         if (p < npad) *reinterpret_cast<uint2*>(dst + off(p)) = q;
     }
@@ -254,7 +262,7 @@ __device__ __forceinline__ int quant_row(const float (&y)[PPT][8], float sf, int
 
 constexpr int kAttnPartSplits = 8;
 
-template <int PPT>
+template <int PPT, int NT>
 struct AttnRow {
     float4 ml[PPT][kAttnPartSplits / 2];  // (m0, l0, m1, l1) pairs
     float4 oa[PPT][kAttnPartSplits], ob[PPT][kAttnPartSplits];
@@ -263,7 +271,7 @@ struct AttnRow {
         const int npk = Hq * D / 8;
 #pragma unroll
         for (int i = 0; i < PPT; ++i) {
-            const int pc = min((int)threadIdx.x + kNT * i, npk - 1);
+            const int pc = min((int)threadIdx.x + NT * i, npk - 1);
             const int h = (8 * pc) / D, d0 = 8 * pc - h * D;
             const int64_t rec = (int64_t)(b * Hq + h) * kAttnPartSplits;
 #pragma unroll
@@ -312,7 +320,7 @@ struct AttnRow {
                 for (int j = 0; j < 8; ++j) O[j] = fmaf(w, ov[j], O[j]);
             }
             const float inv = 1.0f / L;
-            const bool valid = (int)threadIdx.x + kNT * i < npk;
+            const bool valid = (int)threadIdx.x + NT * i < npk;
 #pragma unroll
             for (int j = 0; j < 8; ++j) y[i][j] = valid ? rbf(O[j] * inv) : 0.f;
         }

@@ -144,7 +144,7 @@ def weights_from_arrays(a: dict, device="cuda") -> Dict[str, torch.Tensor]:
     return w
 
 
-def build_device_layout(cfg: BitNetConfig, w: Dict[str, torch.Tensor], wfmt: int = WF_FMT_TQ):
+def build_device_layout(cfg: BitNetConfig, w: Dict[str, torch.Tensor], wfmt: int = WF_FMT_I2S):
     """Fuse per-projection I2_S weights into the kernel layout (and repack to TQ if asked)."""
     dev = w["wq"].device
     hq_tot = cfg.n_heads + 2 * cfg.n_kv_heads
@@ -164,7 +164,7 @@ class BitNetDecoder:
     """Owns the device layout, the caller-side state tensors and the wf_model handle."""
 
     def __init__(self, cfg: BitNetConfig, weights: Dict[str, torch.Tensor], batch: int = 1,
-                 wfmt: int = WF_FMT_TQ, device="cuda", debug_flags: int = 0):
+                 wfmt: int = WF_FMT_I2S, device="cuda", debug_flags: int = 0):
         self.cfg, self.batch, self.wfmt = cfg, batch, wfmt
         self.dev = torch.device(device)
         lay = build_device_layout(cfg, weights, wfmt)
