@@ -73,8 +73,9 @@ def test_gemv_model_shapes_vs_oracle(orc, n, k):
     assert np.array_equal(ops.tq_to_i2s(tq, k).cpu().numpy(), p)
 
 
-@pytest.mark.parametrize("m", [2, 3, 5, 8, 16, 33])
+@pytest.mark.parametrize("m", [2, 3, 5, 8, 16, 33, 128, 600])
 def test_gemm_batches_vs_oracle(orc, m):
+    """VALU path (M < 16) and int8-MFMA path (M >= 16, wf_mfma.hip): bit-exact vs the oracle."""
     from wfamd import ops
     rng = np.random.default_rng(m)
     w = rng.integers(-1, 2, size=(320, 1280)).astype(np.float32)

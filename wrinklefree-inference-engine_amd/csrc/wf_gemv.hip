@@ -12,6 +12,10 @@
 
 namespace wf {
 
+int launch_tgemm_mfma(const uint8_t* w, const int8_t* a, int64_t lda, float scale, int M, int N, int K, float* y,
+                      int64_t ldy, hipStream_t st);
+constexpr int kMfmaMinM = 16;  // rows from which the int8-MFMA GEMM beats the VALU dot4 stream
+
 static thread_local char g_err[512] = "";
 void set_error(const char* fmt, ...) {
     va_list ap;
@@ -324,6 +328,8 @@ int wf_bitnet_gemm_ex(int fmt, const uint8_t* w, const int8_t* a, int64_t lda, f
     WF_REQUIRE(lda >= K && lda % 16 == 0 && aligned16(a) && aligned16(w), "bitnet_gemm: activations/weights must be 16-byte aligned rows");
     WF_REQUIRE(ldy >= N, "bitnet_gemm: bad ldy");
     hipStream_t st = as_stream(stream);
+    // batched rows go to the matrix cores (wf_mfma.hip); GEMV / small M stream on the VALU
+    if (fmt == WF_FMT_I2S && M >= kMfmaMinM) return launch_tgemm_mfma(w, a, lda, scale, M, N, K, y, ldy, st);
     if (fmt == WF_FMT_I2S) return launch_ternary_gemm<FmtI2S>(w, a, lda, scale, M, N, K, y, ldy, st);
     if (fmt == WF_FMT_TQ) return launch_ternary_gemm<FmtTQ>(w, a, lda, scale, M, N, K, y, ldy, st);
     WF_REQUIRE(false, "bitnet_gemm: unknown weight format %d", fmt);
