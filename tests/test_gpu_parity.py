@@ -357,6 +357,36 @@ def test_decode_graph_equals_eager_and_batch_rows_independent():
         assert int(decb.tokens[b]) == int(dec1.tokens[0])
 
 
+def test_decode_batched_mfma_rows_match_single():
+    """Batch >= 16 runs the int8-MFMA GEMMs, the bf16-MFMA LM head and the row argmax; every row
+    (its own start token, positions 0..3) must match a batch-1 run of the same sequence: logits
+    within 1e-4 rel-L2 (the LM head sums in a different fp32 order), same greedy tokens when the
+    top-2 gap is clear."""
+    g, decb = _small_decoder(0, batch=24)
+    toks = [int(t) for t in g["tokens"]]
+    starts = [toks[b % len(toks)] for b in range(24)]
+    decb.set_state(starts, [0] * 24)
+    singles = {}
+    for t in sorted(set(starts)):
+        _, d1 = _small_decoder(0, batch=1)
+        d1.set_state([t], [0])
+        singles[t] = d1
+    for step in range(4):
+        decb.step(graph=True)
+        for d1 in singles.values():
+            d1.step(graph=True)
+        torch.cuda.synchronize()
+        for b in range(24):
+            ref = singles[starts[b]]
+            got = decb.logits[b].float().cpu().numpy()
+            exp = ref.logits[0].float().cpu().numpy()
+            assert rel_l2(got, exp) < 1e-4, (step, b, rel_l2(got, exp))
+            top2 = np.sort(exp)[-2:]
+            if top2[1] - top2[0] > 1e-2 * abs(top2[1]):
+                assert int(decb.tokens[b]) == int(ref.tokens[0]), (step, b)
+            assert int(decb.positions[b]) == step + 1
+
+
 def test_bitnet_linear_native_patch():
     """kernels/bitnet_patch.py BitNetLinearNative on the HIP kernels equals the reference formula
     (per-tensor quantize, scale = ws * act_scale, raw blocked-layout kernel, no correction)."""

@@ -292,6 +292,172 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Batched decode (B >= 16): int8-MFMA ternary GEMM (wf_mfma.hip's fragment scheme) over the codes
+// of k_rownorm, with the same fused epilogues as k_gemv. Block = 4 waves x 2 16-row MFMA tiles =
+// 128 sequences, one 16-weight-row column tile (so QKV's RoPE partner dims and GU's gate/up pairs
+// sit in lanes l and l ^ 8 of the same tile).
+// ---------------------------------------------------------------------------------------------
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+constexpr int kDecMfmaMinB = 16;
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_dec_mfma(GemvArgs a) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+    const int tile = blockIdx.x;
+    const int K = a.K, N = a.N, B = a.B;
+    const int n = tile * 16 + l16;
+    const int m_base = blockIdx.y * 128 + wave * 32;
+    const uint8_t* wp = a.w + (int64_t)min(n, N - 1) * (K / 4);
+    const int8_t* ap[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ap[i] = a.q8 + (int64_t)min(m_base + 16 * i + l16, B - 1) * a.q8_stride + 32 * q;
+    const int sh = 6 - 2 * q;
+    v4i_t acc[2] = {v4i_t{0, 0, 0, 0}, v4i_t{0, 0, 0, 0}};
+    const int steps = K / 64;
+#pragma unroll 4
+    for (int c = 0; c < steps; ++c) {
+        const int boff = 32 * (c >> 1) + 16 * (c & 1), koff = 128 * (c >> 1) + 16 * (c & 1);
+        const uint4 w = ldg_nt(wp + boff);
+        const v4i_t bf = {(int)((w.x >> sh) & 0x03030303u), (int)((w.y >> sh) & 0x03030303u),
+                          (int)((w.z >> sh) & 0x03030303u), (int)((w.w >> sh) & 0x03030303u)};
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            acc[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(*reinterpret_cast<const v4i_t*>(ap[i] + koff), bf, acc[i], 0,
+                                                           0, 0);
+    }
+    // epilogue: lane holds rows m_base + 16 i + 4 q + r of column n
+    float ws = a.ws0;
+    int proj = 0, head = 0, tt = 0;
+    if constexpr (MODE == MODE_QKV) {
+        head = tile >> 3;
+        tt = tile & 7;
+        proj = head < a.Hq ? 0 : (head < a.Hq + a.Hkv ? 1 : 2);
+        ws = proj == 0 ? a.ws0 : (proj == 1 ? a.ws1 : a.ws2);
+    } else if constexpr (MODE == MODE_GU) {
+        ws = l16 < 8 ? a.ws0 : a.ws1;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m_base + 16 * i + 4 * q + r;
+            const int mc = min(m, B - 1);
+            const float v = rbf(corrected(acc[i][r], ws, a.act_sum[mc], a.act_sf[mc]));
+            if constexpr (MODE == MODE_QKV || MODE == MODE_GU) {
+                const float pv = __shfl_xor(v, 8, 64);  // partner column l16 ^ 8 (same rows)
+                if (m >= B) continue;
+                if constexpr (MODE == MODE_GU) {
+                    if (l16 < 8) {
+                        const float g = fmaxf(v, 0.f);
+                        a.out[(int64_t)m * a.out_stride + tile * 8 + l16] = f2bf(rbf(rbf(g * g) * pv));
+                    }
+                } else {
+                    const int i8 = l16 & 7, d0 = 8 * tt + i8;
+                    const float x1 = l16 < 8 ? v : pv, x2 = l16 < 8 ? pv : v;
+                    const int pos = min(max(a.positions[m], 0), a.S - 1);
+                    float y = v;
+                    if (proj < 2) {  // RotaryEmbedding._rotate (direct_inference_full.py:58-70)
+                        const float cs = bf2f(a.rope_cos[(int64_t)pos * 64 + d0]);
+                        const float sn = bf2f(a.rope_sin[(int64_t)pos * 64 + d0]);
+                        y = l16 < 8 ? rbf(rbf(x1 * cs) - rbf(x2 * sn)) : rbf(rbf(x1 * sn) + rbf(x2 * cs));
+                    }
+                    const int d = d0 + (l16 < 8 ? 0 : 64);
+                    if (proj == 0) {
+                        a.out[(int64_t)m * a.out_stride + head * 128 + d] = f2bf(y);
+                    } else {
+                        const int g = head - a.Hq - (proj == 2 ? a.Hkv : 0);
+                        uint16_t* cache = (proj == 1 ? a.kc : a.vc) + (int64_t)m * a.kv_b_stride + ((int64_t)g * a.S + pos) * 128;
+                        cache[d] = f2bf(y);
+                    }
+                }
+            } else {  // O / DN: out = bf16(resid + bf16(o))
+                if (m >= B || n >= N) continue;
+                const int64_t o = (int64_t)m * a.out_stride + n;
+                a.out[o] = f2bf(rbf(bf2f(a.resid[o]) + v));
+            }
+        }
+}
+
+// Batched LM head: logits[b, v] = bf16(sum_k hn[b, k] E[v, k]) on v_mfma_f32_16x16x32_bf16 (lane
+// quarter q takes k = 32s + 8q + j of step s for both operands; fp32 accumulation), 128 sequences
+// x 16 vocabulary rows per block, E read once; per (row, block) (max, first index) partials.
+typedef short v8s_t __attribute__((ext_vector_type(8)));
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_lm_head_mfma(const uint16_t* __restrict__ E, const uint16_t* __restrict__ hn,
+                                                      int H, int V, int B, uint16_t* __restrict__ logits,
+                                                      uint2* __restrict__ part, int nblk) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+    const int vcol = blockIdx.x * 16 + l16;
+    const int m_base = blockIdx.y * 128 + wave * 32;
+    const uint16_t* ep = E + (int64_t)min(vcol, V - 1) * H + 8 * q;
+    const uint16_t* hp[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) hp[i] = hn + (int64_t)min(m_base + 16 * i + l16, B - 1) * H + 8 * q;
+    v4f_t acc[2] = {v4f_t{0.f, 0.f, 0.f, 0.f}, v4f_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll 4
+    for (int k0 = 0; k0 < H; k0 += 32) {
+        const v8s_t bf = __builtin_bit_cast(v8s_t, ldg_nt(reinterpret_cast<const uint8_t*>(ep + k0)));
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const v8s_t*>(hp[i] + k0), bf, acc[i], 0, 0,
+                                                            0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m_base + 16 * i + 4 * q + r;
+            const uint16_t lb = f2bf(acc[i][r]);
+            float bv = (vcol < V) ? bf2f(lb) : -INFINITY;
+            int bi = vcol;
+            if (m < B && vcol < V) logits[(int64_t)m * V + vcol] = lb;
+            // (max, first index) over the 16 columns of this row: lanes l16 of the same quarter
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) {
+                const float ov = __shfl_xor(bv, o, 64);
+                const int oi = __shfl_xor(bi, o, 64);
+                if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+            }
+            if (l16 == 0 && m < B)
+                part[(int64_t)m * nblk + blockIdx.x] = make_uint2(__float_as_uint(bv), (uint32_t)bi);
+        }
+}
+
+// Greedy token per row from the LM-head partials; advances the position.
+__global__ __launch_bounds__(256) void k_argmax_rows(const uint2* __restrict__ part, int nblk, int32_t* tokens,
+                                                     int32_t* positions, int max_seq) {
+    __shared__ float r_val[256];
+    __shared__ int r_idx[256];
+    const int b = blockIdx.x;
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = threadIdx.x; i < nblk; i += 256) {
+        const uint2 v = part[(int64_t)b * nblk + i];
+        const float fv = __uint_as_float(v.x);
+        const int id = (int)v.y;
+        if (fv > best || (fv == best && id < bi)) { best = fv; bi = id; }
+    }
+    r_val[threadIdx.x] = best;
+    r_idx[threadIdx.x] = bi;
+    __syncthreads();
+    for (int s2 = 128; s2 > 0; s2 >>= 1) {
+        if (threadIdx.x < s2) {
+            const float v2 = r_val[threadIdx.x + s2];
+            const int i2 = r_idx[threadIdx.x + s2];
+            if (v2 > r_val[threadIdx.x] || (v2 == r_val[threadIdx.x] && i2 < r_idx[threadIdx.x])) {
+                r_val[threadIdx.x] = v2;
+                r_idx[threadIdx.x] = i2;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        tokens[b] = r_idx[0];
+        positions[b] = min(positions[b] + 1, max_seq - 1);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // embed, standalone row norm (batch > 1 codes; final norm), LM head with fused greedy argmax
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_embed(const uint16_t* __restrict__ embed, const int32_t* __restrict__ tokens,
@@ -564,6 +730,10 @@ int launch_gemv(const GemvArgs& ga, hipStream_t st) {
 
 template <int MODE, int LPR>
 int launch_gemv_fmt(int fmt, const GemvArgs& ga, hipStream_t st) {
+    if (fmt == WF_FMT_I2S && ga.B >= kDecMfmaMinB) {  // batched decode on the matrix cores
+        hipLaunchKernelGGL((k_dec_mfma<MODE>), dim3((ga.N + 15) / 16, (ga.B + 127) / 128), dim3(256), 0, st, ga);
+        return check_launch("dec_mfma");
+    }
     if (fmt == WF_FMT_TQ) return launch_gemv<FmtTQ, MODE, LPR>(ga, st);
     return launch_gemv<FmtI2S, MODE, LPR>(ga, st);
 }
@@ -671,6 +841,13 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
         case WF_OP_LM_HEAD: {  // final norm -> hn, logits = hn @ embed^T, greedy token
             launch_rownorm(m, m->h_a, H, d.final_norm, H, m->hn, st);
             if ((rc = check_launch("final_norm"))) return rc;
+            if (d.wfmt == WF_FMT_I2S && B >= kDecMfmaMinB) {
+                hipLaunchKernelGGL(k_lm_head_mfma, dim3(m->lm_blocks, (B + 127) / 128), dim3(256), 0, st, d.embed, m->hn, H,
+                                   d.vocab, B, m->logits, m->am_part, m->lm_blocks);
+                hipLaunchKernelGGL(k_argmax_rows, dim3(B), dim3(256), 0, st, m->am_part, m->lm_blocks, m->tokens,
+                                   m->positions, S);
+                break;
+            }
             const size_t sh = (size_t)H * 2;
 #define WF_LM(MBV)                                                                                              \
     hipLaunchKernelGGL((k_lm_head<MBV>), dim3(m->lm_blocks, B / MBV), dim3(256), sh * MBV, st, d.embed, m->hn, \
@@ -710,8 +887,8 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_REQUIRE(d.hidden % 128 == 0 && d.inter % 128 == 0, "model_create: hidden/inter must be multiples of 128");
     WF_REQUIRE(k_pad(d.wfmt, d.hidden) <= 8192 && k_pad(d.wfmt, d.inter) <= 8192,
                "model_create: hidden/inter (padded to the weight format) > 8192 not supported");
-    WF_REQUIRE(d.batch >= 1 && d.batch <= 64 && d.max_seq >= 1 && d.vocab >= 1 && d.layers >= 1,
-               "model_create: bad sizes (batch 1..64)");
+    WF_REQUIRE(d.batch >= 1 && d.batch <= 1024 && d.max_seq >= 1 && d.vocab >= 1 && d.layers >= 1,
+               "model_create: bad sizes (batch 1..1024)");
     WF_REQUIRE(d.wfmt == WF_FMT_I2S || d.wfmt == WF_FMT_TQ, "model_create: bad weight format");
     WF_REQUIRE(d.embed && d.final_norm && d.rope_cos && d.rope_sin && d.ln_in && d.ln_post && d.attn_sub && d.ffn_sub &&
                    d.w_qkv && d.w_o && d.w_gu && d.w_d && d.wscale,
