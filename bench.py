@@ -156,6 +156,7 @@ def main():
     import torch.distributed as dist
     from wfamd import WF_FMT_I2S, WF_FMT_TQ, _lib
     from wfamd.model import BITNET_2B, BitNetDecoder, synthetic_weights
+    from wfamd.replicas import replica_rate, timed_steps
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -180,22 +181,9 @@ def main():
 
     for _ in range(args.warmup):
         dec.step(graph=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        dec.step(graph=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    tok_s = B * args.steps * world / el
+    el = timed_steps(lambda: dec.step(graph=True), args.steps, torch.cuda.synchronize,
+                     dist if world > 1 else None, device="cuda")
+    tok_s = replica_rate(B, args.steps, world, el)
     ms_step = 1000.0 * el / args.steps
 
     kern = {} if args.no_op_timing else op_timing(dec, ctx + total // 2)

@@ -51,6 +51,16 @@ int wf_bitnet_gemm(const uint8_t* w, const int8_t* a, float scale, int M, int N,
 /* Same contract, any weight format and strides (lda/ldy in elements, lda % 16 == 0). */
 int wf_bitnet_gemm_ex(int fmt, const uint8_t* w, const int8_t* a, int64_t lda, float scale, int M, int N, int K,
                       float* y, int64_t ldy, void* stream);
+/* BitNetLinear.forward, fused (scripts/direct_inference_full.py:186-208, the layer the reference's
+ * decode runs 7x per block; kernels/bitnet_patch.py:55-78 is the same contract without the
+ * correction): per row m, s = double(max|x[m]|)/127, q = rne(x/float(s)), then
+ * y[m,n] = bf16(fl32(fl32(sum_k enc(W[n,k]) q[k] - ws * sum_k q[k]) * s)).  x, y bf16 (row strides
+ * ldx, ldy in elements; ldx % 8 == 0), W I2_S or TQ [N][row bytes], K % 128 == 0, K <= 8192.
+ * M < 16 is one launch (quantize in the GEMV prologue); M >= 16 with I2_S needs a 16-byte aligned
+ * workspace of wf_bitnet_linear_ws_bytes(M, K) bytes (per-row codes for the int8-MFMA GEMM). */
+int64_t wf_bitnet_linear_ws_bytes(int M, int K);
+int wf_bitnet_linear(int fmt, const uint8_t* w, const uint16_t* x, int64_t ldx, float ws, int M, int N, int K,
+                     uint16_t* y, int64_t ldy, void* workspace, void* stream);
 /* kernels/native.py:27-65 (wrinklefree_inference.kernels.native gemv/gemm): signed (bits-1) dot
  * on the LSB-interleaved layout byte[j] = w[4j] | w[4j+1]<<2 | ..., float(sum) * scale. */
 int wf_bitnet_gemm_lsb(const uint8_t* w, const int8_t* a, float scale, int M, int N, int K, float* y, void* stream);

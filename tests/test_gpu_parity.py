@@ -404,3 +404,64 @@ def test_bitnet_linear_native_patch():
     y1 = lin(cu(x[:1])).cpu().numpy()
     q1, s1 = orc.quantize_i8(x[:1])
     assert np.array_equal(y1, orc.gemm_i2s(p, q1, np.float32(1.5 * s1)))
+
+
+# ------------------------------------------------------------------------------------------------
+# f1: fused BitNetLinear (scripts/direct_inference_full.py:186-208)
+# ------------------------------------------------------------------------------------------------
+def test_bitnet_linear_golden_bitexact():
+    """One row: quantize + ternary GEMV + correction in one launch, bf16 bit-exact with the vectors
+    the reference's own functions produced (tests/golden/make_golden.py gen_linear)."""
+    from wfamd import ops
+    from wfamd._lib import WF_FMT_TQ
+    g = load_golden("linear")
+    for i in range(3):
+        p, x, ws, y = g[f"p{i}"], g[f"x{i}"], float(g[f"ws{i}"]), g[f"y{i}"]
+        xt = cu(x.view(np.int16)).view(torch.bfloat16)
+        out = ops.bitnet_linear(xt, cu(p), ws)
+        assert np.array_equal(bits(out), y), i
+        tq = ops.i2s_to_tq(cu(p))
+        out_tq = ops.bitnet_linear(xt, tq, ws, WF_FMT_TQ, in_features=x.shape[0])
+        assert np.array_equal(bits(out_tq), y), i
+
+
+@pytest.mark.parametrize("m,n,k", [(1, 2560, 2560), (3, 100, 640), (7, 640, 2560), (16, 2560, 2560),
+                                   (40, 136, 6912), (129, 3840, 2560), (300, 13824, 2560)])
+def test_bitnet_linear_rows_vs_oracle(orc, m, n, k):
+    """Every row bf16 bit-exact with the oracle's per-row linear (M < 16: GEMV prologue path;
+    M >= 16: row quantizer + int8 MFMA GEMM), ragged N, strided input rows."""
+    from wfamd import ops
+    rng = np.random.default_rng(m * 131 + n + k)
+    w = rng.integers(-1, 2, size=(n, k)).astype(np.float32)
+    p = orc.pack_i2s(w)
+    x = (rng.standard_normal((m, k + 64)) * rng.uniform(0.05, 3.0, size=(m, 1))).astype(np.float32)
+    x[0, 5] = 40.0  # an outlier sets a row's scale
+    xb = orc.f32_to_bf16(x)
+    xt = cu(xb.view(np.int16)).view(torch.bfloat16)[:, :k]  # row stride k + 64
+    out = bits(ops.bitnet_linear(xt, cu(p), 1.25))
+    for r in range(m):
+        ref = orc.bitnet_linear_bf16(np.ascontiguousarray(xb[r, :k]), p, 1.25)
+        assert np.array_equal(out[r], ref), r
+
+
+def test_bitnet_linear_module_and_errors():
+    from wfamd import ops
+    from wfamd._lib import WF_FMT_TQ
+    from wfamd.linear import BitNetLinear
+    from oracle import oracle as orc
+    rng = np.random.default_rng(21)
+    w = rng.integers(-1, 2, size=(256, 512)).astype(np.float32)
+    x = torch.randn(2, 3, 512, device="cuda").to(torch.bfloat16)
+    lin = BitNetLinear.from_ternary(torch.from_numpy(w), 0.75)
+    lin_tq = BitNetLinear.from_ternary(torch.from_numpy(w), 0.75, fmt=WF_FMT_TQ)
+    y, y_tq = lin(x), lin_tq(x)
+    assert y.shape == (2, 3, 256) and y.dtype == torch.bfloat16
+    assert torch.equal(y, y_tq)
+    p = orc.pack_i2s(w)
+    xb = bits(x.reshape(6, 512))
+    for r in range(6):
+        assert np.array_equal(bits(y.reshape(6, 256))[r], orc.bitnet_linear_bf16(xb[r], p, 0.75))
+    with pytest.raises(ValueError):
+        ops.bitnet_linear(x.float(), lin.packed_weight, 0.75)
+    with pytest.raises(ValueError):
+        ops.bitnet_linear(x[..., :384], lin.packed_weight, 0.75)

@@ -458,26 +458,28 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
 int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
                               float2* ml, float* o, hipStream_t st) {
-    // one block per query head (G = 1): 4x the blocks of one per kv head at Hq/Hkv = 4, a quarter of
-    // the per-lane arithmetic (the kernel is latency-bound on its score/softmax chain at 1 wave/SIMD)
-    const dim3 grid(kAttnPartSplits, Hq, B);
     const int grp = Hq / Hkv;
-    if (grp <= 8) {
-        hipLaunchKernelGGL((k_attn_part<1>), grid, dim3(kAttnPartThreads), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S,
-                           seq_lens, sm_scale, ml, o);
+    if (grp > 8) {
+        set_error("decode_attention_partials: GQA group %d > 8", grp);
+        return WF_EINVAL;
+    }
+    if (B < 16) {
+        // one block per query head (G = 1): 4x the blocks of one per kv head at Hq/Hkv = 4, a quarter
+        // of the per-lane arithmetic (at batch 1 the kernel is latency-bound on its score/softmax
+        // chain; the K/V re-reads of the group's heads hit L2)
+        hipLaunchKernelGGL((k_attn_part<1>), dim3(kAttnPartSplits, Hq, B), dim3(kAttnPartThreads), 0, st, q, q_sb, k, v,
+                           kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, ml, o);
         return check_launch("decode_attention_partials");
     }
+    // batched: one block per kv head, the group's query heads share every K/V load (KV-bound)
+    const dim3 grid(kAttnPartSplits, Hkv, B);
 #define WF_AP(GV)                                                                                                   \
     hipLaunchKernelGGL((k_attn_part<GV>), grid, dim3(kAttnPartThreads), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, \
                        seq_lens, sm_scale, ml, o)
     if (grp == 1) WF_AP(1);
     else if (grp == 2) WF_AP(2);
     else if (grp <= 4) WF_AP(4);
-    else if (grp <= 8) WF_AP(8);
-    else {
-        set_error("decode_attention_partials: GQA group %d > 8", grp);
-        return WF_EINVAL;
-    }
+    else WF_AP(8);
 #undef WF_AP
     return check_launch("decode_attention_partials");
 }

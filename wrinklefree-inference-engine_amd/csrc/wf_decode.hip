@@ -18,18 +18,20 @@
 // up to fp32 reduction order.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <new>
 
 #include "wf_common.h"
 #include "wf_device.h"
 #include "wf_norm.h"
+#include "wf_mfma.h"
 
 namespace wf {
 int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
                               float2* ml, float* o, hipStream_t st);
 
-enum { MODE_QKV = 0, MODE_O = 1, MODE_GU = 2, MODE_DN = 3 };
+enum { MODE_QKV = 0, MODE_O = 1, MODE_GU = 2, MODE_DN = 3, MODE_LINEAR = 4 };  // LINEAR: BitNetLinear drop-in
 constexpr int kNT = 512;  // threads per GEMV / row-norm block (8 waves: 2 per SIMD hide the input-stage latency)
 
 struct GemvArgs {
@@ -56,6 +58,8 @@ struct GemvArgs {
     // QKV extras
     int Hq, Hkv, S;
     const int32_t* positions;
+    int* ws;                   // batched decode: split-K int32 partials
+    size_t ws_ints;
     const uint16_t* rope_cos;
     const uint16_t* rope_sin;
     uint16_t* kc;
@@ -105,7 +109,9 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
     if constexpr (kAttnIn) {
         ar.issue(a.part_ml, a.part_o, b0, a.Hq, 128);
         nr.issue_w(a.nw, K);
-    } else if constexpr (PPT > 0) {
+    } else if constexpr (PPT > 0 && MODE == MODE_LINEAR) {
+        nr.issue_x(a.x + (int64_t)b0 * a.x_stride, K);
+} else if constexpr (PPT > 0) {
         nr.issue(a.x + (int64_t)b0 * a.x_stride, a.nw, K);
     } else {
 #pragma unroll
@@ -138,7 +144,7 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
         ar.fence();
         nr.fence(false);
     } else if constexpr (PPT > 0) {
-        nr.fence();
+        nr.fence(true, MODE != MODE_LINEAR);
     }
     __builtin_amdgcn_sched_barrier(0);
     float sf[MB];
@@ -148,6 +154,9 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
         if constexpr (kAttnIn) {
             ar.finish(a.Hq, 128, y);
             sf[0] = norm_core(nr, K, a.eps, y, red);
+        } else if constexpr (MODE == MODE_LINEAR) {  // quantize x itself (no norm)
+            unpack_row(nr, K, y);
+            sf[0] = absmax_scale<PPT, kNT>(y, red);
         } else {
             sf[0] = norm_row(nr, K, a.eps, y, red);
         }
@@ -250,6 +259,18 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
         }
         WF_STAMP(7);
         return;
+    } else if constexpr (MODE == MODE_LINEAR) {
+        // BitNetLinear (direct_inference_full.py:186-208): y = bf16(fl32(fl32(raw - ws*sum(q)) * s))
+        if (sub == 0) {
+#pragma unroll
+            for (int m = 0; m < MB; ++m) s_out[m][lrow] = corrected(acc[m], a.ws0, asum[m], sf[m]);
+        }
+        __syncthreads();
+        if (threadIdx.x < MB * RPB) {
+            const int m = threadIdx.x / RPB, i = threadIdx.x % RPB;
+            const int n = blockIdx.x * RPB + i;
+            if (n < N) a.out[(int64_t)(b0 + m) * a.out_stride + n] = f2bf(s_out[m][i]);
+        }
     } else {
         // O/DN: out[row] = bf16(resid + bf16(o)); GU: act[8t+i] = bf16(bf16(relu(g)^2) * u)
         if (sub == 0) {
@@ -297,130 +318,251 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
 // 128 sequences, one 16-weight-row column tile (so QKV's RoPE partner dims and GU's gate/up pairs
 // sit in lanes l and l ^ 8 of the same tile).
 // ---------------------------------------------------------------------------------------------
-typedef int v4i_t __attribute__((ext_vector_type(4)));
 constexpr int kDecMfmaMinB = 16;
 
+// Fused decode-step epilogue of one 16 x 16 output tile (rows = sequences, columns = 16 weight rows
+// = one QKV RoPE block / one gate-up tile): lane holds rows r0 + 4q + r of column c0 + l16.
 template <int MODE>
-__global__ __launch_bounds__(256) void k_dec_mfma(GemvArgs a) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
-    const int tile = blockIdx.x;
-    const int K = a.K, N = a.N, B = a.B;
-    const int n = tile * 16 + l16;
-    const int m_base = blockIdx.y * 128 + wave * 32;
-    const uint8_t* wp = a.w + (int64_t)min(n, N - 1) * (K / 4);
-    const int8_t* ap[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) ap[i] = a.q8 + (int64_t)min(m_base + 16 * i + l16, B - 1) * a.q8_stride + 32 * q;
-    const int sh = 6 - 2 * q;
-    v4i_t acc[2] = {v4i_t{0, 0, 0, 0}, v4i_t{0, 0, 0, 0}};
-    const int steps = K / 64;
-#pragma unroll 4
-    for (int c = 0; c < steps; ++c) {
-        const int boff = 32 * (c >> 1) + 16 * (c & 1), koff = 128 * (c >> 1) + 16 * (c & 1);
-        const uint4 w = ldg_nt(wp + boff);
-        const v4i_t bf = {(int)((w.x >> sh) & 0x03030303u), (int)((w.y >> sh) & 0x03030303u),
-                          (int)((w.z >> sh) & 0x03030303u), (int)((w.w >> sh) & 0x03030303u)};
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-            acc[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(*reinterpret_cast<const v4i_t*>(ap[i] + koff), bf, acc[i], 0,
-                                                           0, 0);
-    }
-    // epilogue: lane holds rows m_base + 16 i + 4 q + r of column n
-    float ws = a.ws0;
-    int proj = 0, head = 0, tt = 0;
-    if constexpr (MODE == MODE_QKV) {
-        head = tile >> 3;
-        tt = tile & 7;
-        proj = head < a.Hq ? 0 : (head < a.Hq + a.Hkv ? 1 : 2);
-        ws = proj == 0 ? a.ws0 : (proj == 1 ? a.ws1 : a.ws2);
-    } else if constexpr (MODE == MODE_GU) {
-        ws = l16 < 8 ? a.ws0 : a.ws1;
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
+struct EpiDec {
+    const GemvArgs* a;
+    __device__ __forceinline__ void apply(int r0, int c0, const v4i_t& acc, int l16, int q) {
+        const GemvArgs& g = *a;
+        const int tile = c0 >> 4, n = c0 + l16, B = g.B, N = g.N;
+        float ws = g.ws0;
+        int proj = 0, head = 0, tt = 0;
+        if constexpr (MODE == MODE_QKV) {
+            head = tile >> 3;
+            tt = tile & 7;
+            proj = head < g.Hq ? 0 : (head < g.Hq + g.Hkv ? 1 : 2);
+            ws = proj == 0 ? g.ws0 : (proj == 1 ? g.ws1 : g.ws2);
+        } else if constexpr (MODE == MODE_GU) {
+            ws = l16 < 8 ? g.ws0 : g.ws1;
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int m = m_base + 16 * i + 4 * q + r;
+            const int m = r0 + 4 * q + r;
             const int mc = min(m, B - 1);
-            const float v = rbf(corrected(acc[i][r], ws, a.act_sum[mc], a.act_sf[mc]));
+            const float v = rbf(corrected(acc[r], ws, g.act_sum[mc], g.act_sf[mc]));
             if constexpr (MODE == MODE_QKV || MODE == MODE_GU) {
                 const float pv = __shfl_xor(v, 8, 64);  // partner column l16 ^ 8 (same rows)
-                if (m >= B) continue;
+                if (m >= B || tile * 16 >= N) continue;
                 if constexpr (MODE == MODE_GU) {
                     if (l16 < 8) {
-                        const float g = fmaxf(v, 0.f);
-                        a.out[(int64_t)m * a.out_stride + tile * 8 + l16] = f2bf(rbf(rbf(g * g) * pv));
+                        const float gt = fmaxf(v, 0.f);
+                        g.out[(int64_t)m * g.out_stride + tile * 8 + l16] = f2bf(rbf(rbf(gt * gt) * pv));
                     }
                 } else {
-                    const int i8 = l16 & 7, d0 = 8 * tt + i8;
+                    const int d0 = 8 * tt + (l16 & 7);
                     const float x1 = l16 < 8 ? v : pv, x2 = l16 < 8 ? pv : v;
-                    const int pos = min(max(a.positions[m], 0), a.S - 1);
+                    const int pos = min(max(g.positions[m], 0), g.S - 1);
                     float y = v;
                     if (proj < 2) {  // RotaryEmbedding._rotate (direct_inference_full.py:58-70)
-                        const float cs = bf2f(a.rope_cos[(int64_t)pos * 64 + d0]);
-                        const float sn = bf2f(a.rope_sin[(int64_t)pos * 64 + d0]);
+                        const float cs = bf2f(g.rope_cos[(int64_t)pos * 64 + d0]);
+                        const float sn = bf2f(g.rope_sin[(int64_t)pos * 64 + d0]);
                         y = l16 < 8 ? rbf(rbf(x1 * cs) - rbf(x2 * sn)) : rbf(rbf(x1 * sn) + rbf(x2 * cs));
                     }
                     const int d = d0 + (l16 < 8 ? 0 : 64);
                     if (proj == 0) {
-                        a.out[(int64_t)m * a.out_stride + head * 128 + d] = f2bf(y);
+                        g.out[(int64_t)m * g.out_stride + head * 128 + d] = f2bf(y);
                     } else {
-                        const int g = head - a.Hq - (proj == 2 ? a.Hkv : 0);
-                        uint16_t* cache = (proj == 1 ? a.kc : a.vc) + (int64_t)m * a.kv_b_stride + ((int64_t)g * a.S + pos) * 128;
+                        const int kvh = head - g.Hq - (proj == 2 ? g.Hkv : 0);
+                        uint16_t* cache =
+                            (proj == 1 ? g.kc : g.vc) + (int64_t)m * g.kv_b_stride + ((int64_t)kvh * g.S + pos) * 128;
                         cache[d] = f2bf(y);
                     }
                 }
             } else {  // O / DN: out = bf16(resid + bf16(o))
                 if (m >= B || n >= N) continue;
-                const int64_t o = (int64_t)m * a.out_stride + n;
-                a.out[o] = f2bf(rbf(bf2f(a.resid[o]) + v));
+                const int64_t o = (int64_t)m * g.out_stride + n;
+                g.out[o] = f2bf(rbf(bf2f(g.resid[o]) + v));
             }
         }
+    }
+};
+
+// Batched decode GEMM, split-K: block (j, s, rb) = 128 sequences x 128 weight rows over k-step
+// slice s (wf_mfma.h LDS-DMA pipeline), exact int32 partial sums to ws[s][B][N]; k_dec_epi adds
+// the slices (fixed order, exact) and runs the fused epilogue. Splitting K spreads the 20-108
+// column blocks of a layer over ~256+ CUs (one CU's LDS-DMA stream alone is ~25-30 GB/s).
+struct EpiPartial {
+    int* ws;
+    int B, N;
+    __device__ __forceinline__ void apply(int r0, int c0, const v4i_t& acc, int l16, int q) {
+        const int n = c0 + l16;
+        if (n >= N) return;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = r0 + 4 * q + r;
+            if (m < B) ws[(int64_t)m * N + n] = acc[r];
+        }
+    }
+};
+
+__global__ __launch_bounds__(256) void k_dec_mfma_part(GemvArgs a, int* __restrict__ ws, int steps_per_split) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kTgStagesWide * kTgStageBytes];
+    const int s = blockIdx.y;
+    const int c0 = s * steps_per_split, c1 = min(c0 + steps_per_split, a.K / 64);
+    EpiPartial e{ws + (int64_t)s * a.B * a.N, a.B, a.N};
+    tgemm_tile<2, kTgStagesWide>(a.w, a.q8, a.q8_stride, a.B, a.N, a.K, blockIdx.z * 128, blockIdx.x * 128, lds, e, c0,
+                                 c1);
 }
 
-// Batched LM head: logits[b, v] = bf16(sum_k hn[b, k] E[v, k]) on v_mfma_f32_16x16x32_bf16 (lane
-// quarter q takes k = 32s + 8q + j of step s for both operands; fp32 accumulation), 128 sequences
-// x 16 vocabulary rows per block, E read once; per (row, block) (max, first index) partials.
+// One wave per 16 x 16 output tile: lane (l16, q) sums the nsplit int32 partials of rows
+// r0 + 4q + r, column c0 + l16 and runs EpiDec on them (same fragment layout as the GEMM).
+template <int MODE>
+__global__ __launch_bounds__(256) void k_dec_epi(GemvArgs a, const int* __restrict__ ws, int nsplit) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+    const int c0 = (blockIdx.x * 4 + wave) * 16, r0 = blockIdx.y * 16;
+    if (c0 >= a.N) return;  // whole wave
+    const int n = min(c0 + l16, a.N - 1);
+    v4i_t acc = {0, 0, 0, 0};
+    const int64_t plane = (int64_t)a.B * a.N;
+    for (int s = 0; s < nsplit; ++s)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] += ws[s * plane + (int64_t)min(r0 + 4 * q + r, a.B - 1) * a.N + n];
+    EpiDec<MODE> e{&a};
+    e.apply(r0, c0, acc, l16, q);
+}
+
+// BitNetLinear for many rows: per-row int8 codes (k_quant_rows_lin) -> MFMA GEMM -> this epilogue.
+struct EpiLinear {
+    const GemvArgs* a;
+    __device__ __forceinline__ void apply(int r0, int c0, const v4i_t& acc, int l16, int q) {
+        const GemvArgs& g = *a;
+        const int n = c0 + l16;
+        if (n >= g.N) return;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = r0 + 4 * q + r;
+            if (m < g.B) g.out[(int64_t)m * g.out_stride + n] = f2bf(corrected(acc[r], g.ws0, g.act_sum[m], g.act_sf[m]));
+        }
+    }
+};
+__global__ __launch_bounds__(256) void k_linear_mfma(GemvArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kTgStagesWide * kTgStageBytes];
+    EpiLinear e{&a};
+    tgemm_tile<2, kTgStagesWide>(a.w, a.q8, a.q8_stride, a.B, a.N, a.K, blockIdx.y * 128, blockIdx.x * 128, lds, e);
+}
+// per-row activation quantizer of BitNetLinear: codes, float scale, code sum
+template <int PPT>
+__global__ __launch_bounds__(kNT) void k_quant_rows_lin(const uint16_t* __restrict__ x, int64_t xs, int K,
+                                                        int8_t* __restrict__ q8, int64_t q8s, float* __restrict__ sf,
+                                                        int* __restrict__ asum) {
+    __shared__ float red[2 * kNT / 64];
+    __shared__ int red_i[kNT / 64];
+    const int b = blockIdx.x;
+    NormRow<PPT, kNT> nr;
+    const int npk = K >> 3;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) nr.x[i] = *reinterpret_cast<const uint4*>(x + b * xs + 8 * min((int)threadIdx.x + kNT * i, npk - 1));
+    float y[PPT][8];
+    unpack_row(nr, K, y);
+    const float s = absmax_scale<PPT, kNT>(y, red);
+    int as = quant_row<PPT, kNT>(y, s, K / 8, q8 + (int64_t)b * q8s, [](int p) { return 8 * p; });
+    as = wave_sum_i(as);
+    if ((threadIdx.x & 63) == 0) red_i[threadIdx.x >> 6] = as;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int i = 0; i < kNT / 64; ++i) t += red_i[i];
+        asum[b] = t;
+        sf[b] = s;
+    }
+}
+
+// Batched LM head: logits[b, v] = bf16(sum_k hn[b, k] E[v, k]) on v_mfma_f32_16x16x32_bf16 (fp32
+// accumulation; lane quarter q takes k = 32s + 8q + 0..7 of step s for both operands). Block = 128
+// sequences x 256 vocabulary rows, 4 waves x 64 rows; each k-step is an LDS-DMA pipeline stage
+// (wf_mfma.h scheme): A = hn 8 KiB (wave w loads row tiles 2w, 2w+1), B = the wave's 64 embedding
+// rows x 64 B = 4 KiB; 6 DMA loads per wave per stage. E is read from HBM exactly once.
+// Per (row, block) the (max, first index) of the block's 256 logits goes to `part`.
 typedef short v8s_t __attribute__((ext_vector_type(8)));
 typedef float v4f_t __attribute__((ext_vector_type(4)));
+constexpr int kLmStages = 4;
+constexpr int kLmStageBytes = 8 * 1024 + 4 * 4096;
 __global__ __launch_bounds__(256) void k_lm_head_mfma(const uint16_t* __restrict__ E, const uint16_t* __restrict__ hn,
                                                       int H, int V, int B, uint16_t* __restrict__ logits,
                                                       uint2* __restrict__ part, int nblk) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLmStages * kLmStageBytes];
+    __shared__ float s_val[4][128];
+    __shared__ int s_idx[4][128];
+    constexpr int P = kLmStages;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
-    const int vcol = blockIdx.x * 16 + l16;
-    const int m_base = blockIdx.y * 128 + wave * 32;
-    const uint16_t* ep = E + (int64_t)min(vcol, V - 1) * H + 8 * q;
-    const uint16_t* hp[2];
+    const int m0 = blockIdx.y * 128, n0 = blockIdx.x * 256 + wave * 64;
+    const int steps = H / 32;
+    const uint16_t* asrc[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) hp[i] = hn + (int64_t)min(m_base + 16 * i + l16, B - 1) * H + 8 * q;
-    v4f_t acc[2] = {v4f_t{0.f, 0.f, 0.f, 0.f}, v4f_t{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll 4
-    for (int k0 = 0; k0 < H; k0 += 32) {
-        const v8s_t bf = __builtin_bit_cast(v8s_t, ldg_nt(reinterpret_cast<const uint8_t*>(ep + k0)));
+    for (int u = 0; u < 2; ++u) asrc[u] = hn + (int64_t)min(m0 + 16 * (2 * wave + u) + l16, B - 1) * H + 8 * q;
+    const uint16_t* bsrc[4];
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const v8s_t*>(hp[i] + k0), bf, acc[i], 0, 0,
-                                                            0);
+    for (int j = 0; j < 4; ++j) bsrc[j] = E + (int64_t)min(n0 + 16 * j + l16, V - 1) * H + 8 * q;
+    auto issue = [&](int c) {
+        uint8_t* st = lds + (c % P) * kLmStageBytes;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) glds16(asrc[u] + 32 * c, st + (2 * wave + u) * 1024);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) glds16(bsrc[j] + 32 * c, st + 8192 + wave * 4096 + j * 1024);
+    };
+    v4f_t acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = v4f_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < P - 1; ++c)
+        if (c < steps) issue(c);
+    for (int c = 0; c < steps; ++c) {
+        if (c + P - 2 < steps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * (P - 2)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (c + P - 1 < steps) issue(c + P - 1);
+        const uint8_t* st = lds + (c % P) * kLmStageBytes;
+        v8s_t bf[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const v8s_t*>(st + 8192 + wave * 4096 + j * 1024 + lane * 16);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const v8s_t af = *reinterpret_cast<const v8s_t*>(st + i * 1024 + lane * 16);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[j], acc[i][j], 0, 0, 0);
+        }
     }
+    // epilogue: bf16 logits; per row the (max, first index) over this wave's 64 columns
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int m = m_base + 16 * i + 4 * q + r;
-            const uint16_t lb = f2bf(acc[i][r]);
-            float bv = (vcol < V) ? bf2f(lb) : -INFINITY;
-            int bi = vcol;
-            if (m < B && vcol < V) logits[(int64_t)m * V + vcol] = lb;
-            // (max, first index) over the 16 columns of this row: lanes l16 of the same quarter
+            const int row = 16 * i + 4 * q + r, m = m0 + row;
+            float bv = -INFINITY;
+            int bi = 0x7fffffff;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int n = n0 + 16 * j + l16;
+                const uint16_t lb = f2bf(acc[i][j][r]);
+                if (m < B && n < V) logits[(int64_t)m * V + n] = lb;
+                const float v = n < V ? bf2f(lb) : -INFINITY;
+                if (v > bv) { bv = v; bi = n; }  // columns ascend with j: first index kept on ties
+            }
 #pragma unroll
             for (int o = 8; o > 0; o >>= 1) {
                 const float ov = __shfl_xor(bv, o, 64);
                 const int oi = __shfl_xor(bi, o, 64);
                 if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
             }
-            if (l16 == 0 && m < B)
-                part[(int64_t)m * nblk + blockIdx.x] = make_uint2(__float_as_uint(bv), (uint32_t)bi);
+            if (l16 == 0) {
+                s_val[wave][row] = bv;
+                s_idx[wave][row] = bi;
+            }
         }
+    __syncthreads();
+    if (threadIdx.x < 128 && m0 + (int)threadIdx.x < B) {
+        const int row = threadIdx.x;
+        float bv = s_val[0][row];
+        int bi = s_idx[0][row];
+        for (int w = 1; w < 4; ++w)
+            if (s_val[w][row] > bv || (s_val[w][row] == bv && s_idx[w][row] < bi)) { bv = s_val[w][row]; bi = s_idx[w][row]; }
+        part[(int64_t)(m0 + row) * nblk + blockIdx.x] = make_uint2(__float_as_uint(bv), (uint32_t)bi);
+    }
 }
 
 // Greedy token per row from the LM-head partials; advances the position.
@@ -678,6 +820,8 @@ struct wf_model {
     uint16_t *k_cache = nullptr, *v_cache = nullptr;  // caller-owned (desc)
     int32_t* seq_lens = nullptr;
     uint16_t *h_a = nullptr, *h_b = nullptr, *qbuf = nullptr, *act = nullptr, *hn = nullptr;
+    int* dec_ws = nullptr;      // batched decode split-K partials
+    size_t dec_ws_ints = 0;
     float2* part_ml = nullptr;  // attention partials [B, Hq, kAttnPartSplits] (m, l)
     float* part_o = nullptr;    // [B, Hq, kAttnPartSplits, head_dim] unnormalised o
     int8_t* q8 = nullptr;   // batch > 1: activation codes of the next GEMV [B, q8_stride]
@@ -728,10 +872,28 @@ int launch_gemv(const GemvArgs& ga, hipStream_t st) {
     return check_launch("gemv");
 }
 
+// split-K factor of the batched decode GEMM: ~384 blocks of 128 x 128 over the layer's columns
+int dec_split(int N, int K, int* steps_per_split) {
+    const int cb = (N + 127) / 128, steps = K / 64;
+    const int want = std::max(1, std::min(steps, (384 + cb - 1) / cb));
+    const int sps = (steps + want - 1) / want;
+    if (steps_per_split) *steps_per_split = sps;
+    return (steps + sps - 1) / sps;
+}
+
 template <int MODE, int LPR>
 int launch_gemv_fmt(int fmt, const GemvArgs& ga, hipStream_t st) {
-    if (fmt == WF_FMT_I2S && ga.B >= kDecMfmaMinB) {  // batched decode on the matrix cores
-        hipLaunchKernelGGL((k_dec_mfma<MODE>), dim3((ga.N + 15) / 16, (ga.B + 127) / 128), dim3(256), 0, st, ga);
+    if (fmt == WF_FMT_I2S && ga.B >= kDecMfmaMinB) {  // batched decode on the matrix cores, split-K
+        const int cb = (ga.N + 127) / 128, steps = ga.K / 64;
+        int sps = 0;
+        const int nsplit = dec_split(ga.N, ga.K, &sps);
+        if ((size_t)nsplit * ga.B * ga.N > ga.ws_ints) {
+            set_error("dec_mfma: split-K workspace too small");
+            return WF_EINVAL;
+        }
+        hipLaunchKernelGGL(k_dec_mfma_part, dim3(cb, nsplit, (ga.B + 127) / 128), dim3(256), 0, st, ga, ga.ws, sps);
+        hipLaunchKernelGGL((k_dec_epi<MODE>), dim3((ga.N + 63) / 64, (ga.B + 15) / 16), dim3(256), 0, st, ga,
+                           (const int*)ga.ws, nsplit);
         return check_launch("dec_mfma");
     }
     if (fmt == WF_FMT_TQ) return launch_gemv<FmtTQ, MODE, LPR>(ga, st);
@@ -769,6 +931,8 @@ GemvArgs base_args(const wf_model* m, int l) {
     a.Hkv = d.n_kv_heads;
     a.S = d.max_seq;
     a.positions = m->positions;
+    a.ws = m->dec_ws;
+    a.ws_ints = m->dec_ws_ints;
     a.rope_cos = d.rope_cos;
     a.rope_sin = d.rope_sin;
     const int64_t kvl = (int64_t)d.batch * d.n_kv_heads * d.max_seq * d.head_dim;
@@ -842,10 +1006,11 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             launch_rownorm(m, m->h_a, H, d.final_norm, H, m->hn, st);
             if ((rc = check_launch("final_norm"))) return rc;
             if (d.wfmt == WF_FMT_I2S && B >= kDecMfmaMinB) {
-                hipLaunchKernelGGL(k_lm_head_mfma, dim3(m->lm_blocks, (B + 127) / 128), dim3(256), 0, st, d.embed, m->hn, H,
-                                   d.vocab, B, m->logits, m->am_part, m->lm_blocks);
-                hipLaunchKernelGGL(k_argmax_rows, dim3(B), dim3(256), 0, st, m->am_part, m->lm_blocks, m->tokens,
-                                   m->positions, S);
+                WF_REQUIRE(H % 32 == 0, "lm_head: hidden %% 32 != 0");
+                const int nb = (d.vocab + 255) / 256;
+                hipLaunchKernelGGL(k_lm_head_mfma, dim3(nb, (B + 127) / 128), dim3(256), 0, st, d.embed, m->hn, H, d.vocab, B,
+                                   m->logits, m->am_part, nb);
+                hipLaunchKernelGGL(k_argmax_rows, dim3(B), dim3(256), 0, st, m->am_part, nb, m->tokens, m->positions, S);
                 break;
             }
             const size_t sh = (size_t)H * 2;
@@ -921,6 +1086,12 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_ALLOC(m->h_a, 2 * (size_t)B * d.hidden);
     WF_ALLOC(m->h_b, 2 * (size_t)B * d.hidden);
     WF_ALLOC(m->qbuf, 2 * (size_t)B * d.hidden);
+    if (B >= kDecMfmaMinB && d.wfmt == WF_FMT_I2S) {
+        const int shapes[4][2] = {{m->qkv_rows, d.hidden}, {d.hidden, d.hidden}, {2 * d.inter, d.hidden}, {d.hidden, d.inter}};
+        for (auto& sh : shapes)
+            m->dec_ws_ints = std::max(m->dec_ws_ints, (size_t)dec_split(sh[0], sh[1], nullptr) * B * sh[0]);
+        WF_ALLOC(m->dec_ws, sizeof(int) * m->dec_ws_ints);
+    }
     WF_ALLOC(m->part_ml, sizeof(float2) * (size_t)B * d.n_heads * kAttnPartSplits);
     WF_ALLOC(m->part_o, sizeof(float) * (size_t)B * d.n_heads * kAttnPartSplits * d.head_dim);
     WF_ALLOC(m->hn, 2 * (size_t)B * d.hidden);
@@ -943,7 +1114,7 @@ int wf_model_destroy(wf_model* m) {
     if (m->exec) (void)hipGraphExecDestroy(m->exec);
     if (m->graph) (void)hipGraphDestroy(m->graph);
     if (m->cap) (void)hipStreamDestroy(m->cap);
-    void* ptrs[] = {m->seq_lens, m->h_a, m->h_b, m->qbuf, m->part_ml, m->part_o, m->hn, m->act, m->q8,
+    void* ptrs[] = {m->seq_lens, m->h_a, m->h_b, m->qbuf, m->part_ml, m->part_o, m->hn, m->act, m->q8, m->dec_ws,
                     m->act_sf, m->act_sum, m->tickets, m->am_part};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -961,6 +1132,47 @@ int wf_model_launch_op(wf_model* m, int layer, int op, void* stream) {
     WF_REQUIRE(m, "model_launch_op: null model");
     WF_REQUIRE(layer >= 0 && layer < m->d.layers, "model_launch_op: layer %d out of range", layer);
     return run_op(m, layer, op, as_stream(stream));
+}
+
+int64_t wf_bitnet_linear_ws_bytes(int M, int K) {
+    if (M <= 0 || K <= 0) return 0;
+    return (int64_t)M * ((K + 15) / 16 * 16) + 8 * (int64_t)M + 256;
+}
+
+// BitNetLinear.forward (scripts/direct_inference_full.py:186-208): per-row int8 quantization of x,
+// ternary GEMM, the reference's correction, bf16 out. One launch for M < 16 (quantize in the GEMV
+// prologue), else a quantize launch + the int8-MFMA GEMM (I2_S).
+int wf_bitnet_linear(int fmt, const uint8_t* w, const uint16_t* x, int64_t ldx, float ws, int M, int N, int K,
+                     uint16_t* y, int64_t ldy, void* workspace, void* stream) {
+    WF_REQUIRE(w && x && y, "bitnet_linear: null pointer");
+    WF_REQUIRE(M > 0 && N > 0 && K > 0 && K % 128 == 0, "bitnet_linear: bad shape M=%d N=%d K=%d (K %% 128 == 0)", M, N, K);
+    WF_REQUIRE(fmt == WF_FMT_I2S || fmt == WF_FMT_TQ, "bitnet_linear: unknown weight format %d", fmt);
+    const int kp = fmt == WF_FMT_TQ ? FmtTQ::k_pad(K) : FmtI2S::k_pad(K);
+    WF_REQUIRE(kp <= 8192, "bitnet_linear: K > 8192 not supported");
+    WF_REQUIRE(ldx >= K && ldx % 8 == 0 && ldy >= N && aligned16(x) && aligned16(w), "bitnet_linear: bad strides / alignment");
+    hipStream_t st = as_stream(stream);
+    GemvArgs a{};
+    a.w = w; a.N = N; a.K = K; a.B = M; a.ws0 = ws; a.out = y; a.out_stride = ldy;
+    a.x = x; a.x_stride = ldx;
+    if (M < kDecMfmaMinB || fmt != WF_FMT_I2S) {
+        constexpr int LPR = 32, RPB = kNT / LPR;
+        const dim3 grid((N + RPB - 1) / RPB, M);
+#define WF_LIN(F, PPTV) hipLaunchKernelGGL((k_gemv<F, MODE_LINEAR, LPR, 1, PPTV>), grid, dim3(kNT), (size_t)lds_image_bytes<F>(K), st, a)
+        if (fmt == WF_FMT_TQ) { if (norm_ppt(kp) == 1) WF_LIN(FmtTQ, 1); else WF_LIN(FmtTQ, 2); }
+        else { if (norm_ppt(kp) == 1) WF_LIN(FmtI2S, 1); else WF_LIN(FmtI2S, 2); }
+#undef WF_LIN
+        return check_launch("bitnet_linear");
+    }
+    WF_REQUIRE(workspace && ((uintptr_t)workspace & 15) == 0, "bitnet_linear: workspace of wf_bitnet_linear_ws_bytes() bytes required for M >= 16");
+    const int64_t q8s = (K + 15) / 16 * 16;
+    int8_t* q8 = reinterpret_cast<int8_t*>(workspace);
+    float* sf = reinterpret_cast<float*>(q8 + (int64_t)M * q8s);
+    int* asum = reinterpret_cast<int*>(sf + M);
+    if (norm_ppt(K) == 1) hipLaunchKernelGGL(k_quant_rows_lin<1>, dim3(M), dim3(kNT), 0, st, x, ldx, K, q8, q8s, sf, asum);
+    else hipLaunchKernelGGL(k_quant_rows_lin<2>, dim3(M), dim3(kNT), 0, st, x, ldx, K, q8, q8s, sf, asum);
+    a.q8 = q8; a.q8_stride = q8s; a.act_sf = sf; a.act_sum = asum;
+    hipLaunchKernelGGL(k_linear_mfma, dim3((N + 127) / 128, (M + 127) / 128), dim3(256), 0, st, a);
+    return check_launch("bitnet_linear");
 }
 
 int wf_model_graph_launch(wf_model* m, void* stream) {

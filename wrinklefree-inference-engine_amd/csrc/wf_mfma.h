@@ -1,0 +1,106 @@
+// wf_mfma.h -- LDS-DMA pipelined ternary x int8 GEMM on the gfx950 matrix cores (prefill and
+// batched decode). Included by wf_mfma.hip (raw sgl-kernel epilogue) and wf_decode.hip (fused
+// decode-step epilogues).
+//
+// Fragments (v_mfma_i32_16x16x64_i8; see wf_mfma.hip's header): in k-step c (64 weights) lane
+// (l16 = lane & 15, q = lane >> 4) multiplies A[row l16][k = koff + 32q + 0..15] with
+// enc(W[col l16][same k]); the I2_S bytes [boff, boff + 16) of a weight row hold all 64 weights of
+// the step (quarter q at bit offset 6 - 2q), koff = 128(c>>1) + 16(c&1), boff = 32(c>>1) + 16(c&1).
+//
+// Block = 4 waves = WR x WC, tile 128 rows x (64 WC) columns; wave (wr, wc) owns row tiles
+// [wr * 8/WR, +8/WR) and column tiles [4 wc, +4). Every k-step is one pipeline stage in LDS:
+//   A: 8 KiB = 8 wave-loads (`global_load_lds_dwordx4`: a wave writes 1 KiB in lane order), wave w
+//      loads row tiles 2w, 2w+1; slot (t, lane) <- A[16t + (lane & 15)][koff + 32 (lane >> 4)], so
+//      the MFMA fragment of row tile t is the contiguous KiB t (conflict-free ds_read_b128).
+//   B: 1 KiB per wave (its 64 columns' 16-byte weight groups; waves sharing wc load the same bytes
+//      into their own slot), fragment of column tile j = slot 16j + l16 (4-lane broadcast).
+// Every wave issues exactly 3 LDS-DMA loads per stage, so one counted `s_waitcnt vmcnt(3 (P-2))`
+// retires its share of stage s with P-2 stages still in flight; a raw s_barrier then publishes the
+// stage to all waves (no __syncthreads: it would drain the pipeline with vmcnt(0)). The stage the
+// loop refills is the one every wave finished computing before that barrier.
+#pragma once
+#include "wf_device.h"
+
+namespace wf {
+
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+
+constexpr int kTgStageBytes = 8 * 1024 + 4 * 1024;  // A 8 KiB + 4 waves x 1 KiB of B
+// LDS ring depth P: 4 (48 KiB, 3 blocks per CU) when the grid fills the chip (prefill); 12 (144 KiB,
+// one block per CU, 11 stages = 132 KiB in flight) for the batched-decode grids of 20-200 blocks,
+// whose time is the HBM/L2 latency of a shallow pipeline otherwise.
+constexpr int kTgStagesWide = 4;
+constexpr int kTgStagesDeep = 12;
+
+__device__ __forceinline__ void glds16(const void* g, void* lds) {
+    __builtin_amdgcn_global_load_lds(const_cast<void*>(g), reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                                               reinterpret_cast<uintptr_t>(lds)),
+                                     16, 0, 0);
+}
+
+// Epi::apply(i_tile_row0, j_tile_col0, acc, l16, q): called once per 16x16 output tile with its
+// first row / column; lane holds D[row0 + 4q + r][col0 + l16], r < 4. k-steps [c_begin, c_end)
+// (a split-K slice; the whole K is [0, K/64)).
+template <int WR, int P, class Epi>
+__device__ __forceinline__ void tgemm_tile(const uint8_t* __restrict__ W, const int8_t* __restrict__ A, int64_t lda,
+                                           int M, int N, int K, int m0, int n0, uint8_t* lds, Epi& epi,
+                                           int c_begin = 0, int c_end = -1) {
+    constexpr int WC = 4 / WR;
+    constexpr int TM = 8 / WR;  // row tiles per wave
+    constexpr int TN = 4;       // column tiles per wave
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+    const int wr = wave / WC, wc = wave % WC;
+    if (c_end < 0) c_end = K / 64;
+    const int steps = c_end - c_begin;
+    // per-lane DMA sources: A rows of tiles 2w, 2w+1; B column of this wave's 64
+    const int8_t* asrc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) asrc[u] = A + (int64_t)min(m0 + 16 * (2 * wave + u) + l16, M - 1) * lda + 32 * q;
+    const uint8_t* bsrc = W + (int64_t)min(n0 + 64 * wc + lane, N - 1) * (K / 4);
+
+    auto issue = [&](int cl) {  // cl: step within the slice
+        uint8_t* st = lds + (cl % P) * kTgStageBytes;
+        const int c = c_begin + cl;
+        const int koff = 128 * (c >> 1) + 16 * (c & 1), boff = 32 * (c >> 1) + 16 * (c & 1);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) glds16(asrc[u] + koff, st + (2 * wave + u) * 1024);
+        glds16(bsrc + boff, st + 8192 + wave * 1024);
+    };
+
+    v4i_t acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = v4i_t{0, 0, 0, 0};
+
+#pragma unroll
+    for (int c = 0; c < P - 1; ++c)
+        if (c < steps) issue(c);
+    const int sh = 6 - 2 * q;
+    for (int c = 0; c < steps; ++c) {
+        if (c + P - 2 < steps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (P - 2)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (c + P - 1 < steps) issue(c + P - 1);
+        const uint8_t* st = lds + (c % P) * kTgStageBytes;
+        v4i_t af[TM], bf[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const v4i_t*>(st + (wr * TM + i) * 1024 + lane * 16);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const uint4 w = *reinterpret_cast<const uint4*>(st + 8192 + wave * 1024 + (16 * j + l16) * 16);
+            bf[j] = v4i_t{(int)((w.x >> sh) & 0x03030303u), (int)((w.y >> sh) & 0x03030303u),
+                          (int)((w.z >> sh) & 0x03030303u), (int)((w.w >> sh) & 0x03030303u)};
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) epi.apply(m0 + 16 * (wr * TM + i), n0 + 64 * wc + 16 * j, acc[i][j], l16, q);
+}
+
+}  // namespace wf

@@ -17,82 +17,46 @@
 
 #include "wf_common.h"
 #include "wf_device.h"
+#include "wf_mfma.h"
 
 namespace wf {
 
-typedef int v4i __attribute__((ext_vector_type(4)));
 
-// Block = 4 waves arranged WR x WC; each wave owns TMW x TNW 16x16 tiles:
-// block tile = (WR * TMW * 16) rows x (WC * TNW * 16) columns.
-template <int WR, int WC, int TMW, int TNW>
-__global__ __launch_bounds__(256) void k_tgemm_mfma(const uint8_t* __restrict__ W, const int8_t* __restrict__ A,
-                                                    int64_t lda, float scale, int M, int N, int K,
-                                                    float* __restrict__ Y, int64_t ldy) {
-    static_assert(WR * WC == 4, "4 waves per block");
-    constexpr int BM = WR * TMW * 16, BN = WC * TNW * 16;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int l16 = lane & 15, q = lane >> 4;
-    const int wr = wave / WC, wc = wave % WC;
-    const int m_base = blockIdx.y * BM + wr * TMW * 16;
-    const int n_base = blockIdx.x * BN + wc * TNW * 16;
-    const int64_t wrow = K / 4;
-
-    const uint8_t* wp[TNW];
+// Raw sgl-kernel epilogue: Y[m, n] = float(sum) * scale.
+struct EpiRaw {
+    float* Y;
+    int64_t ldy;
+    float scale;
+    int M, N;
+    __device__ __forceinline__ void apply(int r0, int c0, const v4i_t& acc, int l16, int q) {
+        const int n = c0 + l16;
+        if (n >= N) return;
 #pragma unroll
-    for (int j = 0; j < TNW; ++j) wp[j] = W + (int64_t)min(n_base + 16 * j + l16, N - 1) * wrow;
-    const int8_t* ap[TMW];
-#pragma unroll
-    for (int i = 0; i < TMW; ++i) ap[i] = A + (int64_t)min(m_base + 16 * i + l16, M - 1) * lda + 32 * q;
-    const int sh = 6 - 2 * q;
-
-    v4i acc[TMW][TNW];
-#pragma unroll
-    for (int i = 0; i < TMW; ++i)
-#pragma unroll
-        for (int j = 0; j < TNW; ++j) acc[i][j] = v4i{0, 0, 0, 0};
-
-    const int steps = K / 64;  // K % 128 == 0
-#pragma unroll 2
-    for (int c = 0; c < steps; ++c) {
-        const int boff = 32 * (c >> 1) + 16 * (c & 1);   // byte offset of the 64-weight group
-        const int koff = 128 * (c >> 1) + 16 * (c & 1);  // its first activation
-        v4i bf[TNW];
-#pragma unroll
-        for (int j = 0; j < TNW; ++j) {
-            const uint4 w = ldg_nt(wp[j] + boff);
-            bf[j] = v4i{(int)((w.x >> sh) & 0x03030303u), (int)((w.y >> sh) & 0x03030303u),
-                        (int)((w.z >> sh) & 0x03030303u), (int)((w.w >> sh) & 0x03030303u)};
+        for (int r = 0; r < 4; ++r) {
+            const int m = r0 + 4 * q + r;
+            if (m < M) Y[(int64_t)m * ldy + n] = (float)acc[r] * scale;
         }
-        v4i af[TMW];
-#pragma unroll
-        for (int i = 0; i < TMW; ++i) af[i] = *reinterpret_cast<const v4i*>(ap[i] + koff);
-#pragma unroll
-        for (int i = 0; i < TMW; ++i)
-#pragma unroll
-            for (int j = 0; j < TNW; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int i = 0; i < TMW; ++i)
-#pragma unroll
-        for (int j = 0; j < TNW; ++j) {
-            const int n = n_base + 16 * j + l16;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = m_base + 16 * i + 4 * q + r;
-                if (m < M && n < N) Y[(int64_t)m * ldy + n] = (float)acc[i][j][r] * scale;
-            }
-        }
+};
+
+template <int WR, int P>
+__global__ __launch_bounds__(256) void k_tgemm_lds(const uint8_t* __restrict__ W, const int8_t* __restrict__ A,
+                                                   int64_t lda, float scale, int M, int N, int K, float* __restrict__ Y,
+                                                   int64_t ldy) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[P * kTgStageBytes];
+    EpiRaw e{Y, ldy, scale, M, N};
+    tgemm_tile<WR, P>(W, A, lda, M, N, K, blockIdx.y * 128, blockIdx.x * 64 * (4 / WR), lds, e);
 }
 
 // M >= 16, I2_S, K % 128 == 0, 16-byte aligned rows (checked by the caller).
 int launch_tgemm_mfma(const uint8_t* w, const int8_t* a, int64_t lda, float scale, int M, int N, int K, float* y,
                       int64_t ldy, hipStream_t st) {
-    if (M >= 512) {  // prefill-sized: 128 x 128 block tiles, 2 x 2 waves of 4 x 4 MFMA tiles
-        const dim3 grid((N + 127) / 128, (M + 127) / 128);
-        hipLaunchKernelGGL((k_tgemm_mfma<2, 2, 4, 4>), grid, dim3(256), 0, st, w, a, lda, scale, M, N, K, y, ldy);
-    } else {  // batched decode: 128 x 16 block tiles -> N / 16 blocks
-        const dim3 grid((N + 15) / 16, (M + 127) / 128);
-        hipLaunchKernelGGL((k_tgemm_mfma<4, 1, 2, 1>), grid, dim3(256), 0, st, w, a, lda, scale, M, N, K, y, ldy);
+    if (M >= 512) {  // prefill-sized: 128 x 128 tiles (2 x 2 waves of 4 x 4 MFMA tiles)
+        hipLaunchKernelGGL((k_tgemm_lds<2, kTgStagesWide>), dim3((N + 127) / 128, (M + 127) / 128), dim3(256), 0, st, w,
+                           a, lda, scale, M, N, K, y, ldy);
+    } else {  // batched decode: 128 x 64 tiles (4 x 1 waves of 2 x 4 MFMA tiles), twice the blocks
+        hipLaunchKernelGGL((k_tgemm_lds<4, kTgStagesDeep>), dim3((N + 63) / 64, (M + 127) / 128), dim3(256), 0, st, w, a,
+                           lda, scale, M, N, K, y, ldy);
     }
     return check_launch("tgemm_mfma");
 }

@@ -149,17 +149,23 @@ struct NormRow {
             w[i] = *reinterpret_cast<const uint4*>(nw + 8 * p);
         }
     }
+    // the row only (no norm: BitNetLinear)
+    __device__ __forceinline__ void issue_x(const uint16_t* __restrict__ xrow, int K) {
+        const int npk = K >> 3;
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) x[i] = *reinterpret_cast<const uint4*>(xrow + 8 * min((int)threadIdx.x + NT * i, npk - 1));
+    }
     // norm weight only (the row itself is computed in registers, e.g. AttnRow)
     __device__ __forceinline__ void issue_w(const uint16_t* __restrict__ nw, int K) {
         const int npk = K >> 3;
 #pragma unroll
         for (int i = 0; i < PPT; ++i) w[i] = *reinterpret_cast<const uint4*>(nw + 8 * min((int)threadIdx.x + NT * i, npk - 1));
     }
-    __device__ __forceinline__ void fence(bool with_x = true) {
+    __device__ __forceinline__ void fence(bool with_x = true, bool with_w = true) {
 #pragma unroll
         for (int i = 0; i < PPT; ++i) {
             if (with_x) reg_fence(x[i]);
-            reg_fence(w[i]);
+            if (with_w) reg_fence(w[i]);
         }
     }
 };
@@ -228,6 +234,26 @@ __device__ __forceinline__ float norm_core(const NormRow<PPT, NT>& r, int K, flo
     for (int i = 1; i < NW; ++i) mx = fmaxf(mx, red[NW + i]);
     return (float)act_scale_from_max(mx);
 }
+// Activation scale of a row without normalisation (BitNetLinear's own quantizer,
+// scripts/direct_inference_full.py:196): s = double(max|x|)/127. `red` as norm_core.
+template <int PPT, int NT>
+__device__ __forceinline__ float absmax_scale(const float (&y)[PPT][8], float* red) {
+    constexpr int NW = NT / 64;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float mx = 0.f;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(y[i][j]));
+    mx = wave_max(mx);
+    if (lane == 0) red[NW + wave] = mx;
+    __syncthreads();
+    mx = red[NW];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) mx = fmaxf(mx, red[NW + i]);
+    return (float)act_scale_from_max(mx);
+}
+
 // unpack_row + norm_core
 template <int PPT, int NT>
 __device__ __forceinline__ float norm_row(const NormRow<PPT, NT>& r, int K, float eps, float (&y)[PPT][8], float* red,

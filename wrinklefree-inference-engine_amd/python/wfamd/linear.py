@@ -1,0 +1,52 @@
+"""BitNetLinear on the fused HIP path.
+
+The reference's decode runs this layer seven times per block (scripts/direct_inference_full.py:
+186-208): per-row int8 activation quantization, ternary matmul on the packed weights, then the
+encoding correction y = (raw - ws * sum(q)) * s, cast to bf16. `BitNetLinear.forward` is one C-ABI
+call (wf_bitnet_linear): a single launch for fewer than 16 rows, else a quantize launch plus the
+int8-MFMA GEMM.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from ._lib import WF_FMT_I2S, WF_FMT_TQ
+
+
+class BitNetLinear(nn.Module):
+    """bf16 [..., in_features] -> bf16 [..., out_features] with packed ternary weights.
+
+    `packed` is the blocked I2_S layout [out, in/4] (cache/bitnet_converter.py:26-77) or, with
+    fmt=WF_FMT_TQ, the ~1.6-bit layout; `weight_scale` is the layer's float scale.
+    """
+
+    def __init__(self, in_features: int, out_features: int, packed: torch.Tensor, weight_scale: float,
+                 fmt: int = WF_FMT_I2S):
+        super().__init__()
+        if fmt not in (WF_FMT_I2S, WF_FMT_TQ):
+            raise ValueError(f"unknown weight format {fmt}")
+        if packed.shape[0] != out_features:
+            raise ValueError(f"packed weights have {packed.shape[0]} rows, expected {out_features}")
+        self.in_features = in_features
+        self.out_features = out_features
+        self.fmt = fmt
+        self.weight_scale = float(weight_scale)
+        self.register_buffer("packed_weight", packed)
+
+    @classmethod
+    def from_ternary(cls, weight: torch.Tensor, weight_scale: float, fmt: int = WF_FMT_I2S) -> "BitNetLinear":
+        """Pack a {-1, 0, +1} weight [out, in] on the device."""
+        w = weight.to("cuda") if not weight.is_cuda else weight
+        packed = ops.pack_i2s(w)
+        if fmt == WF_FMT_TQ:
+            packed = ops.i2s_to_tq(packed)
+        return cls(weight.shape[1], weight.shape[0], packed, weight_scale, fmt)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return ops.bitnet_linear(x, self.packed_weight, self.weight_scale, self.fmt, self.in_features)
+
+    def extra_repr(self) -> str:
+        fmt = "i2s" if self.fmt == WF_FMT_I2S else "tq"
+        return f"in_features={self.in_features}, out_features={self.out_features}, fmt={fmt}"

@@ -117,6 +117,33 @@ def bitnet_gemm_lsb(packed: torch.Tensor, activations: torch.Tensor, scale: floa
     return out.cpu() if host else out
 
 
+def bitnet_linear(x: torch.Tensor, packed: torch.Tensor, weight_scale: float, fmt: int = WF_FMT_I2S,
+                  in_features: Optional[int] = None) -> torch.Tensor:
+    """Fused BitNetLinear.forward (scripts/direct_inference_full.py:186-208): bf16 x [..., K] ->
+    bf16 [..., N]; per-row int8 quantization, ternary GEMM and the reference's correction in one
+    (M < 16) or two (M >= 16, int8 MFMA) launches."""
+    if x.dtype != torch.bfloat16:
+        raise ValueError(f"bitnet_linear expects bf16 activations, got {x.dtype}")
+    k = x.shape[-1] if in_features is None else in_features
+    _check_packed(packed, k, fmt)
+    if x.shape[-1] != k:
+        raise ValueError(f"activations have {x.shape[-1]} features, weights expect {k}")
+    host = not (packed.is_cuda and x.is_cuda)
+    w = _on_device(packed)
+    x2 = _on_device(x.reshape(-1, k))
+    if x2.stride(1) != 1 or x2.stride(0) % 8 != 0 or x2.data_ptr() % 16 != 0:
+        x2 = x2.contiguous()
+    m, n = x2.shape[0], w.shape[0]
+    y = torch.empty((m, n), dtype=torch.bfloat16, device=w.device)
+    if m > 0 and n > 0:
+        nws = int(_lib.load().wf_bitnet_linear_ws_bytes(m, k))
+        ws = torch.empty(nws, dtype=torch.uint8, device=w.device) if m >= 16 else None
+        call("wf_bitnet_linear", fmt, w.data_ptr(), x2.data_ptr(), x2.stride(0), float(weight_scale), m, n, k,
+             y.data_ptr(), n, _ptr(ws), _stream())
+    out = y.reshape(*x.shape[:-1], n)
+    return out.cpu() if host else out
+
+
 # ---------------------------------------------------------------------------------------------
 # a3: activation quantizers
 # ---------------------------------------------------------------------------------------------
