@@ -137,7 +137,8 @@ typedef struct {
     int32_t* positions;           /* [batch]: position of the input token; the step increments it  */
     uint16_t* logits;             /* [batch, vocab] bf16                                           */
     uint16_t* k_cache;            /* [layers, batch, n_kv_heads, max_seq, head_dim] bf16           */
-    uint16_t* v_cache;
+    uint16_t* v_cache;            /* same shape; for batch >= 16 with I2_S weights and max_seq % 32 == 0 it is
+                                     stored transposed per (layer, sequence, kv head): [head_dim, max_seq] */
     int debug_flags;              /* reserved, must be 0 (latency studies use the stamp build,
                                      tools/stamps.py)                                             */
 } wf_model_desc;

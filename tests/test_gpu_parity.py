@@ -465,3 +465,39 @@ def test_bitnet_linear_module_and_errors():
         ops.bitnet_linear(x.float(), lin.packed_weight, 0.75)
     with pytest.raises(ValueError):
         ops.bitnet_linear(x[..., :384], lin.packed_weight, 0.75)
+
+
+def test_decode_batched_long_ragged_context_matches_single():
+    """Batched (matrix-core attention on the transposed V cache) vs batch-1 (VALU attention on the
+    row-major cache) over ragged contexts of 0..1900 cached keys: same logical K/V, per-row logits
+    within 1e-4 rel-L2 (attention sums in a different fp32 order; P enters as bf16 hi + lo)."""
+    from wfamd.model import BitNetConfig, BitNetDecoder, synthetic_weights
+    cfg = BitNetConfig(hidden=512, layers=2, n_heads=4, n_kv_heads=1, head_dim=128, inter=768, vocab=1024,
+                       max_seq=2048)
+    w = synthetic_weights(cfg, seed=3)
+    B = 20
+    decb = BitNetDecoder(cfg, w, batch=B)
+    assert decb.v_transposed
+    gen = torch.Generator(device="cuda").manual_seed(11)
+    ctx = 1900
+    kv = [(torch.randn(B, 1, ctx, 128, generator=gen, device="cuda").to(torch.bfloat16),
+           torch.randn(B, 1, ctx, 128, generator=gen, device="cuda").to(torch.bfloat16)) for _ in range(2)]
+    for l in range(2):
+        decb.load_kv(l, *kv[l])
+    pos = [0, 1, 5, 31, 32, 33, 127, 128, 129, 255, 256, 300, 511, 777, 1000, 1023, 1024, 1500, 1899, 1700]
+    toks = [(37 * b + 5) % cfg.vocab for b in range(B)]
+    decb.set_state(toks, pos)
+    decb.step(graph=True)
+    torch.cuda.synchronize()
+    for b in (0, 1, 3, 4, 7, 8, 10, 13, 15, 16, 18):
+        d1 = BitNetDecoder(cfg, w, batch=1)
+        assert not d1.v_transposed
+        for l in range(2):
+            d1.load_kv(l, kv[l][0][b:b + 1], kv[l][1][b:b + 1])
+        d1.set_state([toks[b]], [pos[b]])
+        d1.step(graph=False)
+        torch.cuda.synchronize()
+        got = decb.logits[b].float().cpu().numpy()
+        exp = d1.logits[0].float().cpu().numpy()
+        assert rel_l2(got, exp) < 1e-4, (b, pos[b], rel_l2(got, exp))
+        del d1

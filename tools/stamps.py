@@ -32,6 +32,7 @@ NAMES = {  # slot names per kernel kind (WF_STAMP(i) in csrc/)
              "-", "-"],
     "attn": ["entry", "kv_done", "out", "-", "-", "-", "-", "-"] + ["-"] * 8,
     "lm": ["entry", "staged", "dot", "ticket", "argmax", "-", "-", "-"] + ["-"] * 8,
+    "dgemm": ["entry", "issued", "first_mma", "loop_done", "reduced", "epi_issued", "epi_drained"] + ["-"] * 9,
 }
 
 
@@ -76,6 +77,7 @@ def main():
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--layer", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--warm", action="store_true",
                     help="launch the same op of layer-1 right before (code and inputs warm, weights cold)")
     args = ap.parse_args()
@@ -84,11 +86,12 @@ def main():
         getattr(lib, fn).restype = C.c_int
         getattr(lib, fn).argtypes = [C.c_void_p, C.c_int, C.c_int]
     w = synthetic_weights(BITNET_2B, seed=0)
-    dec = BitNetDecoder(BITNET_2B, w, batch=1, wfmt=WF_FMT_TQ if args.wfmt == "tq" else WF_FMT_I2S,
+    B = args.batch
+    dec = BitNetDecoder(BITNET_2B, w, batch=B, wfmt=WF_FMT_TQ if args.wfmt == "tq" else WF_FMT_I2S,
                         debug_flags=args.flags)
     del w
     dec.fill_kv_random(args.ctx)
-    dec.set_state([1], [args.ctx])
+    dec.set_state([1] * B, [args.ctx] * B)
     for _ in range(3):
         dec.step(graph=False)
     torch.cuda.synchronize()
@@ -96,6 +99,10 @@ def main():
     ops = [(_lib.WF_OP_QKV, "qkv", "gemv", "decode", 7), (_lib.WF_OP_ATTN, "attn", "attn", "attn", 2),
            (_lib.WF_OP_O, "o_proj", "gemv", "decode", 3), (_lib.WF_OP_GATE_UP, "gate_up", "gemv", "decode", 3),
            (_lib.WF_OP_DOWN, "down", "gemv", "decode", 3), (_lib.WF_OP_LM_HEAD, "lm_head", "lm", "decode", 4)]
+    if B >= 16:  # batched matrix-core path: GEMM stamps (slots 0-6), attention as before
+        ops = [(_lib.WF_OP_QKV, "qkv", "dgemm", "decode", 6), (_lib.WF_OP_ATTN, "attn", "attn", "attn", 2),
+               (_lib.WF_OP_O, "o_proj", "dgemm", "decode", 6), (_lib.WF_OP_GATE_UP, "gate_up", "dgemm", "decode", 6),
+               (_lib.WF_OP_DOWN, "down", "dgemm", "decode", 6)]
     res = {}
     for op, name, kind, tu, tail in ops:
         for rep in range(args.reps):

@@ -455,9 +455,180 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
     WF_STAMP(2);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Batched decode attention partials on the bf16 matrix cores (v_mfma_f32_16x16x32_bf16), for a
+// V cache stored transposed per (sequence, kv head): Vt[d][S] (S % 32 == 0). Same partial records
+// as k_attn_part. Block (split s, kv head g, sequence b) = 4 waves; wave w walks 32-key tiles
+// base = t0 + 32 w + 128 i of its split (T = round_up(ceil(Sb / 8), 32)), online softmax per head.
+//   scores: two 16-key MFMA tiles, A = K rows (tile tau, row 4a + r <- key base + 8a + 4 tau + r),
+//     B = Q^T (column = query head of the group, rows >= grp zero; lane quarter q takes dims
+//     32q + 8c .. +8 of MFMA c = 0..3, the same permutation for both operands). Lane (head h, q)
+//     then holds the scores of keys base + 8q + 0..7 -- exactly the A fragment (P rows = heads,
+//     k = keys) of the P.V MFMA, whose B fragment is Vt[16n + l16][base + 8q, +8): one 16-byte load.
+//   P enters the MFMA as bf16 hi + lo (two MFMAs), so P.V keeps ~16 mantissa bits (the VALU path's
+//     fp32 p within ~1e-5 relative). K rows past the split are clamped + masked to -inf, V columns
+//     past it zeroed (0 * stale = 0).
+// ---------------------------------------------------------------------------------------------
+typedef short v8s_t __attribute__((ext_vector_type(8)));
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+constexpr int kAttnMfmaMaxGrp = 8;
+template <bool DB>
+__global__ __launch_bounds__(256) void k_attn_mfma(const uint16_t* __restrict__ q, int64_t q_sb,
+                                                   const uint16_t* __restrict__ K, const uint16_t* __restrict__ Vt,
+                                                   int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv, int S,
+                                                   const int32_t* __restrict__ seq_lens, float sm_scale,
+                                                   float2* __restrict__ ml_out, float* __restrict__ o_out) {
+    constexpr int D = 128;
+    const int s = blockIdx.x, g = blockIdx.y, b = blockIdx.z;
+    const int grp = Hq / Hkv, hq0 = g * grp;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
+    const int Sb = min(seq_lens[b], S);
+    const int T = ((Sb + kAttnPartSplits - 1) / kAttnPartSplits + 31) / 32 * 32;
+    const int t0 = s * T, t1 = min(t0 + T, Sb);
+    __shared__ float sm_m[4][kAttnMfmaMaxGrp], sm_l[4][kAttnMfmaMaxGrp];
+    __shared__ __attribute__((aligned(16))) float sm_o[4][kAttnMfmaMaxGrp][D];
+    const uint16_t* Kb = K + b * kv_sb + g * kv_sh;
+    const uint16_t* Vb = Vt + b * kv_sb + g * kv_sh;
+    WF_STAMP(0);
+
+    float m_run = -INFINITY, l_run = 0.f;
+    v4f_t acc[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[n] = v4f_t{0.f, 0.f, 0.f, 0.f};
+    int base = t0 + 32 * wave;
+    if (base < t1) {
+        v8s_t qf[4];
+        {
+            const uint16_t* qp = q + b * q_sb + (int64_t)(hq0 + min(l16, grp - 1)) * D + 32 * q4;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                uint4 t = *reinterpret_cast<const uint4*>(qp + 8 * c);
+                if (l16 >= grp) t = make_uint4(0, 0, 0, 0);
+                qf[c] = __builtin_bit_cast(v8s_t, t);
+            }
+        }
+        auto load = [&](uint4 (&kr)[2][4], uint4 (&vr)[8], int bs) {
+#pragma unroll
+            for (int tau = 0; tau < 2; ++tau) {
+                const int key = min(bs + 8 * (l16 >> 2) + 4 * tau + (l16 & 3), t1 - 1);
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    kr[tau][c] = *reinterpret_cast<const uint4*>(Kb + (int64_t)key * D + 32 * q4 + 8 * c);
+            }
+#pragma unroll
+            for (int n = 0; n < 8; ++n)
+                vr[n] = *reinterpret_cast<const uint4*>(Vb + (int64_t)(16 * n + l16) * S + bs + 8 * q4);
+        };
+        auto compute = [&](const uint4 (&kr)[2][4], const uint4 (&vr)[8], int bs) {
+            v4f_t sc[2];
+#pragma unroll
+            for (int tau = 0; tau < 2; ++tau) {
+                sc[tau] = v4f_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    sc[tau] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8s_t, kr[tau][c]), qf[c],
+                                                                      sc[tau], 0, 0, 0);
+            }
+            const int lim = t1 - bs - 8 * q4;  // valid keys among this lane's 8
+            float x[8], mx = -INFINITY;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                x[e] = e < lim ? sc[e >> 2][e & 3] * sm_scale : -INFINITY;
+                mx = fmaxf(mx, x[e]);
+            }
+            mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));  // the tile has >= 1 valid key: finite
+            const float mnew = fmaxf(m_run, mx);
+            const float alpha = __expf(m_run - mnew);  // 0 on the first tile
+            m_run = mnew;
+            float p[8], ps = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                p[e] = __expf(x[e] - mnew);
+                ps += p[e];
+            }
+            l_run = l_run * alpha + ps;  // per-lane partial (summed over the quarters at the end)
+            uint32_t hi[4], lo[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                hi[j] = pk_bf16(p[2 * j], p[2 * j + 1]);
+                lo[j] = pk_bf16(p[2 * j] - bf_lo(hi[j]), p[2 * j + 1] - bf_hi(hi[j]));
+            }
+            const v8s_t ph = __builtin_bit_cast(v8s_t, make_uint4(hi[0], hi[1], hi[2], hi[3]));
+            const v8s_t pl = __builtin_bit_cast(v8s_t, make_uint4(lo[0], lo[1], lo[2], lo[3]));
+            float ar[4];  // rescale factor of output row (head) 4 q4 + r
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ar[r] = __shfl(alpha, 4 * q4 + r, 64);
+            uint32_t vm[4] = {~0u, ~0u, ~0u, ~0u};
+            if (lim < 8) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) vm[j] = (2 * j < lim ? 0xffffu : 0u) | (2 * j + 1 < lim ? 0xffff0000u : 0u);
+            }
+#pragma unroll
+            for (int n = 0; n < 8; ++n) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[n][r] *= ar[r];
+                const uint4 v = make_uint4(vr[n].x & vm[0], vr[n].y & vm[1], vr[n].z & vm[2], vr[n].w & vm[3]);
+                const v8s_t vf = __builtin_bit_cast(v8s_t, v);
+                acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vf, acc[n], 0, 0, 0);
+                acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vf, acc[n], 0, 0, 0);
+            }
+        };
+        uint4 kA[2][4], vA[8];
+        load(kA, vA, base);
+        if constexpr (DB) {
+            uint4 kB[2][4], vB[8];
+            for (; base < t1; base += 256) {
+                const int nb = base + 128;
+                if (nb < t1) load(kB, vB, nb);
+                compute(kA, vA, base);
+                if (nb >= t1) break;
+                if (nb + 128 < t1) load(kA, vA, nb + 128);
+                compute(kB, vB, nb);
+            }
+        } else {
+            for (; base < t1; base += 128) {
+                compute(kA, vA, base);
+                if (base + 128 < t1) load(kA, vA, base + 128);
+            }
+        }
+    }
+    WF_STAMP(1);
+    l_run += __shfl_xor(l_run, 16, 64);
+    l_run += __shfl_xor(l_run, 32, 64);
+    if (q4 == 0 && l16 < grp) {
+        sm_m[wave][l16] = m_run;
+        sm_l[wave][l16] = l_run;
+    }
+#pragma unroll
+    for (int n = 0; n < 8; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (4 * q4 + r < grp) sm_o[wave][4 * q4 + r][16 * n + l16] = acc[n][r];
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < grp * (D / 4); idx += 256) {
+        const int h = idx / (D / 4), d = (idx % (D / 4)) * 4;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) mx = fmaxf(mx, sm_m[w][h]);
+        float ls = 0.f, os[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const float a = (sm_m[w][h] == -INFINITY) ? 0.f : __expf(sm_m[w][h] - mx);
+            ls += sm_l[w][h] * a;
+            const float4 ov = *reinterpret_cast<const float4*>(&sm_o[w][h][d]);
+            os[0] += ov.x * a; os[1] += ov.y * a; os[2] += ov.z * a; os[3] += ov.w * a;
+        }
+        const int64_t rec = (int64_t)(b * Hq + hq0 + h) * kAttnPartSplits + s;
+        *reinterpret_cast<float4*>(o_out + rec * D + d) = make_float4(os[0], os[1], os[2], os[3]);
+        if (d == 0) ml_out[rec] = make_float2(mx, ls);
+    }
+    WF_STAMP(2);
+}
+
 int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
-                              float2* ml, float* o, hipStream_t st) {
+                              float2* ml, float* o, hipStream_t st, bool v_trans) {
     const int grp = Hq / Hkv;
     if (grp > 8) {
         set_error("decode_attention_partials: GQA group %d > 8", grp);
@@ -473,6 +644,15 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
     }
     // batched: one block per kv head, the group's query heads share every K/V load (KV-bound)
     const dim3 grid(kAttnPartSplits, Hkv, B);
+    if (v_trans) {  // transposed V cache: matrix-core kernel
+        if (S % 32 != 0) {
+            set_error("decode_attention_partials: transposed V needs S %% 32 == 0 (S=%d)", S);
+            return WF_EINVAL;
+        }
+        hipLaunchKernelGGL((k_attn_mfma<false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S,
+                               seq_lens, sm_scale, ml, o);
+        return check_launch("decode_attention_partials");
+    }
 #define WF_AP(GV)                                                                                                   \
     hipLaunchKernelGGL((k_attn_part<GV>), grid, dim3(kAttnPartThreads), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, \
                        seq_lens, sm_scale, ml, o)

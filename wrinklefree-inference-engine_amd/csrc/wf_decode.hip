@@ -29,7 +29,7 @@
 namespace wf {
 int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
-                              float2* ml, float* o, hipStream_t st);
+                              float2* ml, float* o, hipStream_t st, bool v_trans);
 
 enum { MODE_QKV = 0, MODE_O = 1, MODE_GU = 2, MODE_DN = 3, MODE_LINEAR = 4 };  // LINEAR: BitNetLinear drop-in
 constexpr int kNT = 512;  // threads per GEMV / row-norm block (8 waves: 2 per SIMD hide the input-stage latency)
@@ -65,6 +65,7 @@ struct GemvArgs {
     uint16_t* kc;
     uint16_t* vc;
     int64_t kv_b_stride;
+    int v_t;  // V cache transposed per (sequence, kv head): [D][S] (batched MFMA decode)
 };
 
 // Reference correction (direct_inference_full.py:201-208) for one output:
@@ -319,13 +320,46 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
 // sit in lanes l and l ^ 8 of the same tile).
 // ---------------------------------------------------------------------------------------------
 constexpr int kDecMfmaMinB = 16;
+constexpr int kDecGemmMaxB = 256;  // whole-K register GEMM up to here, split-K LDS-DMA tiles above
 
 // Fused decode-step epilogue of one 16 x 16 output tile (rows = sequences, columns = 16 weight rows
 // = one QKV RoPE block / one gate-up tile): lane holds rows r0 + 4q + r of column c0 + l16.
+// The per-row inputs of the epilogue (scale, code sum, position + RoPE entries, residual) can be
+// loaded before the GEMM's result exists (load(), issued next to the fragment loads).
+struct EpiIn {
+    float sf[4];
+    int as[4];
+    int pos[4];
+    float cs[4], sn[4];
+    uint16_t res[4];
+};
 template <int MODE>
 struct EpiDec {
     const GemvArgs* a;
+    __device__ __forceinline__ void load(int r0, int c0, int l16, int q, EpiIn& in) const {
+        const GemvArgs& g = *a;
+        const int n = min(c0 + l16, g.N - 1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int mc = min(r0 + 4 * q + r, g.B - 1);
+            in.sf[r] = g.act_sf[mc];
+            in.as[r] = g.act_sum[mc];
+            if constexpr (MODE == MODE_QKV) {
+                const int pos = min(max(g.positions[mc], 0), g.S - 1);
+                const int d0 = 8 * ((c0 >> 4) & 7) + (l16 & 7);
+                in.pos[r] = pos;
+                in.cs[r] = bf2f(g.rope_cos[(int64_t)pos * 64 + d0]);
+                in.sn[r] = bf2f(g.rope_sin[(int64_t)pos * 64 + d0]);
+            }
+            if constexpr (MODE == MODE_O || MODE == MODE_DN) in.res[r] = g.resid[(int64_t)mc * g.out_stride + n];
+        }
+    }
     __device__ __forceinline__ void apply(int r0, int c0, const v4i_t& acc, int l16, int q) {
+        EpiIn in;
+        load(r0, c0, l16, q, in);
+        apply(r0, c0, acc, l16, q, in);
+    }
+    __device__ __forceinline__ void apply(int r0, int c0, const v4i_t& acc, int l16, int q, const EpiIn& in) {
         const GemvArgs& g = *a;
         const int tile = c0 >> 4, n = c0 + l16, B = g.B, N = g.N;
         float ws = g.ws0;
@@ -341,8 +375,7 @@ struct EpiDec {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int m = r0 + 4 * q + r;
-            const int mc = min(m, B - 1);
-            const float v = rbf(corrected(acc[r], ws, g.act_sum[mc], g.act_sf[mc]));
+            const float v = rbf(corrected(acc[r], ws, in.as[r], in.sf[r]));
             if constexpr (MODE == MODE_QKV || MODE == MODE_GU) {
                 const float pv = __shfl_xor(v, 8, 64);  // partner column l16 ^ 8 (same rows)
                 if (m >= B || tile * 16 >= N) continue;
@@ -354,11 +387,10 @@ struct EpiDec {
                 } else {
                     const int d0 = 8 * tt + (l16 & 7);
                     const float x1 = l16 < 8 ? v : pv, x2 = l16 < 8 ? pv : v;
-                    const int pos = min(max(g.positions[m], 0), g.S - 1);
+                    const int pos = in.pos[r];
                     float y = v;
                     if (proj < 2) {  // RotaryEmbedding._rotate (direct_inference_full.py:58-70)
-                        const float cs = bf2f(g.rope_cos[(int64_t)pos * 64 + d0]);
-                        const float sn = bf2f(g.rope_sin[(int64_t)pos * 64 + d0]);
+                        const float cs = in.cs[r], sn = in.sn[r];
                         y = l16 < 8 ? rbf(rbf(x1 * cs) - rbf(x2 * sn)) : rbf(rbf(x1 * sn) + rbf(x2 * cs));
                     }
                     const int d = d0 + (l16 < 8 ? 0 : 64);
@@ -366,15 +398,15 @@ struct EpiDec {
                         g.out[(int64_t)m * g.out_stride + head * 128 + d] = f2bf(y);
                     } else {
                         const int kvh = head - g.Hq - (proj == 2 ? g.Hkv : 0);
-                        uint16_t* cache =
-                            (proj == 1 ? g.kc : g.vc) + (int64_t)m * g.kv_b_stride + ((int64_t)kvh * g.S + pos) * 128;
-                        cache[d] = f2bf(y);
+                        uint16_t* cache = (proj == 1 ? g.kc : g.vc) + (int64_t)m * g.kv_b_stride + (int64_t)kvh * g.S * 128;
+                        if (proj == 2 && g.v_t) cache[(int64_t)d * g.S + pos] = f2bf(y);
+                        else cache[(int64_t)pos * 128 + d] = f2bf(y);
                     }
                 }
             } else {  // O / DN: out = bf16(resid + bf16(o))
                 if (m >= B || n >= N) continue;
                 const int64_t o = (int64_t)m * g.out_stride + n;
-                g.out[o] = f2bf(rbf(bf2f(g.resid[o]) + v));
+                g.out[o] = f2bf(rbf(bf2f(in.res[r]) + v));
             }
         }
     }
@@ -405,6 +437,100 @@ __global__ __launch_bounds__(256) void k_dec_mfma_part(GemvArgs a, int* __restri
     EpiPartial e{ws + (int64_t)s * a.B * a.N, a.B, a.N};
     tgemm_tile<2, kTgStagesWide>(a.w, a.q8, a.q8_stride, a.B, a.N, a.K, blockIdx.z * 128, blockIdx.x * 128, lds, e, c0,
                                  c1);
+}
+
+// Batched decode GEMM without split-K (B up to a few hundred): block (column block, row block) =
+// 16 TMT sequences x 16 TNT weight rows over the whole K. Its kDgWaves waves split K by I2_S blocks
+// of 128 (wave w: blocks w, w + kDgWaves, ...); fragments go straight from global memory (L2: the
+// codes are shared by every column block) into registers, two blocks in flight per wave (the
+// whole K of a 2560-deep GEMM is in flight at once). The waves' exact int32 sums are added through
+// LDS and each wave runs the fused EpiDec epilogue on one 16 x 16 tile: no partial slabs, no
+// second launch. Fragment mapping as wf_mfma.h: lane (l16, q) takes A[row][128 kb + 16 h + 32 q,
+// +16) and weight bytes [32 kb + 16 h, +16) of its column, bit offset 6 - 2q.
+constexpr int kDgWaves = 8;
+template <int TMT, int TNT, int NB, int MODE>
+__global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm(GemvArgs a) {
+    static_assert(TMT * TNT == kDgWaves, "one epilogue tile per wave");
+    __shared__ v4i_t red[kDgWaves][TMT * TNT][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+    const int n0 = blockIdx.x * 16 * TNT, m0 = blockIdx.y * 16 * TMT;
+    const int K = a.K, nkb = K >> 7;
+    const int8_t* ap[TMT];
+    const uint8_t* wp[TNT];
+#pragma unroll
+    for (int i = 0; i < TMT; ++i) ap[i] = a.q8 + (int64_t)min(m0 + 16 * i + l16, a.B - 1) * a.q8_stride + 32 * q;
+#pragma unroll
+    for (int j = 0; j < TNT; ++j) wp[j] = a.w + (int64_t)min(n0 + 16 * j + l16, a.N - 1) * (K >> 2);
+    v4i_t acc[TMT][TNT];
+#pragma unroll
+    for (int i = 0; i < TMT; ++i)
+#pragma unroll
+        for (int j = 0; j < TNT; ++j) acc[i][j] = v4i_t{0, 0, 0, 0};
+    uint4 fa[NB][TMT][2], fw[NB][TNT][2];
+    auto load = [&](uint4 (&la)[TMT][2], uint4 (&lw)[TNT][2], int kb) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+            for (int i = 0; i < TMT; ++i) la[i][h] = *reinterpret_cast<const uint4*>(ap[i] + 128 * kb + 16 * h);
+#pragma unroll
+            for (int j = 0; j < TNT; ++j) lw[j][h] = *reinterpret_cast<const uint4*>(wp[j] + 32 * kb + 16 * h);
+        }
+    };
+    const int sh = 6 - 2 * q;
+    auto mma = [&](const uint4 (&la)[TMT][2], const uint4 (&lw)[TNT][2]) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            v4i_t bf[TNT];
+#pragma unroll
+            for (int j = 0; j < TNT; ++j) {
+                const uint4 w = lw[j][h];
+                bf[j] = v4i_t{(int)((w.x >> sh) & 0x03030303u), (int)((w.y >> sh) & 0x03030303u),
+                              (int)((w.z >> sh) & 0x03030303u), (int)((w.w >> sh) & 0x03030303u)};
+            }
+#pragma unroll
+            for (int i = 0; i < TMT; ++i) {
+                const v4i_t af = __builtin_bit_cast(v4i_t, la[i][h]);
+#pragma unroll
+                for (int j = 0; j < TNT; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[j], acc[i][j], 0, 0, 0);
+            }
+        }
+    };
+    // wave w: I2_S blocks w + kDgWaves t, t < cnt; NB of them in flight
+    const int cnt = (nkb - wave + kDgWaves - 1) / kDgWaves;
+    WF_STAMP(0);
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+        if (b < cnt) load(fa[b], fw[b], wave + kDgWaves * b);
+    // the epilogue's per-row inputs, while the fragments are in flight
+    EpiDec<MODE> e{&a};
+    const int er0 = m0 + 16 * (wave / TNT), ec0 = n0 + 16 * (wave % TNT);
+    EpiIn ein;
+    e.load(er0, ec0, l16, q, ein);
+    WF_STAMP(1);
+    for (int t0 = 0; t0 < cnt; t0 += NB) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const int t = t0 + b;
+            if (t < cnt) {
+                mma(fa[b], fw[b]);
+                if (t == 0) WF_STAMP(2);
+                if (t + NB < cnt) load(fa[b], fw[b], wave + kDgWaves * (t + NB));
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < TMT; ++i)
+#pragma unroll
+        for (int j = 0; j < TNT; ++j) red[wave][i * TNT + j][lane] = acc[i][j];
+    WF_STAMP(3);
+    __syncthreads();
+    WF_STAMP(4);
+    v4i_t sum = red[0][wave][lane];
+#pragma unroll
+    for (int w = 1; w < kDgWaves; ++w) sum += red[w][wave][lane];
+    e.apply(er0, ec0, sum, l16, q, ein);
+    WF_STAMP(5);
+    WF_STAMP_DRAIN(6);
 }
 
 // One wave per 16 x 16 output tile: lane (l16, q) sums the nsplit int32 partials of rows
@@ -831,6 +957,7 @@ struct wf_model {
     uint2* am_part = nullptr;
     int lm_blocks = 0;
     int64_t q8_stride = 0;
+    int v_trans = 0;  // batched MFMA decode: V cache [L][B][Hkv][D][S]
     hipStream_t cap = nullptr;
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
@@ -884,7 +1011,15 @@ int dec_split(int N, int K, int* steps_per_split) {
 template <int MODE, int LPR>
 int launch_gemv_fmt(int fmt, const GemvArgs& ga, hipStream_t st) {
     if (fmt == WF_FMT_I2S && ga.B >= kDecMfmaMinB) {  // batched decode on the matrix cores, split-K
-        const int cb = (ga.N + 127) / 128, steps = ga.K / 64;
+        if (ga.B <= kDecGemmMaxB) {
+            const dim3 grid((ga.N + 63) / 64, (ga.B + 31) / 32);
+            if (ga.K <= 3 * 128 * kDgWaves)  // the whole K in flight at once
+                hipLaunchKernelGGL((k_dec_gemm<2, 4, 3, MODE>), grid, dim3(kDgWaves * 64), 0, st, ga);
+            else
+                hipLaunchKernelGGL((k_dec_gemm<2, 4, 2, MODE>), grid, dim3(kDgWaves * 64), 0, st, ga);
+            return check_launch("dec_gemm");
+        }
+        const int cb = (ga.N + 127) / 128;
         int sps = 0;
         const int nsplit = dec_split(ga.N, ga.K, &sps);
         if ((size_t)nsplit * ga.B * ga.N > ga.ws_ints) {
@@ -939,6 +1074,7 @@ GemvArgs base_args(const wf_model* m, int l) {
     a.kc = m->k_cache + l * kvl;
     a.vc = m->v_cache + l * kvl;
     a.kv_b_stride = (int64_t)d.n_kv_heads * d.max_seq * d.head_dim;
+    a.v_t = m->v_trans;
     return a;
 }
 
@@ -975,7 +1111,7 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
         case WF_OP_ATTN:  // split partials; merged by the O projection's input stage
             return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, a.kv_b_stride, (int64_t)S * D,
                                              B, d.n_heads, d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D),
-                                             m->part_ml, m->part_o, st);
+                                             m->part_ml, m->part_o, st, m->v_trans != 0);
         case WF_OP_O:  // h_b = h_a + o_proj(rms_norm(attn_sub_norm)(attn))
             a.w = d.w_o + (int64_t)l * H * wrow_bytes(d.wfmt, H); a.N = H; a.K = H; a.ws0 = wsh[3];
             a.resid = m->h_a; a.out = m->h_b; a.out_stride = H;
@@ -1086,6 +1222,7 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_ALLOC(m->h_a, 2 * (size_t)B * d.hidden);
     WF_ALLOC(m->h_b, 2 * (size_t)B * d.hidden);
     WF_ALLOC(m->qbuf, 2 * (size_t)B * d.hidden);
+    m->v_trans = (B >= kDecMfmaMinB && d.wfmt == WF_FMT_I2S && d.max_seq % 32 == 0) ? 1 : 0;
     if (B >= kDecMfmaMinB && d.wfmt == WF_FMT_I2S) {
         const int shapes[4][2] = {{m->qkv_rows, d.hidden}, {d.hidden, d.hidden}, {2 * d.inter, d.hidden}, {d.hidden, d.inter}};
         for (auto& sh : shapes)

@@ -83,7 +83,7 @@ __attribute__((visibility("hidden"))) static __device__ unsigned long long g_sta
 #define WF_STAMP(i)                                                                                 \
     do {                                                                                            \
         __builtin_amdgcn_sched_barrier(0);                                                          \
-        if ((threadIdx.x & 63) == 0) {                                                              \
+        if ((threadIdx.x & 63) == 0 && threadIdx.x < 256) {                                         \
             const unsigned sb_ = blockIdx.x + 2048u * blockIdx.y + 8192u * blockIdx.z;               \
             if (sb_ < (unsigned)::wf::kStampBlocks) {                                                \
                 unsigned long long* row_ = ::wf::g_stamps + (size_t)sb_ * ::wf::kStampSlots;          \

@@ -179,6 +179,9 @@ class BitNetDecoder:
         self.tokens = torch.zeros(B, dtype=torch.int32, device=self.dev)
         self.positions = torch.zeros(B, dtype=torch.int32, device=self.dev)
         self.logits = torch.zeros(B, cfg.vocab, dtype=torch.bfloat16, device=self.dev)
+        # batch >= 16 on I2_S (the matrix-core decode path) keeps V transposed per (layer, sequence,
+        # kv head): [head_dim, max_seq] (include/wf_bitnet.h wf_model_desc.v_cache)
+        self.v_transposed = batch >= 16 and wfmt == WF_FMT_I2S and cfg.max_seq % 32 == 0
         kv_shape = (L, B, cfg.n_kv_heads, cfg.max_seq, cfg.head_dim)
         self.k_cache = torch.zeros(kv_shape, dtype=torch.bfloat16, device=self.dev)
         self.v_cache = torch.zeros(kv_shape, dtype=torch.bfloat16, device=self.dev)
@@ -216,8 +219,26 @@ class BitNetDecoder:
         """Synthetic context: random bf16 K/V for positions [0, ctx) of every sequence."""
         g = torch.Generator(device=self.dev).manual_seed(seed)
         for l in range(self.cfg.layers):
-            for c in (self.k_cache, self.v_cache):
-                c[l, :, :, :ctx].normal_(generator=g)
+            self.k_cache[l, :, :, :ctx].normal_(generator=g)
+            v = self.v_view(l)
+            (v[..., :ctx] if self.v_transposed else v[:, :, :ctx]).normal_(generator=g)
+
+    def v_view(self, layer: int) -> torch.Tensor:
+        """V cache of one layer as stored: [B, Hkv, S, D], or [B, Hkv, D, S] when transposed."""
+        v = self.v_cache[layer]
+        if self.v_transposed:
+            B, H, S, D = v.shape
+            return v.view(B, H, D, S)
+        return v
+
+    def load_kv(self, layer: int, k: torch.Tensor, v: torch.Tensor) -> None:
+        """Write logical K/V [B, Hkv, n, D] into positions [0, n) of a layer (any storage layout)."""
+        n = k.shape[2]
+        self.k_cache[layer, :, :, :n].copy_(k)
+        if self.v_transposed:
+            self.v_view(layer)[..., :n].copy_(v.transpose(2, 3))
+        else:
+            self.v_cache[layer, :, :, :n].copy_(v)
 
     def step(self, graph: bool = True) -> None:
         """One decode token for every sequence (stream-ordered; no host sync)."""
