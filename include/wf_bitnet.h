@@ -15,6 +15,10 @@
  * Packed-weight formats (enc = w + 1 in {0,1,2}):
  *   WF_FMT_I2S : blocked I2_S [N, K/4] (cache/bitnet_converter.py:26-77) -- the reference layout.
  *   WF_FMT_TQ  : ~1.6-bit [N, ceil(K/80)*16], 5 trits per byte (load-time bijection of I2_S).
+ *   WF_FMT_I2S_MFMA: the I2_S bytes re-tiled for the int8 matrix cores (same size, N % 16 == 0):
+ *                dword ((n/16 * K/128 + kb) * 64 + (n%16) + 16q) * 2 + h = I2_S bytes
+ *                [32 kb + 16 h + 4 q, +4) of row n -- one contiguous KiB-class load per MFMA
+ *                fragment set. Used by the batched (batch >= 16) decode step.
  */
 #ifndef WF_BITNET_H
 #define WF_BITNET_H
@@ -31,7 +35,7 @@ extern "C" {
 #define WF_ENOTSUP 3
 
 enum { WF_F32 = 0, WF_BF16 = 1, WF_F16 = 2, WF_I8 = 3, WF_U8 = 4 };
-enum { WF_FMT_I2S = 0, WF_FMT_TQ = 1 };
+enum { WF_FMT_I2S = 0, WF_FMT_TQ = 1, WF_FMT_I2S_MFMA = 2 };
 
 /* ---- library ------------------------------------------------------------------------------ */
 const char* wf_last_error(void);
@@ -85,6 +89,9 @@ int wf_hf_to_i2s(const uint8_t* hf, int Np, int K, uint8_t* out, void* stream);
 int wf_i2s_to_tq(const uint8_t* i2s, int N, int K, uint8_t* tq, void* stream);
 int wf_tq_to_i2s(const uint8_t* tq, int N, int K, uint8_t* i2s, void* stream);
 int64_t wf_tq_row_bytes(int K);
+/* I2_S <-> WF_FMT_I2S_MFMA (bijection; N % 16 == 0, K % 128 == 0). */
+int wf_i2s_to_mfma(const uint8_t* i2s, int N, int K, uint8_t* out, void* stream);
+int wf_mfma_to_i2s(const uint8_t* mf, int N, int K, uint8_t* i2s, void* stream);
 
 /* ---- KV cache ----------------------------------------------------- */
 /* sgl_kernel.kvcache.KVCacheManager.scatter_kv / gather_kv (tests/test_kv_cache_cpp.py:283-373;

@@ -141,3 +141,28 @@ def test_bytes_accounting():
     from wfamd.model import BITNET_2B
     assert BITNET_2B.ternary_weights() == 2_084_044_800
     assert BITNET_2B.kv_bytes_per_token(1) == 76_800
+
+
+def test_kv_tile_layout_matches_device_offsets():
+    """wfamd.model.to_kv_tiles / from_kv_tiles agree with the device offsets k_tile_off /
+    v_tile_off (csrc/wf_norm.h) the batched decode writes and reads."""
+    import torch
+    from wfamd.model import from_kv_tiles, to_kv_tiles
+    S, D = 96, 128
+    k = torch.arange(S * D, dtype=torch.float32).reshape(1, S, D)
+    v = k + 0.5
+    kt, vt = to_kv_tiles(k, v)
+
+    def koff(t, d):
+        blk, o = t >> 5, t & 31
+        return ((((blk * 2 + ((o >> 2) & 1)) * 16 + (d >> 3)) * 16 + 4 * (o >> 3) + (o & 3)) * 8 + (d & 7))
+
+    def voff(t, d):
+        blk, o = t >> 5, t & 31
+        return ((((blk * 8 + (d >> 4)) * 4 + (o >> 3)) * 16 + (d & 15)) * 8 + (o & 7))
+    kf, vf = kt.reshape(-1), vt.reshape(-1)
+    for t in range(S):
+        for d in range(0, D, 5):
+            assert kf[koff(t, d)] == k[0, t, d] and vf[voff(t, d)] == v[0, t, d]
+    k2, v2 = from_kv_tiles(kt, vt)
+    assert torch.equal(k2, k) and torch.equal(v2, v)

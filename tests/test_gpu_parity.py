@@ -477,7 +477,7 @@ def test_decode_batched_long_ragged_context_matches_single():
     w = synthetic_weights(cfg, seed=3)
     B = 20
     decb = BitNetDecoder(cfg, w, batch=B)
-    assert decb.v_transposed
+    assert decb.kv_tiled
     gen = torch.Generator(device="cuda").manual_seed(11)
     ctx = 1900
     kv = [(torch.randn(B, 1, ctx, 128, generator=gen, device="cuda").to(torch.bfloat16),
@@ -491,7 +491,7 @@ def test_decode_batched_long_ragged_context_matches_single():
     torch.cuda.synchronize()
     for b in (0, 1, 3, 4, 7, 8, 10, 13, 15, 16, 18):
         d1 = BitNetDecoder(cfg, w, batch=1)
-        assert not d1.v_transposed
+        assert not d1.kv_tiled
         for l in range(2):
             d1.load_kv(l, kv[l][0][b:b + 1], kv[l][1][b:b + 1])
         d1.set_state([toks[b]], [pos[b]])
@@ -501,3 +501,22 @@ def test_decode_batched_long_ragged_context_matches_single():
         exp = d1.logits[0].float().cpu().numpy()
         assert rel_l2(got, exp) < 1e-4, (b, pos[b], rel_l2(got, exp))
         del d1
+
+
+def test_mfma_tile_format_roundtrip_and_gemv(orc):
+    """WF_FMT_I2S_MFMA is a bijection of I2_S (device repack both ways; include/wf_bitnet.h layout)."""
+    from wfamd import ops
+    rng = np.random.default_rng(17)
+    for n, k in ((64, 512), (3840, 2560), (2560, 6912)):
+        p = rng.integers(0, 256, size=(n, k // 4)).astype(np.uint8)
+        mf = ops.i2s_to_mfma(cu(p))
+        mfn = mf.cpu().numpy().reshape(-1).view(np.uint32)
+        # spot-check the documented dword order
+        nkb = k // 128
+        for t in rng.integers(0, mfn.size, size=64):
+            h, lane, blk = t & 1, (t >> 1) & 63, t >> 7
+            kb, ct = blk % nkb, blk // nkb
+            row = ct * 16 + (lane & 15)
+            off = 32 * kb + 16 * h + 4 * (lane >> 4)
+            assert mfn[t] == p[row, off:off + 4].view(np.uint32)[0]
+        assert np.array_equal(ops.mfma_to_i2s(mf).cpu().numpy(), p)

@@ -456,18 +456,18 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Batched decode attention partials on the bf16 matrix cores (v_mfma_f32_16x16x32_bf16), for a
-// V cache stored transposed per (sequence, kv head): Vt[d][S] (S % 32 == 0). Same partial records
-// as k_attn_part. Block (split s, kv head g, sequence b) = 4 waves; wave w walks 32-key tiles
+// Batched decode attention partials on the bf16 matrix cores (v_mfma_f32_16x16x32_bf16), on the
+// K / V caches in their tile layouts (wf_norm.h k_tile_off / v_tile_off; S % 32 == 0): every
+// fragment load is one contiguous KiB per wave. Same partial records as k_attn_part. Block (split s, kv head g, sequence b) = 4 waves; wave w walks 32-key tiles
 // base = t0 + 32 w + 128 i of its split (T = round_up(ceil(Sb / 8), 32)), online softmax per head.
 //   scores: two 16-key MFMA tiles, A = K rows (tile tau, row 4a + r <- key base + 8a + 4 tau + r),
 //     B = Q^T (column = query head of the group, rows >= grp zero; lane quarter q takes dims
-//     32q + 8c .. +8 of MFMA c = 0..3, the same permutation for both operands). Lane (head h, q)
+//     32c + 8q .. +8 of MFMA c = 0..3, the same for both operands). Lane (head h, q)
 //     then holds the scores of keys base + 8q + 0..7 -- exactly the A fragment (P rows = heads,
-//     k = keys) of the P.V MFMA, whose B fragment is Vt[16n + l16][base + 8q, +8): one 16-byte load.
+//     k = keys) of the P.V MFMA, whose B fragment is V[base + 8q, +8)[16n + l16].
 //   P enters the MFMA as bf16 hi + lo (two MFMAs), so P.V keeps ~16 mantissa bits (the VALU path's
-//     fp32 p within ~1e-5 relative). K rows past the split are clamped + masked to -inf, V columns
-//     past it zeroed (0 * stale = 0).
+//     fp32 p within ~1e-5 relative). Scores of keys past the split are masked to -inf (select, so a
+//     stale K row cannot leak a NaN), V entries past it zeroed (0 * stale = 0).
 // ---------------------------------------------------------------------------------------------
 typedef short v8s_t __attribute__((ext_vector_type(8)));
 typedef float v4f_t __attribute__((ext_vector_type(4)));
@@ -487,8 +487,8 @@ __global__ __launch_bounds__(256) void k_attn_mfma(const uint16_t* __restrict__ 
     const int t0 = s * T, t1 = min(t0 + T, Sb);
     __shared__ float sm_m[4][kAttnMfmaMaxGrp], sm_l[4][kAttnMfmaMaxGrp];
     __shared__ __attribute__((aligned(16))) float sm_o[4][kAttnMfmaMaxGrp][D];
-    const uint16_t* Kb = K + b * kv_sb + g * kv_sh;
-    const uint16_t* Vb = Vt + b * kv_sb + g * kv_sh;
+    const uint16_t* Kb = K + b * kv_sb + g * kv_sh + lane * 8;
+    const uint16_t* Vb = Vt + b * kv_sb + g * kv_sh + lane * 8;
     WF_STAMP(0);
 
     float m_run = -INFINITY, l_run = 0.f;
@@ -499,25 +499,23 @@ __global__ __launch_bounds__(256) void k_attn_mfma(const uint16_t* __restrict__ 
     if (base < t1) {
         v8s_t qf[4];
         {
-            const uint16_t* qp = q + b * q_sb + (int64_t)(hq0 + min(l16, grp - 1)) * D + 32 * q4;
+            const uint16_t* qp = q + b * q_sb + (int64_t)(hq0 + min(l16, grp - 1)) * D + 8 * q4;
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-                uint4 t = *reinterpret_cast<const uint4*>(qp + 8 * c);
+                uint4 t = *reinterpret_cast<const uint4*>(qp + 32 * c);
                 if (l16 >= grp) t = make_uint4(0, 0, 0, 0);
                 qf[c] = __builtin_bit_cast(v8s_t, t);
             }
         }
         auto load = [&](uint4 (&kr)[2][4], uint4 (&vr)[8], int bs) {
+            const int64_t blk = (int64_t)(bs >> 5) * 4096;  // 32 keys x 128 dims per tile block
 #pragma unroll
-            for (int tau = 0; tau < 2; ++tau) {
-                const int key = min(bs + 8 * (l16 >> 2) + 4 * tau + (l16 & 3), t1 - 1);
+            for (int tau = 0; tau < 2; ++tau)
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
-                    kr[tau][c] = *reinterpret_cast<const uint4*>(Kb + (int64_t)key * D + 32 * q4 + 8 * c);
-            }
+                    kr[tau][c] = *reinterpret_cast<const uint4*>(Kb + blk + (tau * 4 + c) * 512);
 #pragma unroll
-            for (int n = 0; n < 8; ++n)
-                vr[n] = *reinterpret_cast<const uint4*>(Vb + (int64_t)(16 * n + l16) * S + bs + 8 * q4);
+            for (int n = 0; n < 8; ++n) vr[n] = *reinterpret_cast<const uint4*>(Vb + blk + n * 512);
         };
         auto compute = [&](const uint4 (&kr)[2][4], const uint4 (&vr)[8], int bs) {
             v4f_t sc[2];
@@ -628,7 +626,7 @@ __global__ __launch_bounds__(256) void k_attn_mfma(const uint16_t* __restrict__ 
 
 int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
-                              float2* ml, float* o, hipStream_t st, bool v_trans) {
+                              float2* ml, float* o, hipStream_t st, bool kv_tiled) {
     const int grp = Hq / Hkv;
     if (grp > 8) {
         set_error("decode_attention_partials: GQA group %d > 8", grp);
@@ -644,9 +642,9 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
     }
     // batched: one block per kv head, the group's query heads share every K/V load (KV-bound)
     const dim3 grid(kAttnPartSplits, Hkv, B);
-    if (v_trans) {  // transposed V cache: matrix-core kernel
+    if (kv_tiled) {  // tile-layout caches: matrix-core kernel
         if (S % 32 != 0) {
-            set_error("decode_attention_partials: transposed V needs S %% 32 == 0 (S=%d)", S);
+            set_error("decode_attention_partials: tiled K/V need S %% 32 == 0 (S=%d)", S);
             return WF_EINVAL;
         }
         hipLaunchKernelGGL((k_attn_mfma<false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S,

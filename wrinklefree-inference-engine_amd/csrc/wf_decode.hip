@@ -29,7 +29,7 @@
 namespace wf {
 int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
-                              float2* ml, float* o, hipStream_t st, bool v_trans);
+                              float2* ml, float* o, hipStream_t st, bool kv_tiled);
 
 enum { MODE_QKV = 0, MODE_O = 1, MODE_GU = 2, MODE_DN = 3, MODE_LINEAR = 4 };  // LINEAR: BitNetLinear drop-in
 constexpr int kNT = 512;  // threads per GEMV / row-norm block (8 waves: 2 per SIMD hide the input-stage latency)
@@ -65,7 +65,7 @@ struct GemvArgs {
     uint16_t* kc;
     uint16_t* vc;
     int64_t kv_b_stride;
-    int v_t;  // V cache transposed per (sequence, kv head): [D][S] (batched MFMA decode)
+    int kv_t;  // K/V caches in the matrix-core tile layouts (wf_attn.hip kv_tile_off; batched decode)
 };
 
 // Reference correction (direct_inference_full.py:201-208) for one output:
@@ -399,7 +399,7 @@ struct EpiDec {
                     } else {
                         const int kvh = head - g.Hq - (proj == 2 ? g.Hkv : 0);
                         uint16_t* cache = (proj == 1 ? g.kc : g.vc) + (int64_t)m * g.kv_b_stride + (int64_t)kvh * g.S * 128;
-                        if (proj == 2 && g.v_t) cache[(int64_t)d * g.S + pos] = f2bf(y);
+                        if (g.kv_t) cache[proj == 1 ? k_tile_off(pos, d) : v_tile_off(pos, d)] = f2bf(y);
                         else cache[(int64_t)pos * 128 + d] = f2bf(y);
                     }
                 }
@@ -504,6 +504,96 @@ __global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm(GemvArgs a) {
     // the epilogue's per-row inputs, while the fragments are in flight
     EpiDec<MODE> e{&a};
     const int er0 = m0 + 16 * (wave / TNT), ec0 = n0 + 16 * (wave % TNT);
+    EpiIn ein;
+    e.load(er0, ec0, l16, q, ein);
+    WF_STAMP(1);
+    for (int t0 = 0; t0 < cnt; t0 += NB) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const int t = t0 + b;
+            if (t < cnt) {
+                mma(fa[b], fw[b]);
+                if (t == 0) WF_STAMP(2);
+                if (t + NB < cnt) load(fa[b], fw[b], wave + kDgWaves * (t + NB));
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < TMT; ++i)
+#pragma unroll
+        for (int j = 0; j < TNT; ++j) red[wave][i * TNT + j][lane] = acc[i][j];
+    WF_STAMP(3);
+    __syncthreads();
+    WF_STAMP(4);
+    v4i_t sum = red[0][wave][lane];
+#pragma unroll
+    for (int w = 1; w < kDgWaves; ++w) sum += red[w][wave][lane];
+    e.apply(er0, ec0, sum, l16, q, ein);
+    WF_STAMP(5);
+    WF_STAMP_DRAIN(6);
+}
+
+// The same GEMM on the matrix-core tile layouts (WF_FMT_I2S_MFMA weights, tile-ordered codes from
+// k_rownorm<..., TL>): every fragment load is one contiguous wave-instruction (A: 1 KiB of codes per
+// (row tile, I2_S block, half); B: 512 B of weight dwords per (column tile, I2_S block)), so the CU's
+// load pipeline moves whole cache lines (tools/ubench/load_rates: ~4 cycles per distinct line per
+// wave-instruction, whatever the bytes used). Lane (l16, q), block kb, half h: A = 16 codes of
+// k = 128 kb + 16 h + 4 q + jj + 32 g at [4g + jj]; B dword h = I2_S bytes [32 kb + 16 h + 4 q, +4)
+// of its column, decoded into the 4 groups g by shift 6 - 2g -- the same k for both operands.
+template <int TMT, int TNT, int NB, int MODE>
+__global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm_t(GemvArgs a) {
+    static_assert(TMT * TNT == kDgWaves, "one epilogue tile per wave");
+    __shared__ v4i_t red[kDgWaves][TMT * TNT][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+    const int ct0 = blockIdx.x * TNT, rt0 = blockIdx.y * TMT;
+    const int nkb = a.K >> 7;
+    const int nct = a.N >> 4, nrt = (a.B + 15) >> 4;
+    const int8_t* ap[TMT];
+    const uint8_t* wp[TNT];
+#pragma unroll
+    for (int i = 0; i < TMT; ++i) ap[i] = a.q8 + ((int64_t)min(rt0 + i, nrt - 1) * nkb << 11) + lane * 16;
+#pragma unroll
+    for (int j = 0; j < TNT; ++j) wp[j] = a.w + ((int64_t)min(ct0 + j, nct - 1) * nkb << 9) + lane * 8;
+    v4i_t acc[TMT][TNT];
+#pragma unroll
+    for (int i = 0; i < TMT; ++i)
+#pragma unroll
+        for (int j = 0; j < TNT; ++j) acc[i][j] = v4i_t{0, 0, 0, 0};
+    uint4 fa[NB][TMT][2];
+    uint2 fw[NB][TNT];
+    auto load = [&](uint4 (&la)[TMT][2], uint2 (&lw)[TNT], int kb) {
+#pragma unroll
+        for (int i = 0; i < TMT; ++i)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) la[i][h] = *reinterpret_cast<const uint4*>(ap[i] + ((int64_t)kb << 11) + (h << 10));
+#pragma unroll
+        for (int j = 0; j < TNT; ++j) lw[j] = *reinterpret_cast<const uint2*>(wp[j] + ((int64_t)kb << 9));
+    };
+    auto mma = [&](const uint4 (&la)[TMT][2], const uint2 (&lw)[TNT]) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            v4i_t bf[TNT];
+#pragma unroll
+            for (int j = 0; j < TNT; ++j) {
+                const uint32_t w = h ? lw[j].y : lw[j].x;
+                bf[j] = v4i_t{(int)((w >> 6) & 0x03030303u), (int)((w >> 4) & 0x03030303u), (int)((w >> 2) & 0x03030303u),
+                              (int)(w & 0x03030303u)};
+            }
+#pragma unroll
+            for (int i = 0; i < TMT; ++i) {
+                const v4i_t af = __builtin_bit_cast(v4i_t, la[i][h]);
+#pragma unroll
+                for (int j = 0; j < TNT; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[j], acc[i][j], 0, 0, 0);
+            }
+        }
+    };
+    const int cnt = (nkb - wave + kDgWaves - 1) / kDgWaves;
+    WF_STAMP(0);
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+        if (b < cnt) load(fa[b], fw[b], wave + kDgWaves * b);
+    EpiDec<MODE> e{&a};
+    const int er0 = (rt0 + wave / TNT) * 16, ec0 = (ct0 + wave % TNT) * 16;
     EpiIn ein;
     e.load(er0, ec0, l16, q, ein);
     WF_STAMP(1);
@@ -740,7 +830,7 @@ __global__ __launch_bounds__(256) void k_embed(const uint16_t* __restrict__ embe
 }
 
 // One block per row: rms_norm + quantize -> q8/sf/asum (Y16 = false), or the final norm -> bf16.
-template <int PPT, bool Y16>
+template <int PPT, bool Y16, bool TL = false>
 __global__ __launch_bounds__(kNT) void k_rownorm(const uint16_t* __restrict__ x, int64_t xs,
                                                  const uint16_t* __restrict__ nw, int K, float eps,
                                                  int8_t* __restrict__ q8, int64_t q8s, float* __restrict__ sf,
@@ -763,7 +853,9 @@ __global__ __launch_bounds__(kNT) void k_rownorm(const uint16_t* __restrict__ x,
         }
     } else {
         const float s = norm_row(nr, K, eps, y, red);
-        int as = quant_row<PPT, kNT>(y, s, K / 8, q8 + (int64_t)b * q8s, [](int p) { return 8 * p; });
+        int as;
+        if constexpr (TL) as = quant_row_tiled<PPT, kNT>(y, s, K / 8, q8, b, K >> 7);
+        else as = quant_row<PPT, kNT>(y, s, K / 8, q8 + (int64_t)b * q8s, [](int p) { return 8 * p; });
         as = wave_sum_i(as);
         if ((threadIdx.x & 63) == 0) red_i[threadIdx.x >> 6] = as;
         __syncthreads();
@@ -777,7 +869,7 @@ __global__ __launch_bounds__(kNT) void k_rownorm(const uint16_t* __restrict__ x,
 }
 
 // Batch > 1 O-projection input: attention row from the partials -> rms_norm -> int8 codes.
-template <int PPT>
+template <int PPT, bool TL = false>
 __global__ __launch_bounds__(kNT) void k_rownorm_attn(const float2* __restrict__ ml, const float* __restrict__ o, int Hq,
                                                       const uint16_t* __restrict__ nw, float eps, int8_t* __restrict__ q8,
                                                       int64_t q8s, float* __restrict__ sf, int* __restrict__ asum) {
@@ -791,12 +883,16 @@ __global__ __launch_bounds__(kNT) void k_rownorm_attn(const float2* __restrict__
     float y[PPT][8];
     ar.finish(Hq, 128, y);
     const float s = norm_core(nr, K, eps, y, red);
-    int as = quant_row<PPT, kNT>(y, s, K / 8, q8 + (int64_t)b * q8s, [](int p) { return 8 * p; });
+    int as;
+    if constexpr (TL) as = quant_row_tiled<PPT, kNT>(y, s, K / 8, q8, b, K >> 7);
+    else as = quant_row<PPT, kNT>(y, s, K / 8, q8 + (int64_t)b * q8s, [](int p) { return 8 * p; });
     as = wave_sum_i(as);
     if ((threadIdx.x & 63) == 0) red_i[threadIdx.x >> 6] = as;
     __syncthreads();
     if (threadIdx.x == 0) {
-        asum[b] = (red_i[0] + red_i[1]) + (red_i[2] + red_i[3]);
+        int t = 0;
+        for (int i = 0; i < kNT / 64; ++i) t += red_i[i];
+        asum[b] = t;
         sf[b] = s;
     }
 }
@@ -957,7 +1053,7 @@ struct wf_model {
     uint2* am_part = nullptr;
     int lm_blocks = 0;
     int64_t q8_stride = 0;
-    int v_trans = 0;  // batched MFMA decode: V cache [L][B][Hkv][D][S]
+    int kv_tiled = 0;  // batched MFMA decode: K/V caches in the tile layouts (include/wf_bitnet.h)
     hipStream_t cap = nullptr;
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
@@ -1010,6 +1106,14 @@ int dec_split(int N, int K, int* steps_per_split) {
 
 template <int MODE, int LPR>
 int launch_gemv_fmt(int fmt, const GemvArgs& ga, hipStream_t st) {
+    if (fmt == WF_FMT_I2S_MFMA) {  // batched decode on the matrix-core tile layouts
+        const dim3 grid(ga.N / 64 + ((ga.N & 63) ? 1 : 0), (ga.B + 31) / 32);
+        if (ga.K <= 3 * 128 * kDgWaves)  // the whole K in flight at once
+            hipLaunchKernelGGL((k_dec_gemm_t<2, 4, 3, MODE>), grid, dim3(kDgWaves * 64), 0, st, ga);
+        else
+            hipLaunchKernelGGL((k_dec_gemm_t<2, 4, 2, MODE>), grid, dim3(kDgWaves * 64), 0, st, ga);
+        return check_launch("dec_gemm_t");
+    }
     if (fmt == WF_FMT_I2S && ga.B >= kDecMfmaMinB) {  // batched decode on the matrix cores, split-K
         if (ga.B <= kDecGemmMaxB) {
             const dim3 grid((ga.N + 63) / 64, (ga.B + 31) / 32);
@@ -1040,15 +1144,19 @@ void launch_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, const uint
                     hipStream_t st) {
     const wf_model_desc& d = m->d;
     const bool big = norm_ppt(K) != 1;
-#define WF_RN(PPTV, Y)                                                                                            \
-    hipLaunchKernelGGL((k_rownorm<PPTV, Y>), dim3(d.batch), dim3(kNT), 0, st, x, xs, nw, K, d.eps, m->q8, m->q8_stride, \
+#define WF_RN(PPTV, Y, TL)                                                                                          \
+    hipLaunchKernelGGL((k_rownorm<PPTV, Y, TL>), dim3(d.batch), dim3(kNT), 0, st, x, xs, nw, K, d.eps, m->q8, m->q8_stride, \
                        m->act_sf, m->act_sum, y16, (int64_t)K)
+    const bool tl = d.wfmt == WF_FMT_I2S_MFMA;
     if (y16) {
-        if (big) WF_RN(2, true);
-        else WF_RN(1, true);
+        if (big) WF_RN(2, true, false);
+        else WF_RN(1, true, false);
+    } else if (tl) {
+        if (big) WF_RN(2, false, true);
+        else WF_RN(1, false, true);
     } else {
-        if (big) WF_RN(2, false);
-        else WF_RN(1, false);
+        if (big) WF_RN(2, false, false);
+        else WF_RN(1, false, false);
     }
 #undef WF_RN
 }
@@ -1074,7 +1182,7 @@ GemvArgs base_args(const wf_model* m, int l) {
     a.kc = m->k_cache + l * kvl;
     a.vc = m->v_cache + l * kvl;
     a.kv_b_stride = (int64_t)d.n_kv_heads * d.max_seq * d.head_dim;
-    a.v_t = m->v_trans;
+    a.kv_t = m->kv_tiled;
     return a;
 }
 
@@ -1111,7 +1219,7 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
         case WF_OP_ATTN:  // split partials; merged by the O projection's input stage
             return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, a.kv_b_stride, (int64_t)S * D,
                                              B, d.n_heads, d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D),
-                                             m->part_ml, m->part_o, st, m->v_trans != 0);
+                                             m->part_ml, m->part_o, st, m->kv_tiled != 0);
         case WF_OP_O:  // h_b = h_a + o_proj(rms_norm(attn_sub_norm)(attn))
             a.w = d.w_o + (int64_t)l * H * wrow_bytes(d.wfmt, H); a.N = H; a.K = H; a.ws0 = wsh[3];
             a.resid = m->h_a; a.out = m->h_b; a.out_stride = H;
@@ -1119,11 +1227,17 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             a.part_ml = m->part_ml;
             a.part_o = m->part_o;
             if (B > 1) {
-#define WF_RA(PPTV)                                                                                                  \
-    hipLaunchKernelGGL((k_rownorm_attn<PPTV>), dim3(B), dim3(kNT), 0, st, m->part_ml, m->part_o, d.n_heads, a.nw, d.eps, \
-                       m->q8, m->q8_stride, m->act_sf, m->act_sum)
-                if (norm_ppt(H) == 1) WF_RA(1);
-                else WF_RA(2);
+#define WF_RA(PPTV, TL)                                                                                                 \
+    hipLaunchKernelGGL((k_rownorm_attn<PPTV, TL>), dim3(B), dim3(kNT), 0, st, m->part_ml, m->part_o, d.n_heads, a.nw, \
+                       d.eps, m->q8, m->q8_stride, m->act_sf, m->act_sum)
+                const bool tl = d.wfmt == WF_FMT_I2S_MFMA;
+                if (norm_ppt(H) == 1) {
+                    if (tl) WF_RA(1, true);
+                    else WF_RA(1, false);
+                } else {
+                    if (tl) WF_RA(2, true);
+                    else WF_RA(2, false);
+                }
 #undef WF_RA
                 if ((rc = check_launch("rownorm_attn"))) return rc;
             }
@@ -1141,7 +1255,7 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
         case WF_OP_LM_HEAD: {  // final norm -> hn, logits = hn @ embed^T, greedy token
             launch_rownorm(m, m->h_a, H, d.final_norm, H, m->hn, st);
             if ((rc = check_launch("final_norm"))) return rc;
-            if (d.wfmt == WF_FMT_I2S && B >= kDecMfmaMinB) {
+            if ((d.wfmt == WF_FMT_I2S || d.wfmt == WF_FMT_I2S_MFMA) && B >= kDecMfmaMinB) {
                 WF_REQUIRE(H % 32 == 0, "lm_head: hidden %% 32 != 0");
                 const int nb = (d.vocab + 255) / 256;
                 hipLaunchKernelGGL(k_lm_head_mfma, dim3(nb, (B + 127) / 128), dim3(256), 0, st, d.embed, m->hn, H, d.vocab, B,
@@ -1190,7 +1304,9 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
                "model_create: hidden/inter (padded to the weight format) > 8192 not supported");
     WF_REQUIRE(d.batch >= 1 && d.batch <= 1024 && d.max_seq >= 1 && d.vocab >= 1 && d.layers >= 1,
                "model_create: bad sizes (batch 1..1024)");
-    WF_REQUIRE(d.wfmt == WF_FMT_I2S || d.wfmt == WF_FMT_TQ, "model_create: bad weight format");
+    WF_REQUIRE(d.wfmt == WF_FMT_I2S || d.wfmt == WF_FMT_TQ || d.wfmt == WF_FMT_I2S_MFMA, "model_create: bad weight format");
+    WF_REQUIRE(d.wfmt != WF_FMT_I2S_MFMA || (d.batch >= kDecMfmaMinB && d.hidden % 16 == 0 && d.inter % 16 == 0),
+               "model_create: WF_FMT_I2S_MFMA weights need batch >= %d", kDecMfmaMinB);
     WF_REQUIRE(d.embed && d.final_norm && d.rope_cos && d.rope_sin && d.ln_in && d.ln_post && d.attn_sub && d.ffn_sub &&
                    d.w_qkv && d.w_o && d.w_gu && d.w_d && d.wscale,
                "model_create: null weight pointer");
@@ -1222,7 +1338,7 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_ALLOC(m->h_a, 2 * (size_t)B * d.hidden);
     WF_ALLOC(m->h_b, 2 * (size_t)B * d.hidden);
     WF_ALLOC(m->qbuf, 2 * (size_t)B * d.hidden);
-    m->v_trans = (B >= kDecMfmaMinB && d.wfmt == WF_FMT_I2S && d.max_seq % 32 == 0) ? 1 : 0;
+    m->kv_tiled = (B >= kDecMfmaMinB && (d.wfmt == WF_FMT_I2S || d.wfmt == WF_FMT_I2S_MFMA) && d.max_seq % 32 == 0) ? 1 : 0;
     if (B >= kDecMfmaMinB && d.wfmt == WF_FMT_I2S) {
         const int shapes[4][2] = {{m->qkv_rows, d.hidden}, {d.hidden, d.hidden}, {2 * d.inter, d.hidden}, {d.hidden, d.inter}};
         for (auto& sh : shapes)
@@ -1233,7 +1349,7 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_ALLOC(m->part_o, sizeof(float) * (size_t)B * d.n_heads * kAttnPartSplits * d.head_dim);
     WF_ALLOC(m->hn, 2 * (size_t)B * d.hidden);
     WF_ALLOC(m->act, 2 * (size_t)B * d.inter);
-    WF_ALLOC(m->q8, (size_t)B * m->q8_stride);
+    WF_ALLOC(m->q8, (size_t)((B + 15) / 16 * 16) * m->q8_stride);  // tile layout: whole 16-row tiles
     WF_ALLOC(m->act_sf, sizeof(float) * B);
     WF_ALLOC(m->act_sum, sizeof(int) * B);
     WF_ALLOC(m->tickets, sizeof(unsigned) * kTicketWords * TK_COUNT);

@@ -251,6 +251,22 @@ __global__ void k_hf_to_i2s(const uint8_t* __restrict__ hf, int Np, int K, uint8
 }
 
 // I2S -> TQ: one thread per TQ byte (digit i of byte j of chunk c = weight 80c + 16i + j).
+// I2_S <-> matrix-core tiles (include/wf_bitnet.h WF_FMT_I2S_MFMA), one thread per dword.
+__global__ void k_i2s_mfma(const uint8_t* __restrict__ in, int N, int K, uint8_t* __restrict__ out, int fwd) {
+    const int nkb = K >> 7;
+    const int64_t nd = (int64_t)N * K / 16;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nd; t += (int64_t)gridDim.x * blockDim.x) {
+        const int h = (int)(t & 1), lane = (int)((t >> 1) & 63);
+        const int64_t blk = t >> 7;  // ct * nkb + kb
+        const int kb = (int)(blk % nkb);
+        const int64_t ct = blk / nkb;
+        const int64_t n = ct * 16 + (lane & 15);
+        const int64_t src = n * (K / 4) + 32 * kb + 16 * h + 4 * (lane >> 4);
+        if (fwd) reinterpret_cast<uint32_t*>(out)[t] = *reinterpret_cast<const uint32_t*>(in + src);
+        else *reinterpret_cast<uint32_t*>(out + src) = reinterpret_cast<const uint32_t*>(in)[t];
+    }
+}
+
 __global__ void k_i2s_to_tq(const uint8_t* __restrict__ in, int N, int K, uint8_t* __restrict__ out) {
     const int C = FmtTQ::chunks(K);
     const int64_t nb = (int64_t)N * C * 16;
@@ -406,6 +422,18 @@ int wf_hf_to_i2s(const uint8_t* hf, int Np, int K, uint8_t* out, void* stream) {
 }
 
 int64_t wf_tq_row_bytes(int K) { return FmtTQ::row_bytes(K); }
+
+int wf_i2s_to_mfma(const uint8_t* i2s, int N, int K, uint8_t* out, void* stream) {
+    WF_REQUIRE(i2s && out && N > 0 && N % 16 == 0 && K > 0 && K % 128 == 0, "i2s_to_mfma: bad arguments");
+    hipLaunchKernelGGL(k_i2s_mfma, dim3(grid_for((int64_t)N * K / 16)), dim3(256), 0, as_stream(stream), i2s, N, K, out, 1);
+    return check_launch("i2s_to_mfma");
+}
+
+int wf_mfma_to_i2s(const uint8_t* mf, int N, int K, uint8_t* i2s, void* stream) {
+    WF_REQUIRE(i2s && mf && N > 0 && N % 16 == 0 && K > 0 && K % 128 == 0, "mfma_to_i2s: bad arguments");
+    hipLaunchKernelGGL(k_i2s_mfma, dim3(grid_for((int64_t)N * K / 16)), dim3(256), 0, as_stream(stream), mf, N, K, i2s, 0);
+    return check_launch("mfma_to_i2s");
+}
 
 int wf_i2s_to_tq(const uint8_t* i2s, int N, int K, uint8_t* tq, void* stream) {
     WF_REQUIRE(i2s && tq && N > 0 && K > 0 && K % 128 == 0, "i2s_to_tq: bad arguments");

@@ -286,7 +286,48 @@ __device__ __forceinline__ int quant_row(const float (&y)[PPT][8], float sf, int
     return asum;
 }
 
+// quant_row into the matrix-core tile layout of the batched GEMM's activation codes: row `row`,
+// I2_S block kb, half h, lane l16 + 16q holds 16 codes at [4g + jj] = code of
+// k = 128 kb + 16 h + 4 q + jj + 32 g  (the permutation the WF_FMT_I2S_MFMA weight dwords decode to).
+__device__ __forceinline__ int64_t tile_code_pos(int row, int k, int nkb) {
+    const int o = k & 127;
+    return ((((int64_t)(row >> 4) * nkb + (k >> 7)) * 2 + ((o >> 4) & 1)) << 10) +
+           (((row & 15) + 16 * ((o & 15) >> 2)) << 4) + 4 * (o >> 5);
+}
+template <int PPT, int NT>
+__device__ __forceinline__ int quant_row_tiled(const float (&y)[PPT][8], float sf, int npad, int8_t* base, int row,
+                                               int nkb) {
+    const float inv = 1.0f / sf;
+    int asum = 0;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+        const int p = (int)threadIdx.x + NT * i;
+        const uint2 q = quant8(y[i], sf, inv, asum);
+        if (p < npad) {
+            *reinterpret_cast<uint32_t*>(base + tile_code_pos(row, 8 * p, nkb)) = q.x;
+            *reinterpret_cast<uint32_t*>(base + tile_code_pos(row, 8 * p + 4, nkb)) = q.y;
+        }
+    }
+    return asum;
+}
+
 constexpr int kAttnPartSplits = 8;
+
+// Matrix-core tile layouts of the K / V caches (batched decode; head_dim 128, S % 32 == 0), element
+// offsets within one (sequence, kv head) slab of S x 128 bf16. Key position t = 32 blk + o:
+//   K: [blk][tau 2][dg 16][row 16][8 dims], row = 4 (o >> 3) + (o & 3), tau = (o >> 2) & 1, dg = d >> 3
+//      -> the QK MFMA's A fragment (lane = row + 16 q, dims 32 c + 8 q) of key tile tau, step c, is
+//      one contiguous KiB;
+//   V: [blk][n 8][q 4][l 16][8 keys], n = d >> 4, l = d & 15, q = o >> 3 -> the P.V MFMA's B
+//      fragment (lane = l + 16 q, keys 8 q .. +8 of dims 16 n + l) is one contiguous KiB.
+__device__ __forceinline__ int64_t k_tile_off(int t, int d) {
+    const int blk = t >> 5, o = t & 31;
+    return ((((int64_t)blk * 2 + ((o >> 2) & 1)) * 16 + (d >> 3)) * 16 + 4 * (o >> 3) + (o & 3)) * 8 + (d & 7);
+}
+__device__ __forceinline__ int64_t v_tile_off(int t, int d) {
+    const int blk = t >> 5, o = t & 31;
+    return ((((int64_t)blk * 8 + (d >> 4)) * 4 + (o >> 3)) * 16 + (d & 15)) * 8 + (o & 7);
+}
 
 template <int PPT, int NT>
 struct AttnRow {

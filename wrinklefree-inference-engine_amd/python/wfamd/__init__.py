@@ -6,6 +6,6 @@
 
 The reference-facing drop-ins live next to this package: `sgl_kernel` and `wrinklefree_inference`.
 """
-from ._lib import WF_FMT_I2S, WF_FMT_TQ, kernel_available  # noqa: F401
+from ._lib import WF_FMT_I2S, WF_FMT_I2S_MFMA, WF_FMT_TQ, kernel_available  # noqa: F401
 
 __version__ = "0.1.0"

@@ -16,7 +16,7 @@ LIB_PATH = Path(os.environ.get("WF_BITNET_LIB", PKG_ROOT / "lib" / "libwfbitnet.
 
 WF_OK, WF_EINVAL, WF_EHIP, WF_ENOTSUP = 0, 1, 2, 3
 WF_F32, WF_BF16, WF_F16, WF_I8, WF_U8 = 0, 1, 2, 3, 4
-WF_FMT_I2S, WF_FMT_TQ = 0, 1
+WF_FMT_I2S, WF_FMT_TQ, WF_FMT_I2S_MFMA = 0, 1, 2
 (WF_OP_EMBED, WF_OP_QKV, WF_OP_ATTN, WF_OP_O, WF_OP_GATE_UP, WF_OP_DOWN, WF_OP_LM_HEAD) = range(7)
 
 vp, i32, i64, f32 = C.c_void_p, C.c_int, C.c_int64, C.c_float
@@ -40,6 +40,8 @@ SIGNATURES = {
     "wf_i2s_to_tq": (i32, [vp, i32, i32, vp, vp]),
     "wf_tq_to_i2s": (i32, [vp, i32, i32, vp, vp]),
     "wf_tq_row_bytes": (i64, [i32]),
+    "wf_i2s_to_mfma": (i32, [vp, i32, i32, vp, vp]),
+    "wf_mfma_to_i2s": (i32, [vp, i32, i32, vp, vp]),
     "wf_kv_scatter": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp]),
     "wf_kv_gather": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp]),
     "wf_kv_quant_i8": (i32, [vp, i32, i64, vp, vp, vp]),

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import _lib, ops
-from ._lib import WF_FMT_I2S, WF_FMT_TQ, WFModelDesc, call
+from ._lib import WF_FMT_I2S, WF_FMT_I2S_MFMA, WF_FMT_TQ, WFModelDesc, call
 
 
 @dataclass
@@ -49,7 +49,7 @@ class BitNetConfig:
     def weight_bytes_per_token(self, wfmt: int) -> int:
         """Algorithmic HBM bytes of one batch-1 decode step's weight stream (ternary + bf16 LM head)."""
         h, i, kv = self.hidden, self.inter, self.kv_dim
-        rb = (lambda k: k // 4) if wfmt == WF_FMT_I2S else ops.tq_row_bytes
+        rb = ops.tq_row_bytes if wfmt == WF_FMT_TQ else (lambda k: k // 4)
         tern = self.layers * ((h + 2 * kv) * rb(h) + h * rb(h) + 2 * i * rb(h) + h * rb(i))
         return tern + self.vocab * h * 2
 
@@ -156,8 +156,37 @@ def build_device_layout(cfg: BitNetConfig, w: Dict[str, torch.Tensor], wfmt: int
         gate_up = torch.cat([w["wg"][l], w["wu"][l]], dim=0).index_select(0, gu)
         parts = {"w_qkv": qkv, "w_o": w["wo"][l], "w_gu": gate_up, "w_d": w["wd"][l]}
         for name, t in parts.items():
-            out[name].append(ops.i2s_to_tq(t.contiguous()) if wfmt == WF_FMT_TQ else t.contiguous())
+            t = t.contiguous()
+            if wfmt == WF_FMT_TQ:
+                t = ops.i2s_to_tq(t)
+            elif wfmt == WF_FMT_I2S_MFMA:
+                t = ops.i2s_to_mfma(t)
+            out[name].append(t)
     return {k: torch.stack(v).contiguous() for k, v in out.items()}
+
+
+def to_kv_tiles(k: torch.Tensor, v: torch.Tensor):
+    """Logical K/V [..., S, 128] -> the tile layouts of the batched decode (include/wf_bitnet.h;
+    csrc/wf_norm.h k_tile_off / v_tile_off), same shapes. Key t = 32 blk + 8 a + 4 tau + r."""
+    *lead, S, D = k.shape
+    assert D == 128 and S % 32 == 0
+    kt = k.reshape(*lead, S // 32, 4, 2, 4, 16, 8)            # blk, a, tau, r, dg, e
+    nl = len(lead)
+    kt = kt.permute(*range(nl), nl, nl + 2, nl + 4, nl + 1, nl + 3, nl + 5)  # blk, tau, dg, a, r, e
+    vt = v.reshape(*lead, S // 32, 4, 8, 8, 16)                # blk, q, e, n, l
+    vt = vt.permute(*range(nl), nl, nl + 3, nl + 1, nl + 4, nl + 2)          # blk, n, q, l, e
+    return kt.reshape(*lead, S, D).contiguous(), vt.reshape(*lead, S, D).contiguous()
+
+
+def from_kv_tiles(kt: torch.Tensor, vt: torch.Tensor):
+    """Inverse of to_kv_tiles."""
+    *lead, S, D = kt.shape
+    nl = len(lead)
+    k = kt.reshape(*lead, S // 32, 2, 16, 4, 4, 8)            # blk, tau, dg, a, r, e
+    k = k.permute(*range(nl), nl, nl + 3, nl + 1, nl + 4, nl + 2, nl + 5)   # blk, a, tau, r, dg, e
+    v = vt.reshape(*lead, S // 32, 8, 4, 16, 8)                # blk, n, q, l, e
+    v = v.permute(*range(nl), nl, nl + 2, nl + 4, nl + 1, nl + 3)           # blk, q, e, n, l
+    return k.reshape(*lead, S, D).contiguous(), v.reshape(*lead, S, D).contiguous()
 
 
 class BitNetDecoder:
@@ -167,6 +196,10 @@ class BitNetDecoder:
                  wfmt: int = WF_FMT_I2S, device="cuda", debug_flags: int = 0):
         self.cfg, self.batch, self.wfmt = cfg, batch, wfmt
         self.dev = torch.device(device)
+        # batch >= 16 on I2_S runs the matrix-core GEMMs on their tile layout (same bytes, re-tiled)
+        if wfmt == WF_FMT_I2S and batch >= 16 and cfg.hidden % 16 == 0 and cfg.inter % 16 == 0:
+            wfmt = WF_FMT_I2S_MFMA
+        self.wfmt_device = wfmt
         lay = build_device_layout(cfg, weights, wfmt)
         self.w_qkv, self.w_o, self.w_gu, self.w_d = lay["w_qkv"], lay["w_o"], lay["w_gu"], lay["w_d"]
         self.embed = weights["embed"].contiguous()
@@ -179,9 +212,9 @@ class BitNetDecoder:
         self.tokens = torch.zeros(B, dtype=torch.int32, device=self.dev)
         self.positions = torch.zeros(B, dtype=torch.int32, device=self.dev)
         self.logits = torch.zeros(B, cfg.vocab, dtype=torch.bfloat16, device=self.dev)
-        # batch >= 16 on I2_S (the matrix-core decode path) keeps V transposed per (layer, sequence,
-        # kv head): [head_dim, max_seq] (include/wf_bitnet.h wf_model_desc.v_cache)
-        self.v_transposed = batch >= 16 and wfmt == WF_FMT_I2S and cfg.max_seq % 32 == 0
+        # batch >= 16 on I2_S (the matrix-core decode path) keeps K and V in the tile layouts of
+        # include/wf_bitnet.h (wf_model_desc.k_cache); to_kv_tiles / from_kv_tiles convert
+        self.kv_tiled = batch >= 16 and wfmt in (WF_FMT_I2S, WF_FMT_I2S_MFMA) and cfg.max_seq % 32 == 0
         kv_shape = (L, B, cfg.n_kv_heads, cfg.max_seq, cfg.head_dim)
         self.k_cache = torch.zeros(kv_shape, dtype=torch.bfloat16, device=self.dev)
         self.v_cache = torch.zeros(kv_shape, dtype=torch.bfloat16, device=self.dev)
@@ -216,29 +249,31 @@ class BitNetDecoder:
         self.positions.copy_(torch.as_tensor(positions, dtype=torch.int32))
 
     def fill_kv_random(self, ctx: int, seed: int = 0) -> None:
-        """Synthetic context: random bf16 K/V for positions [0, ctx) of every sequence."""
+        """Synthetic context: random bf16 K/V for positions [0, ctx) of every sequence (storage
+        order; in the tile layouts whole 32-key blocks)."""
         g = torch.Generator(device=self.dev).manual_seed(seed)
+        D = self.cfg.head_dim
         for l in range(self.cfg.layers):
-            self.k_cache[l, :, :, :ctx].normal_(generator=g)
-            v = self.v_view(l)
-            (v[..., :ctx] if self.v_transposed else v[:, :, :ctx]).normal_(generator=g)
-
-    def v_view(self, layer: int) -> torch.Tensor:
-        """V cache of one layer as stored: [B, Hkv, S, D], or [B, Hkv, D, S] when transposed."""
-        v = self.v_cache[layer]
-        if self.v_transposed:
-            B, H, S, D = v.shape
-            return v.view(B, H, D, S)
-        return v
+            for c in (self.k_cache, self.v_cache):
+                if self.kv_tiled:
+                    B, H, S, _ = c[l].shape
+                    c[l].view(B, H, S * D)[..., :(ctx + 31) // 32 * 32 * D].normal_(generator=g)
+                else:
+                    c[l, :, :, :ctx].normal_(generator=g)
 
     def load_kv(self, layer: int, k: torch.Tensor, v: torch.Tensor) -> None:
         """Write logical K/V [B, Hkv, n, D] into positions [0, n) of a layer (any storage layout)."""
         n = k.shape[2]
-        self.k_cache[layer, :, :, :n].copy_(k)
-        if self.v_transposed:
-            self.v_view(layer)[..., :n].copy_(v.transpose(2, 3))
-        else:
+        if not self.kv_tiled:
+            self.k_cache[layer, :, :, :n].copy_(k)
             self.v_cache[layer, :, :, :n].copy_(v)
+            return
+        kl, vl = from_kv_tiles(self.k_cache[layer], self.v_cache[layer])
+        kl[:, :, :n].copy_(k)
+        vl[:, :, :n].copy_(v)
+        kt, vt = to_kv_tiles(kl, vl)
+        self.k_cache[layer].copy_(kt)
+        self.v_cache[layer].copy_(vt)
 
     def step(self, graph: bool = True) -> None:
         """One decode token for every sequence (stream-ordered; no host sync)."""

@@ -224,6 +224,23 @@ def tq_row_bytes(k: int) -> int:
     return int(_lib.load().wf_tq_row_bytes(k))
 
 
+def i2s_to_mfma(i2s: torch.Tensor) -> torch.Tensor:
+    """I2_S [N, K/4] -> the matrix-core tile layout (include/wf_bitnet.h WF_FMT_I2S_MFMA), same shape."""
+    w = _on_device(i2s).contiguous()
+    n, k4 = w.shape
+    out = torch.empty_like(w)
+    call("wf_i2s_to_mfma", w.data_ptr(), n, 4 * k4, out.data_ptr(), _stream())
+    return out
+
+
+def mfma_to_i2s(mf: torch.Tensor) -> torch.Tensor:
+    w = _on_device(mf).contiguous()
+    n, k4 = w.shape
+    out = torch.empty_like(w)
+    call("wf_mfma_to_i2s", w.data_ptr(), n, 4 * k4, out.data_ptr(), _stream())
+    return out
+
+
 def i2s_to_tq(i2s: torch.Tensor) -> torch.Tensor:
     p = _on_device(i2s)
     n, k = p.shape[0], p.shape[1] * 4
