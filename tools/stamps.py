@@ -62,6 +62,13 @@ def summarize(st, kind, tail_slot):
         if col.size:
             out[name] = [round(float(col.min()), 2), round(float(np.median(col)), 2), round(float(col.max()), 2),
                          int(col.size)]
+    # per-block durations: median over blocks of (slot - own entry)
+    for sl, name in enumerate(NAMES[kind][:16]):
+        if name == "-" or sl == 0:
+            continue
+        ok = st[:, sl] > 0
+        if ok.any():
+            out.setdefault("block_dur", {})[name] = round(float(np.median((st[ok, sl] - st[ok, 0]) * 0.01)), 2)
     tails = np.nonzero(st[:, tail_slot] > 0)[0]
     if tails.size:
         i = tails[0]

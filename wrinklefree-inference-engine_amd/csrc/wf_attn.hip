@@ -7,6 +7,8 @@
 // the [.., S, D] layout). The G query heads of a GQA group share every K/V load.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "wf_common.h"
 #include "wf_device.h"
 #include "wf_norm.h"
@@ -473,7 +475,7 @@ typedef short v8s_t __attribute__((ext_vector_type(8)));
 typedef float v4f_t __attribute__((ext_vector_type(4)));
 constexpr int kAttnMfmaMaxGrp = 8;
 template <bool DB>
-__global__ __launch_bounds__(256) void k_attn_mfma(const uint16_t* __restrict__ q, int64_t q_sb,
+__global__ __launch_bounds__(256, 4) void k_attn_mfma(const uint16_t* __restrict__ q, int64_t q_sb,
                                                    const uint16_t* __restrict__ K, const uint16_t* __restrict__ Vt,
                                                    int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv, int S,
                                                    const int32_t* __restrict__ seq_lens, float sm_scale,
@@ -648,7 +650,7 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
             return WF_EINVAL;
         }
         hipLaunchKernelGGL((k_attn_mfma<false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S,
-                               seq_lens, sm_scale, ml, o);
+                           seq_lens, sm_scale, ml, o);
         return check_launch("decode_attention_partials");
     }
 #define WF_AP(GV)                                                                                                   \

@@ -336,6 +336,7 @@ struct EpiIn {
 template <int MODE>
 struct EpiDec {
     const GemvArgs* a;
+    // independent per-row loads (issue before the fragment loads) ...
     __device__ __forceinline__ void load(int r0, int c0, int l16, int q, EpiIn& in) const {
         const GemvArgs& g = *a;
         const int n = min(c0 + l16, g.N - 1);
@@ -344,19 +345,28 @@ struct EpiDec {
             const int mc = min(r0 + 4 * q + r, g.B - 1);
             in.sf[r] = g.act_sf[mc];
             in.as[r] = g.act_sum[mc];
-            if constexpr (MODE == MODE_QKV) {
-                const int pos = min(max(g.positions[mc], 0), g.S - 1);
-                const int d0 = 8 * ((c0 >> 4) & 7) + (l16 & 7);
+            if constexpr (MODE == MODE_QKV) in.pos[r] = g.positions[mc];
+            if constexpr (MODE == MODE_O || MODE == MODE_DN) in.res[r] = g.resid[(int64_t)mc * g.out_stride + n];
+        }
+    }
+    // ... and the RoPE entries, which depend on the position (issue after them)
+    __device__ __forceinline__ void load_rope(int c0, int l16, EpiIn& in) const {
+        if constexpr (MODE == MODE_QKV) {
+            const GemvArgs& g = *a;
+            const int d0 = 8 * ((c0 >> 4) & 7) + (l16 & 7);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int pos = min(max(in.pos[r], 0), g.S - 1);
                 in.pos[r] = pos;
                 in.cs[r] = bf2f(g.rope_cos[(int64_t)pos * 64 + d0]);
                 in.sn[r] = bf2f(g.rope_sin[(int64_t)pos * 64 + d0]);
             }
-            if constexpr (MODE == MODE_O || MODE == MODE_DN) in.res[r] = g.resid[(int64_t)mc * g.out_stride + n];
         }
     }
     __device__ __forceinline__ void apply(int r0, int c0, const v4i_t& acc, int l16, int q) {
         EpiIn in;
         load(r0, c0, l16, q, in);
+        load_rope(c0, l16, in);
         apply(r0, c0, acc, l16, q, in);
     }
     __device__ __forceinline__ void apply(int r0, int c0, const v4i_t& acc, int l16, int q, const EpiIn& in) {
@@ -498,14 +508,15 @@ __global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm(GemvArgs a) {
     // wave w: I2_S blocks w + kDgWaves t, t < cnt; NB of them in flight
     const int cnt = (nkb - wave + kDgWaves - 1) / kDgWaves;
     WF_STAMP(0);
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-        if (b < cnt) load(fa[b], fw[b], wave + kDgWaves * b);
-    // the epilogue's per-row inputs, while the fragments are in flight
+    // the epilogue's per-row inputs, around the fragment loads
     EpiDec<MODE> e{&a};
     const int er0 = m0 + 16 * (wave / TNT), ec0 = n0 + 16 * (wave % TNT);
     EpiIn ein;
     e.load(er0, ec0, l16, q, ein);
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+        if (b < cnt) load(fa[b], fw[b], wave + kDgWaves * b);
+    e.load_rope(ec0, l16, ein);
     WF_STAMP(1);
     for (int t0 = 0; t0 < cnt; t0 += NB) {
 #pragma unroll
@@ -589,13 +600,14 @@ __global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm_t(GemvArgs a) {
     };
     const int cnt = (nkb - wave + kDgWaves - 1) / kDgWaves;
     WF_STAMP(0);
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-        if (b < cnt) load(fa[b], fw[b], wave + kDgWaves * b);
     EpiDec<MODE> e{&a};
     const int er0 = (rt0 + wave / TNT) * 16, ec0 = (ct0 + wave % TNT) * 16;
     EpiIn ein;
     e.load(er0, ec0, l16, q, ein);
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+        if (b < cnt) load(fa[b], fw[b], wave + kDgWaves * b);
+    e.load_rope(ec0, l16, ein);
     WF_STAMP(1);
     for (int t0 = 0; t0 < cnt; t0 += NB) {
 #pragma unroll
