@@ -139,6 +139,15 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
         if constexpr (MODE == MODE_O || MODE == MODE_DN)
             resid_raw[m] = a.resid[(int64_t)(b0 + m) * a.out_stride + min(row, N - 1)];
     }
+    // batch 1 QKV: the RoPE entries of the epilogue (position: a scalar load, so the wait for it
+    // does not drain the vector loads above)
+    uint16_t rope_c = 0, rope_s = 0;
+    if constexpr (MODE == MODE_QKV && MB == 1) {
+        const int pos = min(max(a.positions[b0], 0), a.S - 1);
+        const int d0 = 8 * (blockIdx.x & 7) + (threadIdx.x & 7);
+        rope_c = a.rope_cos[(int64_t)pos * 64 + d0];
+        rope_s = a.rope_sin[(int64_t)pos * 64 + d0];
+    }
     // every load above is in flight before any input-stage arithmetic (hipcc would otherwise hoist
     // that math above the weight stream to save registers)
     if constexpr (kAttnIn) {
@@ -240,8 +249,8 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
             float x1 = s_out[m][i], x2 = s_out[m][8 + i];
             const int pos = min(max(a.positions[bi], 0), a.S - 1);  // never write outside the cache
             if (proj < 2) {  // RotaryEmbedding._rotate (direct_inference_full.py:58-70)
-                const float c = bf2f(a.rope_cos[(int64_t)pos * 64 + d0]);
-                const float s = bf2f(a.rope_sin[(int64_t)pos * 64 + d0]);
+                const float c = bf2f(MB == 1 ? rope_c : a.rope_cos[(int64_t)pos * 64 + d0]);
+                const float s = bf2f(MB == 1 ? rope_s : a.rope_sin[(int64_t)pos * 64 + d0]);
                 const float r1 = rbf(rbf(x1 * c) - rbf(x2 * s));
                 const float r2 = rbf(rbf(x1 * s) + rbf(x2 * c));
                 x1 = r1;
