@@ -707,6 +707,15 @@ __global__ __launch_bounds__(kNT) void k_quant_rows_lin(const uint16_t* __restri
     }
 }
 
+// [R][H] bf16 -> the fragment layout (bf_tile_off), one thread per 8-element piece (R % 16 == 0).
+__global__ void k_bf_tile(const uint16_t* __restrict__ src, int R, int H, uint16_t* __restrict__ dst) {
+    const int64_t np = (int64_t)R * (H >> 3);
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < np; t += (int64_t)gridDim.x * blockDim.x) {
+        const int r = (int)(t / (H >> 3)), p = (int)(t % (H >> 3));
+        *reinterpret_cast<uint4*>(dst + bf_tile_off(r, p, H)) = *reinterpret_cast<const uint4*>(src + t * 8);
+    }
+}
+
 // Batched LM head: logits[b, v] = bf16(sum_k hn[b, k] E[v, k]) on v_mfma_f32_16x16x32_bf16 (fp32
 // accumulation; lane quarter q takes k = 32s + 8q + 0..7 of step s for both operands). Block = 128
 // sequences x 256 vocabulary rows, 4 waves x 64 rows; each k-step is an LDS-DMA pipeline stage
@@ -727,18 +736,21 @@ __global__ __launch_bounds__(256) void k_lm_head_mfma(const uint16_t* __restrict
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
     const int m0 = blockIdx.y * 128, n0 = blockIdx.x * 256 + wave * 64;
     const int steps = H / 32;
+    // both operands in the fragment layout (bf_tile_off): fragment (tile, k-step c) of this lane at
+    // tile_base + 512 c elements -- one contiguous KiB per wave-instruction
+    const int nrt = (B + 15) >> 4, nvt = V >> 4;
     const uint16_t* asrc[2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) asrc[u] = hn + (int64_t)min(m0 + 16 * (2 * wave + u) + l16, B - 1) * H + 8 * q;
+    for (int u = 0; u < 2; ++u) asrc[u] = hn + (((int64_t)min((m0 >> 4) + 2 * wave + u, nrt - 1) * steps) << 9) + lane * 8;
     const uint16_t* bsrc[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bsrc[j] = E + (int64_t)min(n0 + 16 * j + l16, V - 1) * H + 8 * q;
+    for (int j = 0; j < 4; ++j) bsrc[j] = E + (((int64_t)min((n0 >> 4) + j, nvt - 1) * steps) << 9) + lane * 8;
     auto issue = [&](int c) {
         uint8_t* st = lds + (c % P) * kLmStageBytes;
 #pragma unroll
-        for (int u = 0; u < 2; ++u) glds16(asrc[u] + 32 * c, st + (2 * wave + u) * 1024);
+        for (int u = 0; u < 2; ++u) glds16(asrc[u] + 512 * c, st + (2 * wave + u) * 1024);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) glds16(bsrc[j] + 32 * c, st + 8192 + wave * 4096 + j * 1024);
+        for (int j = 0; j < 4; ++j) glds16(bsrc[j] + 512 * c, st + 8192 + wave * 4096 + j * 1024);
     };
     v4f_t acc[8][4];
 #pragma unroll
@@ -868,7 +880,7 @@ __global__ __launch_bounds__(kNT) void k_rownorm(const uint16_t* __restrict__ x,
         for (int i = 0; i < PPT; ++i) {
             const int p = threadIdx.x + kNT * i;
             if (p < K / 8)
-                *reinterpret_cast<uint4*>(y16 + (int64_t)b * ys + 8 * p) =
+                *reinterpret_cast<uint4*>(y16 + (TL ? bf_tile_off(b, p, K) : (int64_t)b * ys + 8 * p)) =
                     make_uint4(pk_bf16(y[i][0], y[i][1]), pk_bf16(y[i][2], y[i][3]), pk_bf16(y[i][4], y[i][5]),
                                pk_bf16(y[i][6], y[i][7]));
         }
@@ -1075,6 +1087,7 @@ struct wf_model {
     int lm_blocks = 0;
     int64_t q8_stride = 0;
     int kv_tiled = 0;  // batched MFMA decode: K/V caches in the tile layouts (include/wf_bitnet.h)
+    uint16_t* embed_t = nullptr;  // batched LM head: the tied embedding in the fragment layout (copy)
     hipStream_t cap = nullptr;
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
@@ -1169,9 +1182,14 @@ void launch_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, const uint
     hipLaunchKernelGGL((k_rownorm<PPTV, Y, TL>), dim3(d.batch), dim3(kNT), 0, st, x, xs, nw, K, d.eps, m->q8, m->q8_stride, \
                        m->act_sf, m->act_sum, y16, (int64_t)K)
     const bool tl = d.wfmt == WF_FMT_I2S_MFMA;
-    if (y16) {
-        if (big) WF_RN(2, true, false);
-        else WF_RN(1, true, false);
+    if (y16) {  // final norm: the matrix-core LM head reads it in the fragment layout
+        if (m->embed_t) {
+            if (big) WF_RN(2, true, true);
+            else WF_RN(1, true, true);
+        } else {
+            if (big) WF_RN(2, true, false);
+            else WF_RN(1, true, false);
+        }
     } else if (tl) {
         if (big) WF_RN(2, false, true);
         else WF_RN(1, false, true);
@@ -1276,11 +1294,10 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
         case WF_OP_LM_HEAD: {  // final norm -> hn, logits = hn @ embed^T, greedy token
             launch_rownorm(m, m->h_a, H, d.final_norm, H, m->hn, st);
             if ((rc = check_launch("final_norm"))) return rc;
-            if ((d.wfmt == WF_FMT_I2S || d.wfmt == WF_FMT_I2S_MFMA) && B >= kDecMfmaMinB) {
-                WF_REQUIRE(H % 32 == 0, "lm_head: hidden %% 32 != 0");
+            if (m->embed_t) {
                 const int nb = (d.vocab + 255) / 256;
-                hipLaunchKernelGGL(k_lm_head_mfma, dim3(nb, (B + 127) / 128), dim3(256), 0, st, d.embed, m->hn, H, d.vocab, B,
-                                   m->logits, m->am_part, nb);
+                hipLaunchKernelGGL(k_lm_head_mfma, dim3(nb, (B + 127) / 128), dim3(256), 0, st, m->embed_t, m->hn, H, d.vocab,
+                                   B, m->logits, m->am_part, nb);
                 hipLaunchKernelGGL(k_argmax_rows, dim3(B), dim3(256), 0, st, m->am_part, nb, m->tokens, m->positions, S);
                 break;
             }
@@ -1368,7 +1385,13 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     }
     WF_ALLOC(m->part_ml, sizeof(float2) * (size_t)B * d.n_heads * kAttnPartSplits);
     WF_ALLOC(m->part_o, sizeof(float) * (size_t)B * d.n_heads * kAttnPartSplits * d.head_dim);
-    WF_ALLOC(m->hn, 2 * (size_t)B * d.hidden);
+    WF_ALLOC(m->hn, 2 * (size_t)((B + 15) / 16 * 16) * d.hidden);  // fragment layout: whole row tiles
+    if ((d.wfmt == WF_FMT_I2S || d.wfmt == WF_FMT_I2S_MFMA) && B >= kDecMfmaMinB && d.vocab % 16 == 0 &&
+        d.hidden % 32 == 0) {
+        WF_ALLOC(m->embed_t, 2 * (size_t)d.vocab * d.hidden);
+        hipLaunchKernelGGL(k_bf_tile, dim3(4096), dim3(256), 0, nullptr, d.embed, d.vocab, d.hidden, m->embed_t);
+        if ((e = hipStreamSynchronize(nullptr)) != hipSuccess) return fail(e);
+    }
     WF_ALLOC(m->act, 2 * (size_t)B * d.inter);
     WF_ALLOC(m->q8, (size_t)((B + 15) / 16 * 16) * m->q8_stride);  // tile layout: whole 16-row tiles
     WF_ALLOC(m->act_sf, sizeof(float) * B);
@@ -1389,7 +1412,7 @@ int wf_model_destroy(wf_model* m) {
     if (m->graph) (void)hipGraphDestroy(m->graph);
     if (m->cap) (void)hipStreamDestroy(m->cap);
     void* ptrs[] = {m->seq_lens, m->h_a, m->h_b, m->qbuf, m->part_ml, m->part_o, m->hn, m->act, m->q8, m->dec_ws,
-                    m->act_sf, m->act_sum, m->tickets, m->am_part};
+                    m->act_sf, m->act_sum, m->tickets, m->am_part, m->embed_t};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete[] m->d.wscale;

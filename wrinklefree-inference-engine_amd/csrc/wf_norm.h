@@ -311,6 +311,13 @@ __device__ __forceinline__ int quant_row_tiled(const float (&y)[PPT][8], float s
     return asum;
 }
 
+// bf16 matrix-core fragment layout of a [rows][H] operand (16 x 32 fragments): element offset of
+// the 8-element piece p (k = 8p) of row r. Fragment (row tile, k-step s) = 64 lanes x 8 elements,
+// lane l16 + 16q = row 16 rt + l16, k = 32 s + 8 q: one contiguous KiB per wave-instruction.
+__device__ __forceinline__ int64_t bf_tile_off(int r, int p, int H) {
+    return ((((int64_t)(r >> 4) * (H >> 5) + (p >> 2)) << 6) + (r & 15) + 16 * (p & 3)) << 3;
+}
+
 constexpr int kAttnPartSplits = 8;
 
 // Matrix-core tile layouts of the K / V caches (batched decode; head_dim 128, S % 32 == 0), element
