@@ -562,7 +562,8 @@ __global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm(GemvArgs a) {
 // of its column, decoded into the 4 groups g by shift 6 - 2g -- the same k for both operands.
 template <int TMT, int TNT, int NB, int MODE>
 __global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm_t(GemvArgs a) {
-    static_assert(TMT * TNT == kDgWaves, "one epilogue tile per wave");
+    constexpr int EPT = TMT * TNT / kDgWaves;  // epilogue tiles per wave
+    static_assert(EPT * kDgWaves == TMT * TNT, "whole epilogue tiles per wave");
     __shared__ v4i_t red[kDgWaves][TMT * TNT][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
     const int ct0 = blockIdx.x * TNT, rt0 = blockIdx.y * TMT;
@@ -610,13 +611,20 @@ __global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm_t(GemvArgs a) {
     const int cnt = (nkb - wave + kDgWaves - 1) / kDgWaves;
     WF_STAMP(0);
     EpiDec<MODE> e{&a};
-    const int er0 = (rt0 + wave / TNT) * 16, ec0 = (ct0 + wave % TNT) * 16;
-    EpiIn ein;
-    e.load(er0, ec0, l16, q, ein);
+    int er0[EPT], ec0[EPT];
+    EpiIn ein[EPT];
+#pragma unroll
+    for (int x = 0; x < EPT; ++x) {
+        const int tile = wave * EPT + x;
+        er0[x] = (rt0 + tile / TNT) * 16;
+        ec0[x] = (ct0 + tile % TNT) * 16;
+        e.load(er0[x], ec0[x], l16, q, ein[x]);
+    }
 #pragma unroll
     for (int b = 0; b < NB; ++b)
         if (b < cnt) load(fa[b], fw[b], wave + kDgWaves * b);
-    e.load_rope(ec0, l16, ein);
+#pragma unroll
+    for (int x = 0; x < EPT; ++x) e.load_rope(ec0[x], l16, ein[x]);
     WF_STAMP(1);
     for (int t0 = 0; t0 < cnt; t0 += NB) {
 #pragma unroll
@@ -636,10 +644,14 @@ __global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm_t(GemvArgs a) {
     WF_STAMP(3);
     __syncthreads();
     WF_STAMP(4);
-    v4i_t sum = red[0][wave][lane];
 #pragma unroll
-    for (int w = 1; w < kDgWaves; ++w) sum += red[w][wave][lane];
-    e.apply(er0, ec0, sum, l16, q, ein);
+    for (int x = 0; x < EPT; ++x) {
+        const int tile = wave * EPT + x;
+        v4i_t sum = red[0][tile][lane];
+#pragma unroll
+        for (int w = 1; w < kDgWaves; ++w) sum += red[w][tile][lane];
+        e.apply(er0[x], ec0[x], sum, l16, q, ein[x]);
+    }
     WF_STAMP(5);
     WF_STAMP_DRAIN(6);
 }
@@ -1141,6 +1153,11 @@ int dec_split(int N, int K, int* steps_per_split) {
 template <int MODE, int LPR>
 int launch_gemv_fmt(int fmt, const GemvArgs& ga, hipStream_t st) {
     if (fmt == WF_FMT_I2S_MFMA) {  // batched decode on the matrix-core tile layouts
+        if (ga.N >= 8192) {  // wide layers (gate|up): 128-column tiles halve the code re-reads
+            const dim3 grid((ga.N + 127) / 128, (ga.B + 31) / 32);
+            hipLaunchKernelGGL((k_dec_gemm_t<2, 8, 2, MODE>), grid, dim3(kDgWaves * 64), 0, st, ga);
+            return check_launch("dec_gemm_t");
+        }
         const dim3 grid(ga.N / 64 + ((ga.N & 63) ? 1 : 0), (ga.B + 31) / 32);
         if (ga.K <= 3 * 128 * kDgWaves)  // the whole K in flight at once
             hipLaunchKernelGGL((k_dec_gemm_t<2, 4, 3, MODE>), grid, dim3(kDgWaves * 64), 0, st, ga);
