@@ -192,7 +192,7 @@ def main():
         dom_name = max(kern, key=lambda k: kern[k]["us_per_step"])
         dom = kern[dom_name]
         traffic = None
-        pmc = ROOT / "profiles" / "pmc_traffic.json"
+        pmc = ROOT / "profiles" / ("pmc_traffic.json" if B < 16 else f"pmc_traffic_b{B}.json")
         if pmc.exists():
             try:
                 traffic = json.loads(pmc.read_text()).get(dom_name, {}).get("hbm_bytes_per_launch")

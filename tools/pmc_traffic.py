@@ -6,7 +6,10 @@ reports half the bytes of 16-byte-per-lane coalesced streaming reads (every weig
 these kernels), so the read side is doubled. Writes profiles/pmc_traffic.json keyed by bench.py's
 op names, plus a copy named per round.
 
-    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write r01
+    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write r01 [pmc_traffic]
+
+The last argument names the unsuffixed copy bench.py reads (pmc_traffic.json for batch 1,
+pmc_traffic_b128.json for the batched step).
 """
 import csv
 import json
@@ -23,10 +26,15 @@ def op_name(kernel: str):
     m = re.search(r"k_gemv<wf::Fmt(\w+), (\d)", kernel)
     if m:
         return MODES[m.group(2)], m.group(1)
-    if "k_attn_part" in kernel:
+    m = re.search(r"k_dec_gemm(?:_t)?<\d+, \d+, \d+, (\d)>", kernel)
+    if m:  # batched matrix-core GEMMs (last template argument = mode)
+        return MODES[m.group(1)], "I2S_MFMA" if "k_dec_gemm_t" in kernel else "I2S"
+    if "k_attn_part" in kernel or "k_attn_mfma" in kernel:
         return "attn", None
     if "k_lm_head" in kernel:
         return "lm_head", None
+    if "k_rownorm_attn" in kernel:
+        return "rownorm_attn", None
     if "k_rownorm" in kernel:
         return "rownorm", None
     if "k_embed" in kernel:
@@ -53,6 +61,7 @@ def read(d: Path, counter: str):
 def main():
     fetch_dir, write_dir = Path(sys.argv[1]), Path(sys.argv[2])
     tag = sys.argv[3] if len(sys.argv) > 3 else "r01"
+    stem = sys.argv[4] if len(sys.argv) > 4 else "pmc_traffic"
     fetch, fmts = read(fetch_dir, "FETCH_SIZE")
     write, _ = read(write_dir, "WRITE_SIZE")
     out = {"_note": "bytes per launch; read side = 2 x FETCH_SIZE (gfx950 wide-read correction), "
@@ -67,8 +76,8 @@ def main():
                    "hbm_bytes_per_launch": round(fb + wb)}
     (ROOT / "profiles").mkdir(exist_ok=True)
     txt = json.dumps(out, indent=1)
-    (ROOT / "profiles" / "pmc_traffic.json").write_text(txt + "\n")
-    (ROOT / "profiles" / f"pmc_traffic_{tag}.json").write_text(txt + "\n")
+    (ROOT / "profiles" / f"{stem}.json").write_text(txt + "\n")
+    (ROOT / "profiles" / f"{stem}_{tag}.json").write_text(txt + "\n")
     print(txt)
 
 

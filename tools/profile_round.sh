@@ -1,0 +1,41 @@
+#!/bin/bash
+# Round-end evidence on one MI355X: parity tests, smoke, the batch-1 bench line (with the CPU
+# baseline), the batch-128 bench line, rocprofv3 kernel stats of both, the HBM-traffic PMC passes
+# of both, and the prefill GEMM bench. Outputs under gpurun_out/round/ (copied into profiles/ by
+# hand). Every GPU step has its own time limit; the script stops at the first failure.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$(pwd)
+O=$R/gpurun_out/round
+mkdir -p "$O"
+export TMPDIR=/tmp
+TAG=${TAG:-r01}
+step() { echo "== $1"; }
+
+step pytest
+timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider -rf > "$O/pytest_gpu.log" 2>&1 || exit $?
+tail -2 "$O/pytest_gpu.log"
+step smoke
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || exit $?
+step bench-b1
+timeout -k 10 600 python bench.py --steps 200 --warmup 10 > "$O/bench_b1.log" 2>&1 || exit $?
+tail -1 "$O/bench_b1.log" | cut -c1-200
+step bench-b128
+timeout -k 10 600 python bench.py --batch 128 --steps 100 --warmup 10 --no-cpu-baseline > "$O/bench_b128.log" 2>&1 || exit $?
+tail -1 "$O/bench_b128.log" | cut -c1-200
+for B in 1 128; do
+    step "rocprof b$B"
+    cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof_b$B" -o run -- \
+        python3 "$R/bench.py" --batch $B --steps 100 --warmup 10 --no-cpu-baseline > "$O/prof_b$B.log" 2>&1 || exit $?
+    cd "$R" && python3 tools/prof_summary.py "$O/prof_b$B" > "$O/kernel_stats_b$B.txt" 2>&1 || exit $?
+    for C in FETCH_SIZE WRITE_SIZE; do
+        step "pmc $C b$B"
+        cd /tmp && timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$O/pmc_${C}_b$B" -o run -- \
+            python3 "$R/bench.py" --batch $B --steps 20 --warmup 5 --no-cpu-baseline --no-op-timing > "$O/pmc_${C}_b$B.log" 2>&1 || exit $?
+        cd "$R"
+    done
+done
+step prefill
+timeout -k 10 300 python tools/prefill_gemm_bench.py > "$O/prefill.log" 2>&1 || exit $?
+tail -1 "$O/prefill.log"
+echo "== done"
