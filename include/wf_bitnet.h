@@ -121,6 +121,25 @@ int wf_decode_attention(const void* q, int q_dtype, int64_t q_sb, int64_t q_sh, 
                         int B, int Hq, int Hkv, int D, int S, const int32_t* seq_lens, float sm_scale, void* out,
                         int out_dtype, int64_t o_sb, int64_t o_sh, void* ws, void* stream);
 
+/* ---- SGLang BitNet linear method, MSB-interleaved layout ------------------- */
+/* Layout (sglang_backend/bitnet_quantization.py:99-105, :128-133): byte j of row n =
+ * code(w[4j])<<6 | code(w[4j+1])<<4 | code(w[4j+2])<<2 | code(w[4j+3]), code = w + 1.        */
+/* weights.abs().max().item() (bitnet_quantization.py:84): *out = max|x| (device float).       */
+int wf_absmax(const void* x, int dtype, int64_t n, float* out, void* stream);
+/* quantize_to_bitnet (bitnet_quantization.py:69-109) given its scale (the caller maps a scale
+ * < 1e-6 to 1.0 and raises for K % 128 != 0 like the reference's assert): normalized =
+ * rnd_dtype(w / float(scale)); code 2 if > 0.5, 0 if < -0.5, else 1. out [N, K/4].            */
+int wf_msb_ternarize(const void* w, int dtype, int N, int K, float scale, uint8_t* out, void* stream);
+/* dequantize_bitnet (bitnet_quantization.py:211-252): out[n,k] = (code-1) * float(scale) in
+ * out_dtype (F32/BF16/F16); K % 16 == 0, 16-byte aligned.                                    */
+int wf_msb_dequant(const uint8_t* packed, int N, int K, float scale, void* out, int out_dtype, void* stream);
+/* BitNetLinearMethod.apply (bitnet_quantization.py:366-409) computed from the packed bytes:
+ * y[m,n] = rnd(rnd(ws * sum_k (code-1) x[m,k]) + bias[n]), ws = scale rounded to the compute
+ * dtype (x_dtype: BF16 or F16; y and bias in the same dtype; bias may be NULL). fp32 accumulate.
+ * WF_ENOTSUP when K % 64 != 0 or K > 16384 (the caller then multiplies the dequantised matrix). */
+int wf_msb_linear(const uint8_t* w, float scale, const void* x, int x_dtype, int64_t ldx, int M, int N, int K,
+                  const void* bias, void* y, int64_t ldy, void* stream);
+
 /* ---- whole decode step (scripts/direct_inference_full.py:181-302) ------ */
 typedef struct {
     int hidden, layers, n_heads, n_kv_heads, head_dim, inter, vocab, max_seq, batch;

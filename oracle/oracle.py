@@ -57,6 +57,8 @@ def _load(path: Path):
         "orc_bitnet_linear_bf16": [vp, vp, f32, i32, i32, vp],
         "orc_attention_gqa_bf16": [vp, vp, vp, i32, i32, i32, i32, i32, f32, vp],
         "orc_decode_step": [vp, i32, i32, vp, vp],
+        "orc_msb_ternarize": [vp, i32, i32, i32, f32, vp], "orc_msb_dequant": [vp, i32, i32, f32, vp],
+        "orc_msb_linear": [vp, f32, vp, vp, i32, i32, i32, i32, vp],
     }
     for name, argt in sig.items():
         fn = getattr(L, name)
@@ -260,3 +262,36 @@ def f32_to_bf16(x: np.ndarray) -> np.ndarray:
     r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
     nan = np.isnan(np.asarray(x, dtype=np.float32))
     return np.where(nan, (u >> 16).astype(np.uint16) | 0x40, r).astype(np.uint16)
+
+
+# ---- SGLang BitNet linear method, MSB-interleaved layout (§8 a12) ----
+_MSB_DT = {"float32": 0, "bfloat16": 1, "float16": 2}
+
+
+def msb_ternarize(w: np.ndarray, scale: float, dtype: str = "float32") -> np.ndarray:
+    """w: float32 array holding values of `dtype`; returns uint8 [N, K/4]."""
+    w = np.ascontiguousarray(w, dtype=np.float32)
+    n, k = w.shape
+    out = np.zeros((n, k // 4), np.uint8)
+    _ck(lib().orc_msb_ternarize(_p(w), _MSB_DT[dtype], n, k, float(scale), _p(out)), "msb_ternarize")
+    return out
+
+
+def msb_dequant(p: np.ndarray, scale: float) -> np.ndarray:
+    p = np.ascontiguousarray(p, dtype=np.uint8)
+    out = np.zeros((p.shape[0], p.shape[1] * 4), np.float32)
+    _ck(lib().orc_msb_dequant(_p(p), p.shape[0], p.shape[1] * 4, float(scale), _p(out)), "msb_dequant")
+    return out
+
+
+def msb_linear(p: np.ndarray, ws: float, x: np.ndarray, bias: np.ndarray | None = None,
+               dtype: str = "bfloat16") -> np.ndarray:
+    """x [M, K] float32 holding values of `dtype`; ws = the weight scale rounded to `dtype`."""
+    p = np.ascontiguousarray(p, dtype=np.uint8)
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    b = None if bias is None else np.ascontiguousarray(bias, dtype=np.float32)
+    m, k = x.shape
+    y = np.zeros((m, p.shape[0]), np.float32)
+    _ck(lib().orc_msb_linear(_p(p), float(ws), _p(x), None if b is None else _p(b), _MSB_DT[dtype], m, p.shape[0],
+                             k, _p(y)), "msb_linear")
+    return y

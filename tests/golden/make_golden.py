@@ -351,12 +351,69 @@ def gen_decode():
     return save("decode", **out)
 
 
+def gen_msb():
+    """SGLang BitNet linear method: quantize_to_bitnet (bitnet_quantization.py:69-109),
+    dequantize_bitnet (:211-252, LUT path: numba is absent), BitNetLinearMethod.apply (:366-409) in
+    bf16 and fp16 with and without bias, and the activation-sparsity masks (activation_sparsity.py)."""
+    from wrinklefree_inference.sglang_backend import activation_sparsity as rsp
+    from wrinklefree_inference.sglang_backend import bitnet_quantization as rbq
+    g = torch.Generator().manual_seed(12)
+    out = {}
+    # ternarisation: fp32 / bf16 / fp16 weights, an all-zero matrix (scale -> 1.0) and exact +-0.5 ties
+    w32 = torch.randn(96, 256, generator=g)
+    wb = (torch.randn(64, 384, generator=g) * 0.3).to(torch.bfloat16)
+    wh = (torch.randn(32, 128, generator=g) * 3.0).to(torch.float16)
+    wz = torch.zeros(8, 128)
+    wt = torch.zeros(4, 128)
+    wt[0, :8] = torch.tensor([2.0, 1.0, -1.0, 0.999, -1.001, 1.001, -2.0, 0.0])
+    wt[1:, :] = torch.randn(3, 128, generator=g)
+    for name, w in (("w32", w32), ("wb", wb), ("wh", wh), ("wz", wz), ("wt", wt)):
+        packed, scale = rbq.quantize_to_bitnet(w)
+        out[f"{name}_in"] = w.float().numpy()
+        out[f"{name}_dtype"] = np.array({torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}[w.dtype])
+        out[f"{name}_packed"] = packed.numpy()
+        out[f"{name}_scale"] = np.array(scale, dtype=np.float64)
+        out[f"{name}_deq"] = rbq.dequantize_bitnet(packed, scale, w.shape[0], w.shape[1]).numpy()
+    # linear: N=192, K=1024 packed from random weights
+    wl = torch.randn(192, 1024, generator=g)
+    pl, sl = rbq.quantize_to_bitnet(wl)
+    out["lin_packed"], out["lin_scale"] = pl.numpy(), np.array(sl, dtype=np.float64)
+    bias = torch.randn(192, generator=g)
+    out["lin_bias"] = bias.numpy()
+    for m in (1, 3, 32):
+        x = torch.randn(m, 1024, generator=g)
+        out[f"lin_x{m}"] = x.numpy()
+        for dt, tag in ((torch.bfloat16, "bf"), (torch.float16, "h")):
+            meth = rbq.BitNetLinearMethod(compute_dtype=dt)
+            y = meth.apply(pl, sl, x, 192, 1024)
+            yb = meth.apply(pl, sl, x, 192, 1024, bias=bias)
+            out[f"lin_y{m}_{tag}"] = y.view(torch.int16).numpy().view(np.uint16)
+            out[f"lin_yb{m}_{tag}"] = yb.view(torch.int16).numpy().view(np.uint16)
+    # activation sparsity (float32 activations, 4 tokens)
+    xs = torch.randn(4, 256, generator=g) * torch.linspace(0.2, 3.0, 4).unsqueeze(1)
+    out["sp_x"] = xs.numpy()
+    out["sp_topk"], out["sp_topk_r"] = rsp.apply_top_k_sparsity(xs, 0.4)[0].numpy(), np.array(0.6)
+    thr, r = rsp.apply_threshold_sparsity(xs, 0.5)
+    out["sp_thr"], out["sp_thr_r"] = thr.numpy(), np.array(r)
+    ad, r = rsp.apply_adaptive_sparsity(xs, 0.3, 0.7)
+    out["sp_adapt"], out["sp_adapt_r"] = ad.numpy(), np.array(r)
+    return save("msb", **out)
+
+
+GENERATORS = {"packing": lambda: gen_packing(), "quant": lambda: gen_quant(), "gemv": lambda: gen_gemv(),
+              "linear": lambda: gen_linear(), "kv": lambda: gen_kv(), "attention": lambda: gen_attention(),
+              "decode": lambda: gen_decode(), "msb": lambda: gen_msb()}
+
+
 def main():
     torch.set_num_threads(8)
-    paths = [gen_packing(), gen_quant(), gen_gemv(), gen_linear(), gen_kv(), gen_attention(), gen_decode()]
-    manifest = {p.name: hashlib.sha256(p.read_bytes()).hexdigest() for p in paths}
+    names = sys.argv[1:] or list(GENERATORS)
+    paths = [GENERATORS[n]() for n in names]
+    mpath = OUT / "manifest.json"
+    manifest = json.loads(mpath.read_text()) if mpath.exists() else {}
+    manifest.update({p.name: hashlib.sha256(p.read_bytes()).hexdigest() for p in paths})
     manifest["_generator"] = "tests/golden/make_golden.py (reference @ /root/reference, torch " + torch.__version__ + ")"
-    (OUT / "manifest.json").write_text(json.dumps(manifest, indent=2, sort_keys=True) + "\n")
+    mpath.write_text(json.dumps(manifest, indent=2, sort_keys=True) + "\n")
     for p in paths:
         print(f"{p.name}: {p.stat().st_size} bytes")
 

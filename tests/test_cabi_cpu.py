@@ -166,3 +166,19 @@ def test_kv_tile_layout_matches_device_offsets():
             assert kf[koff(t, d)] == k[0, t, d] and vf[voff(t, d)] == v[0, t, d]
     k2, v2 = from_kv_tiles(kt, vt)
     assert torch.equal(k2, k) and torch.equal(v2, v)
+
+
+def test_sglang_backend_surface():
+    from wrinklefree_inference.sglang_backend import BITNET_QUANT_TYPES, BitNetConfig
+    from wrinklefree_inference.sglang_backend import bitnet_quantization as bq
+    for n in ("BitNetQuantType", "BITNET_BLOCK_SIZE", "BitNetWeightSpec", "quantize_to_bitnet", "dequantize_bitnet",
+              "dequantize_bitnet_reference", "bitnet_matmul_reference", "BitNetLinearMethod", "validate_bitnet_model"):
+        assert hasattr(bq, n), n
+    assert bq.BITNET_BLOCK_SIZE == 128 and len(BITNET_QUANT_TYPES) == 3 and int(bq.BitNetQuantType.I2_S) == 30
+    assert BitNetConfig.get_name() == "bitnet" and "I2_S" in repr(BitNetConfig())
+    spec = bq.BitNetWeightSpec((8, 128), bq.BitNetQuantType.I2_S, 1.0, (8, 32))
+    assert spec.compression_ratio == pytest.approx(16 / 1.58)
+    r = bq.validate_bitnet_model("/nonexistent/model-i2_s.gguf")
+    assert not r["valid"] and r["errors"]
+    meth = bq.BitNetLinearMethod()
+    assert meth.compute_dtype == torch.bfloat16 and meth.get_sparsity_stats() == {"enabled": False}

@@ -156,3 +156,72 @@ def test_decode_step_matches_reference(orc):
         top2 = np.sort(ref)[-2:]
         if top2[1] - top2[0] > 0.05 * abs(top2[1]):
             assert nxt == int(np.argmax(ref)), pos
+
+
+def _bits_to_f32(bits: np.ndarray, half: bool) -> np.ndarray:
+    if half:
+        return bits.view(np.float16).astype(np.float32)
+    return (bits.astype(np.uint32) << 16).view(np.float32)
+
+
+def _round_dt(x: np.ndarray, dt: str) -> np.ndarray:
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32))
+    return t.to(getattr(torch, dt)).float().numpy()
+
+
+class TestMsbLinearMethod:
+    """a12: sglang_backend/bitnet_quantization.py:69-153, :211-252, :366-409."""
+
+    def test_ternarize_matches_reference(self, orc):
+        g = load_golden("msb")
+        for name in ("w32", "wb", "wh", "wz", "wt"):
+            dt = ["float32", "bfloat16", "float16"][int(g[f"{name}_dtype"])]
+            got = orc.msb_ternarize(g[f"{name}_in"], float(g[f"{name}_scale"]), dt)
+            assert np.array_equal(got, g[f"{name}_packed"]), name
+        assert float(g["wz_scale"]) == 1.0 and np.all(g["wz_packed"] == 0x55)
+        # the exact +-0.5 ties of row 0 (w / max|w| with max = 2): 0.5 -> 0, -0.5 -> 0, 0.4995 -> 0
+        assert g["wt_packed"][0, 0] == (2 << 6 | 1 << 4 | 1 << 2 | 1)
+
+    def test_dequant_matches_reference(self, orc):
+        g = load_golden("msb")
+        for name in ("w32", "wb", "wh", "wz", "wt"):
+            assert np.array_equal(orc.msb_dequant(g[f"{name}_packed"], float(g[f"{name}_scale"])), g[f"{name}_deq"])
+
+    @pytest.mark.parametrize("tag,dt", [("bf", "bfloat16"), ("h", "float16")])
+    def test_linear_matches_reference(self, orc, tag, dt):
+        """The reference multiplies rnd(+-scale) weights in its GEMM order; the oracle sums in double and
+        applies rnd(scale) once: equal up to one rounding of the output (1 ulp of the compute dtype)."""
+        g = load_golden("msb")
+        ws = float(_round_dt(np.array([g["lin_scale"]], np.float32), dt)[0])
+        bias = _round_dt(g["lin_bias"], dt)
+        ulp = 2.0 ** -7 if tag == "bf" else 2.0 ** -10
+        for m in (1, 3, 32):
+            x = _round_dt(g[f"lin_x{m}"], dt)
+            for key, b in ((f"lin_y{m}_{tag}", None), (f"lin_yb{m}_{tag}", bias)):
+                ref = _bits_to_f32(g[key], tag == "h")
+                got = orc.msb_linear(g["lin_packed"], ws, x, b, dt)
+                err = np.abs(got - ref)
+                assert np.all(err <= ulp * np.abs(ref) + 1e-3 * ws), (key, float(err.max()))
+                assert np.mean(got == ref) > 0.9, key
+
+
+class TestActivationSparsity:
+    """Our device-op restatement of sglang_backend/activation_sparsity.py (host logic, runs on CPU
+    tensors too) against the reference's outputs."""
+
+    def test_masks_match_reference(self):
+        import torch
+        from wrinklefree_inference.sglang_backend import activation_sparsity as sp
+        g = load_golden("msb")
+        x = torch.from_numpy(g["sp_x"])
+        y, r = sp.apply_top_k_sparsity(x, 0.4)
+        assert np.array_equal(y.numpy(), g["sp_topk"]) and r == pytest.approx(float(g["sp_topk_r"]))
+        y, r = sp.apply_threshold_sparsity(x, 0.5)
+        assert np.array_equal(y.numpy(), g["sp_thr"]) and r == pytest.approx(float(g["sp_thr_r"]))
+        y, r = sp.apply_adaptive_sparsity(x, 0.3, 0.7)
+        assert np.array_equal(y.numpy(), g["sp_adapt"]) and r == pytest.approx(float(g["sp_adapt_r"]))
+        cfg = sp.get_qsparse_config()
+        y, r = sp.apply_sparsity(x, cfg)
+        assert np.array_equal(y.numpy(), g["sp_topk"]) and cfg.get_average_sparsity() == pytest.approx(0.6)
+        assert sp.apply_sparsity(x, sp.get_default_config())[0] is x

@@ -321,6 +321,13 @@ static inline int grid_for(int64_t n, int per = 256, int cap = 4096) {
 
 using namespace wf;
 
+namespace wf {
+int launch_absmax(const void* x, int dt, int64_t n, float* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_absmax, dim3(grid_for(n, 256, 2048)), dim3(256), 0, st, x, dt, n, reinterpret_cast<unsigned*>(out));
+    return check_launch("absmax");
+}
+}  // namespace wf
+
 extern "C" {
 
 const char* wf_last_error(void) { return wf::g_err; }

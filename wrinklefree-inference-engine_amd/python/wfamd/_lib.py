@@ -49,6 +49,10 @@ SIGNATURES = {
     "wf_decode_attention_ws_bytes": (i64, [i32, i32, i32, i32]),
     "wf_decode_attention": (i32, [vp, i32, i64, i64, vp, vp, i32, i64, i64, i64, f32, f32, i32, i32, i32, i32, i32,
                                   vp, f32, vp, i32, i64, i64, vp, vp]),
+    "wf_absmax": (i32, [vp, i32, i64, vp, vp]),
+    "wf_msb_ternarize": (i32, [vp, i32, i32, i32, f32, vp, vp]),
+    "wf_msb_dequant": (i32, [vp, i32, i32, f32, vp, i32, vp]),
+    "wf_msb_linear": (i32, [vp, f32, vp, i32, i64, i32, i32, i32, vp, vp, i64, vp]),
     "wf_model_create": (i32, [vp, vp]),
     "wf_model_destroy": (i32, [vp]),
     "wf_model_step": (i32, [vp, vp]),

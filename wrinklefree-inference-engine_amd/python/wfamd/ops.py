@@ -357,3 +357,55 @@ def register_torch_ops() -> bool:
     globals()["_torch_lib"] = lib
     _registered = True
     return True
+
+
+# ---------------------------------------------------------------------------------------------
+# a12: the SGLang BitNet linear method on the MSB-interleaved layout
+# (sglang_backend/bitnet_quantization.py:69-409)
+# ---------------------------------------------------------------------------------------------
+def absmax(x: torch.Tensor) -> float:
+    """max|x| over the whole tensor (device reduction; `.item()` like the reference)."""
+    xd = _on_device(x)
+    out = torch.empty(1, dtype=torch.float32, device=xd.device)
+    call("wf_absmax", xd.data_ptr(), _dtcode(xd), xd.numel(), out.data_ptr(), _stream())
+    return float(out.item())
+
+
+def msb_ternarize(weights: torch.Tensor, scale: float) -> torch.Tensor:
+    """quantize_to_bitnet's ternarise + pack (bitnet_quantization.py:88-105) for a given scale."""
+    n, k = weights.shape
+    wd = _on_device(weights)
+    out = torch.empty((n, k // 4), dtype=torch.uint8, device=wd.device)
+    call("wf_msb_ternarize", wd.data_ptr(), _dtcode(wd), n, k, float(scale), out.data_ptr(), _stream())
+    return out
+
+
+def msb_dequant(packed: torch.Tensor, scale: float, out_features: int, in_features: int,
+                dtype: torch.dtype = torch.float32) -> torch.Tensor:
+    """dequantize_bitnet (bitnet_quantization.py:211-252): (code - 1) * float(scale) -> dtype."""
+    if packed.dtype != torch.uint8 or tuple(packed.shape) != (out_features, in_features // 4):
+        raise ValueError(f"packed must be uint8 [{out_features}, {in_features // 4}], got {packed.dtype} "
+                         f"{tuple(packed.shape)}")
+    pd = _on_device(packed)
+    out = torch.empty((out_features, in_features), dtype=dtype, device=pd.device)
+    call("wf_msb_dequant", pd.data_ptr(), out_features, in_features, float(scale), out.data_ptr(), _dtcode(out),
+         _stream())
+    return out
+
+
+def msb_linear(packed: torch.Tensor, scale: float, x: torch.Tensor, out_features: int, in_features: int,
+               bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x [..., K] (bf16/f16, the compute dtype) @ dequant(packed)^T (+ bias), read from the 2-bit
+    bytes. Raises NotImplementedError for shapes the direct kernel does not take (K % 64 != 0 or
+    K > 16384); the caller then uses the dequantised matrix."""
+    if x.dtype not in (torch.bfloat16, torch.float16):
+        raise ValueError(f"msb_linear computes in bf16/f16, got {x.dtype}")
+    x2 = x.reshape(-1, in_features)
+    if x2.stride(-1) != 1 or x2.stride(0) % 8 != 0 or x2.data_ptr() % 16 != 0:
+        x2 = x2.contiguous()
+    m = x2.shape[0]
+    y = torch.empty((m, out_features), dtype=x.dtype, device=x2.device)
+    b = None if bias is None else bias.to(device=x2.device, dtype=x.dtype).contiguous()
+    call("wf_msb_linear", packed.data_ptr(), float(scale), x2.data_ptr(), _dtcode(x2), x2.stride(0), m, out_features,
+         in_features, _ptr(b), y.data_ptr(), out_features, _stream())
+    return y.reshape(*x.shape[:-1], out_features)
