@@ -6,7 +6,7 @@ w[4j] (bits 7-6) .. w[4j+3] (bits 1-0) as code = w + 1. The reference is a CPU m
 once (numba/LUT), cache the bf16 matrix and run `x @ W^T`. Here every piece runs on the GPU:
 
 * `quantize_to_bitnet` / `dequantize_bitnet`: HIP kernels (wf_msb_ternarize / wf_msb_dequant).
-* `BitNetLinearMethod.apply` for up to 16 rows reads the packed 2-bit bytes directly
+* `BitNetLinearMethod.apply` for up to 4 rows reads the packed 2-bit bytes directly
   (wf_msb_linear: codes -> bf16/fp16 +-1/0 pairs in registers, v_dot2 accumulate; 8x fewer HBM bytes
   than the cached bf16 matrix the reference multiplies). Larger batches (or K the direct kernel
   does not take) multiply the cached dequantised matrix with the library GEMM (hipBLASLt), which
@@ -45,8 +45,9 @@ class BitNetQuantType(IntEnum):
 BITNET_QUANT_TYPES = {BitNetQuantType.I2_S, BitNetQuantType.TL1, BitNetQuantType.TL2}
 BITNET_BLOCK_SIZE = 128
 
-# rows up to which apply() reads the packed bytes directly (above: cached bf16 matrix + GEMM)
-DIRECT_MAX_ROWS = 16
+# rows up to which apply() reads the packed bytes directly (above: cached bf16 matrix + GEMM);
+# measured crossover (tools/msb_bench.py): 4 rows 5.9-19 us vs GEMM 11-38 us, 16 rows 23-72 us vs 12-38 us
+DIRECT_MAX_ROWS = 4
 
 
 @dataclass
