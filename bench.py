@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-op-timing", action="store_true")
+    ap.add_argument("--max-seq", type=int, default=0, help="KV rows per (sequence, kv head); 0 = model default")
     return ap.parse_args()
 
 
@@ -168,6 +169,9 @@ def main():
         raise SystemExit("gfx950 HIP kernels unavailable: build with __graft_entry__.build()")
 
     cfg = BITNET_2B
+    if args.max_seq:
+        import dataclasses
+        cfg = dataclasses.replace(cfg, max_seq=args.max_seq)
     B = args.batch
     wfmt = WF_FMT_TQ if args.wfmt == "tq" else WF_FMT_I2S
     total = args.warmup + args.steps

@@ -6,6 +6,7 @@
 // head dimension, so one wave-instruction reads 4 contiguous 256-byte K rows (coalesced 1 KiB for
 // the [.., S, D] layout). The G query heads of a GQA group share every K/V load.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -460,8 +461,10 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
 // ---------------------------------------------------------------------------------------------
 // Batched decode attention partials on the bf16 matrix cores (v_mfma_f32_16x16x32_bf16), on the
 // K / V caches in their tile layouts (wf_norm.h k_tile_off / v_tile_off; S % 32 == 0): every
-// fragment load is one contiguous KiB per wave. Same partial records as k_attn_part. Block (split s, kv head g, sequence b) = 4 waves; wave w walks 32-key tiles
-// base = t0 + 32 w + 128 i of its split (T = round_up(ceil(Sb / 8), 32)), online softmax per head.
+// fragment load is one contiguous KiB per wave. Same partial records as k_attn_part (a record holds
+// the keys its block's waves took, not a contiguous range: the merge is order-free). Block
+// (split s, kv head g, sequence b) = 4 waves; wave w walks 32-key tiles base = 32 (4 s + w) + 1024 i
+// (round-robin over the 32 waves of (b, g)), online softmax per head.
 //   scores: two 16-key MFMA tiles, A = K rows (tile tau, row 4a + r <- key base + 8a + 4 tau + r),
 //     B = Q^T (column = query head of the group, rows >= grp zero; lane quarter q takes dims
 //     32c + 8q .. +8 of MFMA c = 0..3, the same for both operands). Lane (head h, q)
@@ -474,8 +477,8 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
 typedef short v8s_t __attribute__((ext_vector_type(8)));
 typedef float v4f_t __attribute__((ext_vector_type(4)));
 constexpr int kAttnMfmaMaxGrp = 8;
-template <bool DB>
-__global__ __launch_bounds__(256, 4) void k_attn_mfma(const uint16_t* __restrict__ q, int64_t q_sb,
+template <bool DB, bool RR>
+__global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* __restrict__ q, int64_t q_sb,
                                                    const uint16_t* __restrict__ K, const uint16_t* __restrict__ Vt,
                                                    int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv, int S,
                                                    const int32_t* __restrict__ seq_lens, float sm_scale,
@@ -485,8 +488,12 @@ __global__ __launch_bounds__(256, 4) void k_attn_mfma(const uint16_t* __restrict
     const int grp = Hq / Hkv, hq0 = g * grp;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
     const int Sb = min(seq_lens[b], S);
+    // 32-key tiles dealt round-robin over the 4 * kAttnPartSplits waves of (b, g): wave (s, w)
+    // takes tiles 4 s + w + 32 i, so per-wave tile counts differ by at most one and a block's four
+    // waves finish together (a contiguous split per block left wave 0 with twice the tiles)
     const int T = ((Sb + kAttnPartSplits - 1) / kAttnPartSplits + 31) / 32 * 32;
-    const int t0 = s * T, t1 = min(t0 + T, Sb);
+    const int kStride = RR ? 32 * 4 * kAttnPartSplits : 128;
+    const int t1 = RR ? Sb : min(s * T + T, Sb);
     __shared__ float sm_m[4][kAttnMfmaMaxGrp], sm_l[4][kAttnMfmaMaxGrp];
     __shared__ __attribute__((aligned(16))) float sm_o[4][kAttnMfmaMaxGrp][D];
     const uint16_t* Kb = K + b * kv_sb + g * kv_sh + lane * 8;
@@ -497,7 +504,7 @@ __global__ __launch_bounds__(256, 4) void k_attn_mfma(const uint16_t* __restrict
     v4f_t acc[8];
 #pragma unroll
     for (int n = 0; n < 8; ++n) acc[n] = v4f_t{0.f, 0.f, 0.f, 0.f};
-    int base = t0 + 32 * wave;
+    int base = RR ? 32 * (4 * s + wave) : s * T + 32 * wave;
     if (base < t1) {
         v8s_t qf[4];
         {
@@ -578,18 +585,18 @@ __global__ __launch_bounds__(256, 4) void k_attn_mfma(const uint16_t* __restrict
         load(kA, vA, base);
         if constexpr (DB) {
             uint4 kB[2][4], vB[8];
-            for (; base < t1; base += 256) {
-                const int nb = base + 128;
+            for (; base < t1; base += 2 * kStride) {
+                const int nb = base + kStride;
                 if (nb < t1) load(kB, vB, nb);
                 compute(kA, vA, base);
                 if (nb >= t1) break;
-                if (nb + 128 < t1) load(kA, vA, nb + 128);
+                if (nb + kStride < t1) load(kA, vA, nb + kStride);
                 compute(kB, vB, nb);
             }
         } else {
-            for (; base < t1; base += 128) {
+            for (; base < t1; base += kStride) {
                 compute(kA, vA, base);
-                if (base + 128 < t1) load(kA, vA, base + 128);
+                if (base + kStride < t1) load(kA, vA, base + kStride);
             }
         }
     }
@@ -649,8 +656,16 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
             set_error("decode_attention_partials: tiled K/V need S %% 32 == 0 (S=%d)", S);
             return WF_EINVAL;
         }
-        hipLaunchKernelGGL((k_attn_mfma<false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S,
-                           seq_lens, sm_scale, ml, o);
+        static const int variant = getenv("WF_ATTN_VARIANT") ? atoi(getenv("WF_ATTN_VARIANT")) : 0;
+        if (variant == 1)
+            hipLaunchKernelGGL((k_attn_mfma<false, true>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv,
+                               S, seq_lens, sm_scale, ml, o);
+        else if (variant == 2)
+            hipLaunchKernelGGL((k_attn_mfma<true, false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv,
+                               S, seq_lens, sm_scale, ml, o);
+        else
+            hipLaunchKernelGGL((k_attn_mfma<false, false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq,
+                               Hkv, S, seq_lens, sm_scale, ml, o);
         return check_launch("decode_attention_partials");
     }
 #define WF_AP(GV)                                                                                                   \
