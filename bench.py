@@ -44,6 +44,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-op-timing", action="store_true")
     ap.add_argument("--max-seq", type=int, default=0, help="KV rows per (sequence, kv head); 0 = model default")
+    ap.add_argument("--ctx-dist", choices=["fixed", "uniform"], default="fixed",
+                    help="uniform: per-sequence contexts drawn from U[1, max_seq - steps) with seed 0 (SURVEY §8d "
+                         "config 4), on paged KV")
+    ap.add_argument("--paged", action="store_true", help="paged KV (32-token pages; batch >= 16)")
     return ap.parse_args()
 
 
@@ -176,12 +180,23 @@ def main():
     wfmt = WF_FMT_TQ if args.wfmt == "tq" else WF_FMT_I2S
     total = args.warmup + args.steps
     ctx = max(1, min(args.ctx, cfg.max_seq - total - 1))
+    import numpy as np
+    paged = args.paged or args.ctx_dist == "uniform"
+    if args.ctx_dist == "uniform":
+        ctxs = np.random.default_rng(0).integers(1, cfg.max_seq - total - 1, size=B)
+    else:
+        ctxs = np.full(B, ctx, dtype=np.int64)
+    num_pages = int(sum((c + total + 1 + 31) // 32 for c in ctxs)) if paged else 0
     w = synthetic_weights(cfg, seed=0, device="cuda")
-    dec = BitNetDecoder(cfg, w, batch=B, wfmt=wfmt)
+    dec = BitNetDecoder(cfg, w, batch=B, wfmt=wfmt, num_pages=num_pages, page_seed=0 if paged else None)
     del w
     torch.cuda.empty_cache()
+    if paged:
+        for b in range(B):
+            dec.reserve(b, int(ctxs[b]) + total + 1)
     dec.fill_kv_random(ctx, seed=1)
-    dec.set_state([1] * B, [ctx] * B)
+    dec.set_state([1] * B, [int(c) for c in ctxs])
+    ctx = int(round(float(ctxs.mean())))
 
     for _ in range(args.warmup):
         dec.step(graph=True)
@@ -216,10 +231,15 @@ def main():
             "value": round(tok_s, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "int8", "data": "synthetic",
-            "config": {"workload": f"decode batch={B} (BASELINE configs[1])" if B == 1 else f"decode batch={B}",
+            "config": {"workload": f"decode batch={B} (BASELINE configs[1])" if B == 1 else
+                       f"decode batch={B}" + (" (BASELINE configs[3]: contexts U[1, max_seq), continuous decode)"
+                                              if args.ctx_dist == "uniform" else ""),
                        "model": "bitnet-b1.58-2B-4T (random init)", "global_batch": B * world, "seq_len": ctx,
                        "parallelism": f"replicas{world}", "weights": "ternary " + ("TQ ~1.6-bit" if wfmt else "I2_S 2-bit"),
-                       "activations": "int8 per-token", "lm_head": "bf16", "kv": "bf16"},
+                       "activations": "int8 per-token", "lm_head": "bf16",
+                       "kv": "bf16, paged (32-token pages)" if paged else "bf16",
+                       **({"ctx_mean": ctx, "ctx_min": int(ctxs.min()), "ctx_max": int(ctxs.max())}
+                          if args.ctx_dist == "uniform" else {})},
             "step_hbm_gbs": round(step_bytes / (ms_step / 1000.0) / 1e9, 1),
             "gemv_hbm_gbs": kern.get("gate_up", {}).get("gbs") if kern else None,
             "roofline": roof, "cpu_baseline": cpu, "kernels": kern,

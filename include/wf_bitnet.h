@@ -167,6 +167,19 @@ typedef struct {
                                      stored transposed per (layer, sequence, kv head): [head_dim, max_seq] */
     int debug_flags;              /* reserved, must be 0 (latency studies use the stamp build,
                                      tools/stamps.py)                                             */
+    /* Paged KV (optional; batched matrix-core decode only: batch >= 16, I2_S weights, head_dim 128,
+     * max_seq % 32 == 0). Replaces the dense per-sequence planes of k_cache / v_cache above with a
+     * shared pool of 32-token pages, the MI355X-native counterpart of sgl_kernel.kvcache's paged
+     * pool (tests/test_kv_cache_cpp.py:283-373) for the attention of SURVEY §8f rank 2:
+     *   k_cache, v_cache : [layers, num_pages, n_kv_heads, 32 * head_dim] bf16, each 32-token page
+     *                      of one kv head in the K / V tile layout of one 32-key block;
+     *   page_table       : [batch, max_seq / 32] int32, page of block t >> 5 of sequence b. It is
+     *                      read by every step (caller-owned, device memory, may change between
+     *                      steps); entries of blocks a step touches must be in [0, num_pages)
+     *                      (out-of-range ids are clamped on the device: wrong keys, never a fault).
+     * page_table == NULL keeps the dense layout. */
+    const int32_t* page_table;
+    int num_pages;
 } wf_model_desc;
 
 typedef struct wf_model wf_model;

@@ -125,6 +125,27 @@ def test_kv_manager_allocation_semantics():
         m.scatter_kv(torch.zeros(1, 16), torch.zeros(1, 16), torch.tensor([0]), None, 0)
 
 
+def test_decoder_page_pool_semantics():
+    """The paged decoder's host allocator follows the same allocation / failure order as
+    KVCacheManager (tests/test_kv_cache_cpp.py:20-73 golden)."""
+    from wfamd.model import PagePool
+    g = load_golden("kv")
+    m = PagePool(10)
+    a = m.allocate_pages(4)
+    m.free_pages(a[1:3])
+    b = m.allocate_pages(3)
+    single = m.allocate_pages(1)
+    too_many = m.allocate_pages(100)
+    assert np.array_equal(a, g["pg_a"]) and np.array_equal(b, g["pg_b"])
+    assert int(single[0]) == int(g["pg_single"]) and too_many.size == int(g["pg_too_many"])
+    assert m.num_free_pages() == int(g["pg_free_after"])
+    m.free_pages([-1, 10])  # ignored
+    assert m.num_free_pages() == int(g["pg_free_after"])
+    s = PagePool(64, seed=3)  # scattered placement: a permutation of the pool
+    ids = s.allocate_pages(64)
+    assert sorted(ids.tolist()) == list(range(64)) and ids.tolist() != list(range(64))
+
+
 def test_model_layout_permutations():
     from wfamd.model import gate_up_interleave, qkv_row_permutation
     p = qkv_row_permutation(3, 128)

@@ -503,6 +503,72 @@ def test_decode_batched_long_ragged_context_matches_single():
         del d1
 
 
+def test_decode_paged_kv_equals_dense():
+    """Paged KV (32-token pages from a shuffled pool, page table per sequence) vs
+    the dense tile-layout planes: the same arithmetic on the same keys, so logits, next tokens and
+    the K/V rows the steps append are bit-identical, over ragged contexts (0..1900, page edges),
+    several graph-replayed steps that cross page boundaries, and a sequence released and
+    re-admitted onto recycled pages."""
+    from wfamd.model import BitNetConfig, BitNetDecoder, from_kv_tiles, synthetic_weights
+    cfg = BitNetConfig(hidden=512, layers=2, n_heads=4, n_kv_heads=1, head_dim=128, inter=768, vocab=1024,
+                       max_seq=2048)
+    w = synthetic_weights(cfg, seed=5)
+    B = 20
+    dense = BitNetDecoder(cfg, w, batch=B)
+    paged = BitNetDecoder(cfg, w, batch=B, num_pages=B * cfg.max_seq // 32 // 2, page_seed=7)
+    assert dense.kv_tiled and paged.paged
+    gen = torch.Generator(device="cuda").manual_seed(13)
+    ctx = 1900
+    pos = [0, 1, 5, 31, 32, 33, 127, 128, 129, 255, 256, 300, 511, 777, 1000, 1023, 1024, 1500, 1899, 1700]
+    for l in range(2):
+        k = torch.randn(B, 1, ctx, 128, generator=gen, device="cuda").to(torch.bfloat16)
+        v = torch.randn(B, 1, ctx, 128, generator=gen, device="cuda").to(torch.bfloat16)
+        for b in range(B):  # keys past a sequence's position are never read: keep them out of the pool
+            k[b, :, pos[b]:] = 0
+            v[b, :, pos[b]:] = 0
+        dense.load_kv(l, k, v)
+        paged.load_kv(l, k[:, :, :max(pos)], v[:, :, :max(pos)], lengths=pos)
+    steps = 6
+    for b in range(B):
+        paged.reserve(b, pos[b] + steps + 3)
+    assert paged.pool.num_free_pages() < paged.pool.num_pages
+    toks = [(37 * b + 5) % cfg.vocab for b in range(B)]
+    for dec in (dense, paged):
+        dec.set_state(toks, pos)
+    for i in range(steps):
+        dense.step(graph=True)
+        paged.step(graph=True)
+        torch.cuda.synchronize()
+        assert torch.equal(dense.logits.view(torch.int16), paged.logits.view(torch.int16)), i
+        assert torch.equal(dense.tokens, paged.tokens) and torch.equal(dense.positions, paged.positions)
+    # the appended rows sit in the right pages: compare every sequence's K/V through the page table
+    for l in range(2):
+        kd, vd = from_kv_tiles(dense.k_cache[l], dense.v_cache[l])
+        for b in (0, 3, 4, 5, 8, 17, 18):
+            n = pos[b] + steps
+            nblk = (n + 31) // 32
+            ids = torch.from_numpy(paged.seq_pages[b][:nblk].astype(np.int64)).cuda()
+            kt = paged.k_cache[l].index_select(0, ids).transpose(0, 1).reshape(1, nblk * 32, 128)
+            vt = paged.v_cache[l].index_select(0, ids).transpose(0, 1).reshape(1, nblk * 32, 128)
+            kp, vp = from_kv_tiles(kt, vt)
+            assert torch.equal(kp[:, :n], kd[b, :, :n]) and torch.equal(vp[:, :n], vd[b, :, :n]), (l, b)
+    # release + re-admit sequence 3 at position 0 on recycled pages: it decodes like a fresh dense row
+    free0 = paged.pool.num_free_pages()
+    paged.release(3)
+    assert paged.pool.num_free_pages() > free0
+    paged.reserve(3, 40)
+    t3 = int(dense.tokens[3])
+    for dec in (dense, paged):
+        p = dec.positions.clone()
+        p[3] = 0
+        dec.positions.copy_(p)
+    for i in range(3):
+        dense.step(graph=True)
+        paged.step(graph=True)
+    torch.cuda.synchronize()
+    assert torch.equal(dense.logits[3].view(torch.int16), paged.logits[3].view(torch.int16)), t3
+
+
 def test_mfma_tile_format_roundtrip_and_gemv(orc):
     """WF_FMT_I2S_MFMA is a bijection of I2_S (device repack both ways; include/wf_bitnet.h layout)."""
     from wfamd import ops

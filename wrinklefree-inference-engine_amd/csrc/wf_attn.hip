@@ -482,7 +482,8 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
                                                    const uint16_t* __restrict__ K, const uint16_t* __restrict__ Vt,
                                                    int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv, int S,
                                                    const int32_t* __restrict__ seq_lens, float sm_scale,
-                                                   float2* __restrict__ ml_out, float* __restrict__ o_out) {
+                                                   float2* __restrict__ ml_out, float* __restrict__ o_out,
+                                                   const int32_t* __restrict__ pt, int pps, int npages, int64_t kv_pgs) {
     constexpr int D = 128;
     const int s = blockIdx.x, g = blockIdx.y, b = blockIdx.z;
     const int grp = Hq / Hkv, hq0 = g * grp;
@@ -496,8 +497,11 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
     const int t1 = RR ? Sb : min(s * T + T, Sb);
     __shared__ float sm_m[4][kAttnMfmaMaxGrp], sm_l[4][kAttnMfmaMaxGrp];
     __shared__ __attribute__((aligned(16))) float sm_o[4][kAttnMfmaMaxGrp][D];
+    // dense: (sequence, kv head) slab of S / 32 blocks; paged: block j of sequence b in page
+    // pt[b][j] (kv_sb = 0, kv_sh = the kv head stride inside a page)
     const uint16_t* Kb = K + b * kv_sb + g * kv_sh + lane * 8;
     const uint16_t* Vb = Vt + b * kv_sb + g * kv_sh + lane * 8;
+    const int32_t* ptb = pt ? pt + (int64_t)b * pps : nullptr;
     WF_STAMP(0);
 
     float m_run = -INFINITY, l_run = 0.f;
@@ -517,7 +521,9 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
             }
         }
         auto load = [&](uint4 (&kr)[2][4], uint4 (&vr)[8], int bs) {
-            const int64_t blk = (int64_t)(bs >> 5) * 4096;  // 32 keys x 128 dims per tile block
+            // 32 keys x 128 dims per tile block (bs is wave-uniform: the page id is a scalar load)
+            const int64_t blk = ptb ? (int64_t)min(max(ptb[__builtin_amdgcn_readfirstlane(bs) >> 5], 0), npages - 1) * kv_pgs
+                                    : (int64_t)(bs >> 5) * 4096;
 #pragma unroll
             for (int tau = 0; tau < 2; ++tau)
 #pragma unroll
@@ -635,7 +641,8 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
 
 int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
-                              float2* ml, float* o, hipStream_t st, bool kv_tiled) {
+                              float2* ml, float* o, hipStream_t st, bool kv_tiled, const int32_t* pt, int pps,
+                              int npages, int64_t kv_pgs) {
     const int grp = Hq / Hkv;
     if (grp > 8) {
         set_error("decode_attention_partials: GQA group %d > 8", grp);
@@ -659,13 +666,13 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
         static const int variant = getenv("WF_ATTN_VARIANT") ? atoi(getenv("WF_ATTN_VARIANT")) : 0;
         if (variant == 1)
             hipLaunchKernelGGL((k_attn_mfma<false, true>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv,
-                               S, seq_lens, sm_scale, ml, o);
+                               S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs);
         else if (variant == 2)
             hipLaunchKernelGGL((k_attn_mfma<true, false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv,
-                               S, seq_lens, sm_scale, ml, o);
+                               S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs);
         else
             hipLaunchKernelGGL((k_attn_mfma<false, false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq,
-                               Hkv, S, seq_lens, sm_scale, ml, o);
+                               Hkv, S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs);
         return check_launch("decode_attention_partials");
     }
 #define WF_AP(GV)                                                                                                   \

@@ -29,7 +29,8 @@
 namespace wf {
 int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
-                              float2* ml, float* o, hipStream_t st, bool kv_tiled);
+                              float2* ml, float* o, hipStream_t st, bool kv_tiled, const int32_t* pt = nullptr,
+                              int pps = 0, int npages = 0, int64_t kv_pgs = 0);
 
 enum { MODE_QKV = 0, MODE_O = 1, MODE_GU = 2, MODE_DN = 3, MODE_LINEAR = 4 };  // LINEAR: BitNetLinear drop-in
 constexpr int kNT = 512;  // threads per GEMV / row-norm block (8 waves: 2 per SIMD hide the input-stage latency)
@@ -66,6 +67,11 @@ struct GemvArgs {
     uint16_t* vc;
     int64_t kv_b_stride;
     int kv_t;  // K/V caches in the matrix-core tile layouts (wf_attn.hip kv_tile_off; batched decode)
+    // paged K/V (kv_t only): page of block t >> 5 of sequence m = pt[m * pps + (t >> 5)], page
+    // stride kv_pgs elements, kv head stride 32 * 128 inside a page
+    const int32_t* pt;
+    int pps, npages;
+    int64_t kv_pgs;
 };
 
 // Reference correction (direct_inference_full.py:201-208) for one output:
@@ -417,6 +423,12 @@ struct EpiDec {
                         g.out[(int64_t)m * g.out_stride + head * 128 + d] = f2bf(y);
                     } else {
                         const int kvh = head - g.Hq - (proj == 2 ? g.Hkv : 0);
+                        if (g.pt) {  // paged: block pos >> 5 lives in page pt[m][pos >> 5]
+                            const int pg = min(max(g.pt[(int64_t)m * g.pps + (pos >> 5)], 0), g.npages - 1);
+                            uint16_t* cache = (proj == 1 ? g.kc : g.vc) + pg * g.kv_pgs + (int64_t)kvh * 4096;
+                            cache[proj == 1 ? k_tile_off(pos & 31, d) : v_tile_off(pos & 31, d)] = f2bf(y);
+                            continue;
+                        }
                         uint16_t* cache = (proj == 1 ? g.kc : g.vc) + (int64_t)m * g.kv_b_stride + (int64_t)kvh * g.S * 128;
                         if (g.kv_t) cache[proj == 1 ? k_tile_off(pos, d) : v_tile_off(pos, d)] = f2bf(y);
                         else cache[(int64_t)pos * 128 + d] = f2bf(y);
@@ -1234,7 +1246,12 @@ GemvArgs base_args(const wf_model* m, int l) {
     a.ws_ints = m->dec_ws_ints;
     a.rope_cos = d.rope_cos;
     a.rope_sin = d.rope_sin;
-    const int64_t kvl = (int64_t)d.batch * d.n_kv_heads * d.max_seq * d.head_dim;
+    const int64_t kvl = d.page_table ? (int64_t)d.num_pages * d.n_kv_heads * 32 * d.head_dim
+                                     : (int64_t)d.batch * d.n_kv_heads * d.max_seq * d.head_dim;
+    a.pt = d.page_table;
+    a.pps = d.max_seq / 32;
+    a.npages = d.num_pages;
+    a.kv_pgs = (int64_t)d.n_kv_heads * 32 * d.head_dim;
     a.kc = m->k_cache + l * kvl;
     a.vc = m->v_cache + l * kvl;
     a.kv_b_stride = (int64_t)d.n_kv_heads * d.max_seq * d.head_dim;
@@ -1273,6 +1290,10 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             if ((rc = gemv_input(m, a, m->h_a, H, d.ln_in + (int64_t)l * H, st))) return rc;
             return launch_gemv_fmt<MODE_QKV, kLprQKV>(d.wfmt, a, st);
         case WF_OP_ATTN:  // split partials; merged by the O projection's input stage
+            if (a.pt)  // paged pool: kv head stride 32 * D inside a page
+                return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, 0, 32 * D, B, d.n_heads,
+                                                 d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D), m->part_ml,
+                                                 m->part_o, st, true, a.pt, a.pps, a.npages, a.kv_pgs);
             return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, a.kv_b_stride, (int64_t)S * D,
                                              B, d.n_heads, d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D),
                                              m->part_ml, m->part_o, st, m->kv_tiled != 0);
@@ -1394,6 +1415,12 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_ALLOC(m->h_b, 2 * (size_t)B * d.hidden);
     WF_ALLOC(m->qbuf, 2 * (size_t)B * d.hidden);
     m->kv_tiled = (B >= kDecMfmaMinB && (d.wfmt == WF_FMT_I2S || d.wfmt == WF_FMT_I2S_MFMA) && d.max_seq % 32 == 0) ? 1 : 0;
+    if (d.page_table && !(m->kv_tiled && d.head_dim == 128 && d.num_pages >= 1)) {
+        set_error("model_create: paged KV needs batch >= %d, I2_S weights, head_dim 128, max_seq %% 32 == 0 and "
+                  "num_pages >= 1", kDecMfmaMinB);
+        wf_model_destroy(m);
+        return WF_EINVAL;
+    }
     if (B >= kDecMfmaMinB && d.wfmt == WF_FMT_I2S) {
         const int shapes[4][2] = {{m->qkv_rows, d.hidden}, {d.hidden, d.hidden}, {2 * d.inter, d.hidden}, {d.hidden, d.inter}};
         for (auto& sh : shapes)

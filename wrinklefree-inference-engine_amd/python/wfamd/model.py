@@ -189,11 +189,46 @@ def from_kv_tiles(kt: torch.Tensor, vt: torch.Tensor):
     return k.reshape(*lead, S, D).contiguous(), v.reshape(*lead, S, D).contiguous()
 
 
+class PagePool:
+    """Host-side free list of KV pages, with the semantics of sgl_kernel.kvcache.KVCacheManager's
+    allocator (tests/test_kv_cache_cpp.py:283-373: allocate_pages(n) -> int32 ids, empty when the
+    pool is short; free_pages(ids); num_free_pages()). Pages here hold 32 tokens of every kv head
+    of every layer (the tile block of the batched attention); ids index the pool dimension of the
+    decoder's k_cache / v_cache."""
+
+    def __init__(self, num_pages: int, seed: Optional[int] = None):
+        self.num_pages = int(num_pages)
+        order = np.arange(self.num_pages, dtype=np.int32)
+        if seed is not None:  # scattered placement (a long-running server's pool), not id order
+            np.random.default_rng(seed).shuffle(order)
+        self._free = list(order[::-1])
+
+    def num_free_pages(self) -> int:
+        return len(self._free)
+
+    def allocate_pages(self, n: int) -> np.ndarray:
+        if n > len(self._free):
+            return np.zeros(0, dtype=np.int32)
+        out = [self._free.pop() for _ in range(n)]
+        return np.asarray(out, dtype=np.int32)
+
+    def free_pages(self, ids) -> None:
+        for i in np.asarray(ids, dtype=np.int64).reshape(-1):
+            if 0 <= i < self.num_pages:  # out-of-range ids are ignored, as the reference twin's free_page (:66-69)
+                self._free.append(int(i))
+
+
 class BitNetDecoder:
-    """Owns the device layout, the caller-side state tensors and the wf_model handle."""
+    """Owns the device layout, the caller-side state tensors and the wf_model handle.
+
+    num_pages > 0 (batch >= 16, I2_S): paged KV. k_cache / v_cache become a pool of 32-token pages
+    [layers, num_pages, n_kv_heads, 32 * head_dim] and `page_table` [batch, max_seq / 32] maps each
+    sequence's 32-token blocks to pages (include/wf_bitnet.h wf_model_desc.page_table); `reserve`
+    / `release` grow and free a sequence's pages from `pool` between steps."""
 
     def __init__(self, cfg: BitNetConfig, weights: Dict[str, torch.Tensor], batch: int = 1,
-                 wfmt: int = WF_FMT_I2S, device="cuda", debug_flags: int = 0):
+                 wfmt: int = WF_FMT_I2S, device="cuda", debug_flags: int = 0, num_pages: int = 0,
+                 page_seed: Optional[int] = None):
         self.cfg, self.batch, self.wfmt = cfg, batch, wfmt
         self.dev = torch.device(device)
         # batch >= 16 on I2_S runs the matrix-core GEMMs on their tile layout (same bytes, re-tiled)
@@ -215,7 +250,17 @@ class BitNetDecoder:
         # batch >= 16 on I2_S (the matrix-core decode path) keeps K and V in the tile layouts of
         # include/wf_bitnet.h (wf_model_desc.k_cache); to_kv_tiles / from_kv_tiles convert
         self.kv_tiled = batch >= 16 and wfmt in (WF_FMT_I2S, WF_FMT_I2S_MFMA) and cfg.max_seq % 32 == 0
-        kv_shape = (L, B, cfg.n_kv_heads, cfg.max_seq, cfg.head_dim)
+        self.paged = num_pages > 0
+        if self.paged:
+            if not (self.kv_tiled and cfg.head_dim == 128):
+                raise ValueError("paged KV needs batch >= 16, I2_S weights, head_dim 128 and max_seq % 32 == 0")
+            kv_shape = (L, num_pages, cfg.n_kv_heads, 32 * cfg.head_dim)
+            self.pool = PagePool(num_pages, page_seed)
+            self.seq_pages = [np.zeros(0, dtype=np.int32) for _ in range(B)]
+            self._pt_host = np.zeros((B, cfg.max_seq // 32), dtype=np.int32)
+            self.page_table = torch.zeros((B, cfg.max_seq // 32), dtype=torch.int32, device=self.dev)
+        else:
+            kv_shape = (L, B, cfg.n_kv_heads, cfg.max_seq, cfg.head_dim)
         self.k_cache = torch.zeros(kv_shape, dtype=torch.bfloat16, device=self.dev)
         self.v_cache = torch.zeros(kv_shape, dtype=torch.bfloat16, device=self.dev)
         d = WFModelDesc()
@@ -231,6 +276,8 @@ class BitNetDecoder:
         d.tokens, d.positions, d.logits = self.tokens.data_ptr(), self.positions.data_ptr(), self.logits.data_ptr()
         d.k_cache, d.v_cache = self.k_cache.data_ptr(), self.v_cache.data_ptr()
         d.debug_flags = int(debug_flags)
+        if self.paged:
+            d.page_table, d.num_pages = self.page_table.data_ptr(), int(num_pages)
         self._desc = d
         h = C.c_void_p()
         call("wf_model_create", C.addressof(d), C.addressof(h))
@@ -244,6 +291,27 @@ class BitNetDecoder:
         except Exception:
             pass
 
+    def reserve(self, b: int, n_tokens: int) -> None:
+        """Give sequence b pages for positions [0, n_tokens) (allocating only the missing blocks)."""
+        need = (int(n_tokens) + 31) // 32 - len(self.seq_pages[b])
+        if need <= 0:
+            return
+        if need + len(self.seq_pages[b]) > self._pt_host.shape[1]:
+            raise ValueError(f"sequence {b}: {n_tokens} tokens exceed max_seq {self.cfg.max_seq}")
+        got = self.pool.allocate_pages(need)
+        if len(got) != need:
+            raise RuntimeError(f"KV page pool exhausted ({self.pool.num_free_pages()} free, {need} needed)")
+        self.seq_pages[b] = np.concatenate([self.seq_pages[b], got])
+        self._pt_host[b, :len(self.seq_pages[b])] = self.seq_pages[b]
+        self.page_table[b].copy_(torch.from_numpy(self._pt_host[b]))
+
+    def release(self, b: int) -> None:
+        """Return sequence b's pages to the pool (a finished request)."""
+        self.pool.free_pages(self.seq_pages[b])
+        self.seq_pages[b] = np.zeros(0, dtype=np.int32)
+        self._pt_host[b] = 0
+        self.page_table[b].zero_()
+
     def set_state(self, tokens, positions) -> None:
         self.tokens.copy_(torch.as_tensor(tokens, dtype=torch.int32))
         self.positions.copy_(torch.as_tensor(positions, dtype=torch.int32))
@@ -255,15 +323,35 @@ class BitNetDecoder:
         D = self.cfg.head_dim
         for l in range(self.cfg.layers):
             for c in (self.k_cache, self.v_cache):
-                if self.kv_tiled:
+                if self.paged:
+                    c[l].normal_(generator=g)
+                elif self.kv_tiled:
                     B, H, S, _ = c[l].shape
                     c[l].view(B, H, S * D)[..., :(ctx + 31) // 32 * 32 * D].normal_(generator=g)
                 else:
                     c[l, :, :, :ctx].normal_(generator=g)
 
-    def load_kv(self, layer: int, k: torch.Tensor, v: torch.Tensor) -> None:
-        """Write logical K/V [B, Hkv, n, D] into positions [0, n) of a layer (any storage layout)."""
+    def load_kv(self, layer: int, k: torch.Tensor, v: torch.Tensor, lengths=None) -> None:
+        """Write logical K/V [B, Hkv, n, D] into positions [0, n) of a layer (any storage layout).
+        Paged: only the first lengths[b] (default n) positions of sequence b, on pages reserved for them."""
         n = k.shape[2]
+        if self.paged:
+            B, H, _, D = k.shape
+            nblk = (n + 31) // 32
+            kp = torch.zeros(B, H, nblk * 32, D, dtype=torch.bfloat16, device=self.dev)
+            vp = torch.zeros_like(kp)
+            kp[:, :, :n].copy_(k)
+            vp[:, :, :n].copy_(v)
+            kt, vt = to_kv_tiles(kp, vp)
+            for b in range(B):
+                nb = (min(n, int(lengths[b]) if lengths is not None else n) + 31) // 32
+                if nb == 0:
+                    continue
+                self.reserve(b, 32 * nb)
+                ids = torch.from_numpy(self.seq_pages[b][:nb].astype(np.int64)).to(self.dev)
+                self.k_cache[layer].index_copy_(0, ids, kt[b].reshape(H, nblk, 32 * D)[:, :nb].transpose(0, 1))
+                self.v_cache[layer].index_copy_(0, ids, vt[b].reshape(H, nblk, 32 * D)[:, :nb].transpose(0, 1))
+            return
         if not self.kv_tiled:
             self.k_cache[layer, :, :, :n].copy_(k)
             self.v_cache[layer, :, :, :n].copy_(v)
