@@ -48,6 +48,7 @@ def parse():
                     help="uniform: per-sequence contexts drawn from U[1, max_seq - steps) with seed 0 (SURVEY §8d "
                          "config 4), on paged KV")
     ap.add_argument("--paged", action="store_true", help="paged KV (32-token pages; batch >= 16)")
+    ap.add_argument("--no-gemv", action="store_true", help="skip the standalone GEMV benchmark")
     return ap.parse_args()
 
 
@@ -95,6 +96,73 @@ def op_timing(dec, ctx, reps: int = 5):
         res[name] = {"us": round(us, 3), "bytes": nbytes, "gbs": round(nbytes / us / 1e3, 1),
                      "launches_per_step": per_tok, "us_per_step": round(us * per_tok, 2)}
     return res
+
+
+GEMV_SHAPES = [("q_proj/o_proj", 2560, 2560), ("k_proj/v_proj", 640, 2560), ("gate/up", 6912, 2560),
+               ("down", 2560, 6912)]  # (N, K): scripts/benchmark_kernels.py:132-138 plus k/v
+
+
+def gemv_bench(rotate_bytes: float = 1.2e9, reps: int = 3):
+    """The reference's kernel benchmark (scripts/benchmark_kernels.py:40-66) on the GPU: one
+    sgl_kernel bitnet_gemv call (C-ABI wf_bitnet_gemv, raw enc-sum GEMV + scale, output
+    preallocated) per launch, random ternary I2_S weights, int8 activations. The launches of one
+    timed replay rotate through >= 1.2 GB of distinct weight buffers (SURVEY §8d cache hygiene: the
+    256 MB Infinity Cache cannot serve them), captured in a HIP graph (no host gaps); per-call µs =
+    replay time / calls, GB/s = (W_bytes + K + 4N) / µs as benchmark_kernels.py:61-66."""
+    import torch
+    from wfamd import _lib
+    lib = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    st = torch.cuda.current_stream()
+    out = {}
+    for name, N, K in GEMV_SHAPES:
+        wb = N * K // 4
+        nbuf = max(8, int(rotate_bytes // wb) + 1)
+        w = torch.randint(0, 255, (nbuf, N, K // 4), dtype=torch.uint8, device="cuda", generator=g)
+        w &= 0xAA  # every 2-bit field in {0, 2}: valid enc codes (w = -1 / +1)
+        a = torch.randint(-128, 128, (K,), dtype=torch.int8, device="cuda", generator=g)
+        y = torch.empty(N, dtype=torch.float32, device="cuda")
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            cs = torch.cuda.current_stream().cuda_stream
+            for i in range(nbuf):
+                _lib.check(lib.wf_bitnet_gemv(w[i].data_ptr(), a.data_ptr(), 0.01, N, K, y.data_ptr(), cs), "gemv")
+        graph.replay()
+        times = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            graph.replay()
+            e1.record(st)
+            torch.cuda.synchronize()
+            times.append(1000.0 * e0.elapsed_time(e1) / nbuf)
+        us = sorted(times)[len(times) // 2]
+        nbytes = wb + K + 4 * N
+        out[name] = {"N": N, "K": K, "us": round(us, 3), "bytes": nbytes, "gbs": round(nbytes / us / 1e3, 1),
+                     "calls_per_replay": nbuf}
+        del w, graph
+        torch.cuda.empty_cache()
+    return out
+
+
+def cpu_gemv(seconds_per_shape: float = 1.5):
+    """The oracle's I2_S GEMV (oracle/wf_oracle.c, OpenMP) on the same shapes on the host cores."""
+    import numpy as np
+    from oracle import oracle as orc
+    rng = np.random.default_rng(0)
+    out = {}
+    for name, N, K in GEMV_SHAPES:
+        p = (rng.integers(0, 256, size=(N, K // 4), dtype=np.uint8) & 0xAA).astype(np.uint8)
+        a = rng.integers(-128, 128, size=K, dtype=np.int8)
+        orc.gemv_i2s(p, a, 0.01)
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds_per_shape:
+            orc.gemv_i2s(p, a, 0.01)
+            n += 1
+        us = 1e6 * (time.perf_counter() - t0) / n
+        nbytes = N * K // 4 + K + 4 * N
+        out[name] = {"us": round(us, 1), "gbs": round(nbytes / us / 1e3, 2)}
+    return out
 
 
 def cpu_baseline(ctx: int, seconds: float):
@@ -221,9 +289,14 @@ def main():
                 "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom_name,
                 "bytes_per_launch": dom["bytes"], "us_per_launch": dom["us"]}
     step_bytes = cfg.weight_bytes_per_token(wfmt) + B * cfg.kv_bytes_per_token(ctx + total // 2)
+    gemv = None if (args.no_gemv or B != 1) else gemv_bench()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(ctx, args.cpu_seconds)
+        if gemv:
+            cg = cpu_gemv()
+            for k, v in cg.items():
+                gemv[k]["cpu_us"], gemv[k]["cpu_gbs"] = v["us"], v["gbs"]
 
     if rank == 0:
         line = {
@@ -242,6 +315,7 @@ def main():
                           if args.ctx_dist == "uniform" else {})},
             "step_hbm_gbs": round(step_bytes / (ms_step / 1000.0) / 1e9, 1),
             "gemv_hbm_gbs": kern.get("gate_up", {}).get("gbs") if kern else None,
+            "gemv": gemv,
             "roofline": roof, "cpu_baseline": cpu, "kernels": kern,
         }
         print(json.dumps(line))
