@@ -92,6 +92,16 @@ int64_t wf_tq_row_bytes(int K);
 /* I2_S <-> WF_FMT_I2S_MFMA (bijection; N % 16 == 0, K % 128 == 0). */
 int wf_i2s_to_mfma(const uint8_t* i2s, int N, int K, uint8_t* out, void* stream);
 int wf_mfma_to_i2s(const uint8_t* mf, int N, int K, uint8_t* i2s, void* stream);
+/* int8 activation codes [M][lda] -> the matrix-core tile order the batched decode step's row
+ * quantizer writes: per (16-row tile rt, I2_S block kb, half h) one KiB, lane l16 + 16q holding
+ * the codes of row 16rt + l16 at k = 128kb + 16h + 4q + jj + 32g in byte 4g + jj (csrc/wf_norm.h
+ * tile_code_pos). out holds ceil(M/16)*16*K bytes; rows >= M are zero. K % 128 == 0. */
+int wf_codes_to_tiles(const int8_t* a, int64_t lda, int M, int K, int8_t* out, void* stream);
+/* bitnet_gemm (the sgl_kernel contract above: Y = float(sum enc(W) * A) * scale, fp32 out) for
+ * prefill-sized M on the matrix-core tile layouts: w in WF_FMT_I2S_MFMA, a from wf_codes_to_tiles.
+ * Bit-identical to wf_bitnet_gemm on the same logical operands. K % 128 == 0, N % 16 == 0. */
+int wf_bitnet_gemm_tiled(const uint8_t* w, const int8_t* a, float scale, int M, int N, int K, float* y, int64_t ldy,
+                         void* stream);
 
 /* ---- KV cache ----------------------------------------------------- */
 /* sgl_kernel.kvcache.KVCacheManager.scatter_kv / gather_kv (tests/test_kv_cache_cpp.py:283-373;

@@ -569,6 +569,24 @@ def test_decode_paged_kv_equals_dense():
     assert torch.equal(dense.logits[3].view(torch.int16), paged.logits[3].view(torch.int16)), t3
 
 
+@pytest.mark.parametrize("m,n,k", [(16, 16, 128), (130, 272, 384), (300, 3840, 2560), (513, 2560, 6912),
+                                   (1024, 13824, 2560)])
+def test_prefill_gemm_tiled_vs_oracle(orc, m, n, k):
+    """wf_bitnet_gemm_tiled (tile-layout prefill GEMM, XCD-grouped 128 x 256 tiles) is bit-exact with
+    the oracle's raw enc-sum GEMM and with wf_bitnet_gemm on the same operands, over ragged M / N
+    tails (partial row and column blocks) and the 2B-4T layer shapes."""
+    from wfamd import ops
+    rng = np.random.default_rng(m + n + k)
+    c = rng.integers(0, 3, size=(n, k // 4, 4)).astype(np.uint8)  # enc codes in {0, 1, 2}
+    p = (c[..., 0] << 6) | (c[..., 1] << 4) | (c[..., 2] << 2) | c[..., 3]
+    a = rng.integers(-128, 128, size=(m, k)).astype(np.int8)
+    at = ops.codes_to_tiles(cu(a))
+    y = ops.bitnet_gemm_tiled(ops.i2s_to_mfma(cu(p)), at, 0.37, m).cpu().numpy()
+    rows = slice(None) if m * n * k < 2e9 else slice(0, 64)
+    assert np.array_equal(y[rows], orc.gemm_i2s(p, a[rows], 0.37))
+    assert np.array_equal(y, ops.bitnet_gemm(cu(p), cu(a), 0.37).cpu().numpy())
+
+
 def test_mfma_tile_format_roundtrip_and_gemv(orc):
     """WF_FMT_I2S_MFMA is a bijection of I2_S (device repack both ways; include/wf_bitnet.h layout)."""
     from wfamd import ops

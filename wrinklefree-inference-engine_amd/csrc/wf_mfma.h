@@ -38,6 +38,19 @@ __device__ __forceinline__ void glds16(const void* g, void* lds) {
                                      16, 0, 0);
 }
 
+// The same LDS-DMA as inline asm: hipcc does not see it write LDS, so it does not put a
+// `s_waitcnt vmcnt(0)` in front of every ds_read that might alias the DMA destination (with the
+// builtin it does, which drains the whole ring before each stage's fragment reads). The caller
+// counts completion with its own vmcnt + barrier (cdna_hip_programming.md, LDS-DMA recipe).
+__device__ __forceinline__ void glds16_asm(const void* g, const void* lds) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(lds));
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(dst)
+                 : "memory");
+}
+
 // Epi::apply(i_tile_row0, j_tile_col0, acc, l16, q): called once per 16x16 output tile with its
 // first row / column; lane holds D[row0 + 4q + r][col0 + l16], r < 4. k-steps [c_begin, c_end)
 // (a split-K slice; the whole K is [0, K/64)).

@@ -42,6 +42,8 @@ SIGNATURES = {
     "wf_tq_row_bytes": (i64, [i32]),
     "wf_i2s_to_mfma": (i32, [vp, i32, i32, vp, vp]),
     "wf_mfma_to_i2s": (i32, [vp, i32, i32, vp, vp]),
+    "wf_codes_to_tiles": (i32, [vp, i64, i32, i32, vp, vp]),
+    "wf_bitnet_gemm_tiled": (i32, [vp, vp, f32, i32, i32, i32, vp, i64, vp]),
     "wf_kv_scatter": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp]),
     "wf_kv_gather": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp]),
     "wf_kv_quant_i8": (i32, [vp, i32, i64, vp, vp, vp]),

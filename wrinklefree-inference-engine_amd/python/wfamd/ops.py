@@ -233,6 +233,25 @@ def i2s_to_mfma(i2s: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def codes_to_tiles(a: torch.Tensor) -> torch.Tensor:
+    """int8 codes [M, K] -> matrix-core tile order (include/wf_bitnet.h wf_codes_to_tiles), flat
+    int8 tensor of ceil(M/16)*16*K bytes."""
+    a = _on_device(a).contiguous()
+    m, k = a.shape
+    out = torch.empty((m + 15) // 16 * 16 * k, dtype=torch.int8, device=a.device)
+    call("wf_codes_to_tiles", a.data_ptr(), k, m, k, out.data_ptr(), _stream())
+    return out
+
+
+def bitnet_gemm_tiled(w_mfma: torch.Tensor, a_tiles: torch.Tensor, scale: float, m: int) -> torch.Tensor:
+    """Prefill GEMM on tile layouts (wf_bitnet_gemm_tiled): float32 [m, N]."""
+    n, k4 = w_mfma.shape
+    y = torch.empty(m, n, dtype=torch.float32, device=w_mfma.device)
+    call("wf_bitnet_gemm_tiled", w_mfma.data_ptr(), a_tiles.data_ptr(), float(scale), m, n, 4 * k4, y.data_ptr(), n,
+         _stream())
+    return y
+
+
 def mfma_to_i2s(mf: torch.Tensor) -> torch.Tensor:
     w = _on_device(mf).contiguous()
     n, k4 = w.shape
