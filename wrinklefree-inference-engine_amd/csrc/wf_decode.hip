@@ -772,9 +772,9 @@ __global__ __launch_bounds__(256) void k_lm_head_mfma(const uint16_t* __restrict
     auto issue = [&](int c) {
         uint8_t* st = lds + (c % P) * kLmStageBytes;
 #pragma unroll
-        for (int u = 0; u < 2; ++u) glds16(asrc[u] + 512 * c, st + (2 * wave + u) * 1024);
+        for (int u = 0; u < 2; ++u) glds16_asm(asrc[u] + 512 * c, st + (2 * wave + u) * 1024);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) glds16(bsrc[j] + 512 * c, st + 8192 + wave * 4096 + j * 1024);
+        for (int j = 0; j < 4; ++j) glds16_asm(bsrc[j] + 512 * c, st + 8192 + wave * 4096 + j * 1024);
     };
     v4f_t acc[8][4];
 #pragma unroll

@@ -76,8 +76,8 @@ __device__ __forceinline__ void tgemm_tile(const uint8_t* __restrict__ W, const 
         const int c = c_begin + cl;
         const int koff = 128 * (c >> 1) + 16 * (c & 1), boff = 32 * (c >> 1) + 16 * (c & 1);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) glds16(asrc[u] + koff, st + (2 * wave + u) * 1024);
-        glds16(bsrc + boff, st + 8192 + wave * 1024);
+        for (int u = 0; u < 2; ++u) glds16_asm(asrc[u] + koff, st + (2 * wave + u) * 1024);
+        glds16_asm(bsrc + boff, st + 8192 + wave * 1024);
     };
 
     v4i_t acc[TM][TN];
