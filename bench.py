@@ -280,7 +280,8 @@ def main():
         dom = kern[dom_name]
         traffic = None
         pmc = ROOT / "profiles" / ("pmc_traffic.json" if B < 16 else f"pmc_traffic_b{B}.json")
-        if pmc.exists():
+        # the PMC files are measured on the fixed-context workload (tools/profile_round.sh)
+        if pmc.exists() and args.ctx_dist == "fixed":
             try:
                 traffic = json.loads(pmc.read_text()).get(dom_name, {}).get("hbm_bytes_per_launch")
             except Exception:

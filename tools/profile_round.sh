@@ -23,19 +23,24 @@ tail -1 "$O/bench_b1.log" | cut -c1-200
 step bench-b128
 timeout -k 10 600 python bench.py --batch 128 --steps 100 --warmup 10 --no-cpu-baseline > "$O/bench_b128.log" 2>&1 || exit $?
 tail -1 "$O/bench_b128.log" | cut -c1-200
+step bench-b128-uniform-paged
+timeout -k 10 600 python bench.py --batch 128 --steps 100 --warmup 10 --no-cpu-baseline --ctx-dist uniform > "$O/bench_b128u.log" 2>&1 || exit $?
+tail -1 "$O/bench_b128u.log" | cut -c1-200
 for B in 1 128; do
     step "rocprof b$B"
     cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof_b$B" -o run -- \
-        python3 "$R/bench.py" --batch $B --steps 100 --warmup 10 --no-cpu-baseline > "$O/prof_b$B.log" 2>&1 || exit $?
+        python3 "$R/bench.py" --batch $B --steps 100 --warmup 10 --no-cpu-baseline --no-gemv > "$O/prof_b$B.log" 2>&1 || exit $?
     cd "$R" && python3 tools/prof_summary.py "$O/prof_b$B" > "$O/kernel_stats_b$B.txt" 2>&1 || exit $?
     for C in FETCH_SIZE WRITE_SIZE; do
         step "pmc $C b$B"
         cd /tmp && timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$O/pmc_${C}_b$B" -o run -- \
-            python3 "$R/bench.py" --batch $B --steps 20 --warmup 5 --no-cpu-baseline --no-op-timing > "$O/pmc_${C}_b$B.log" 2>&1 || exit $?
+            python3 "$R/bench.py" --batch $B --steps 20 --warmup 5 --no-cpu-baseline --no-op-timing --no-gemv > "$O/pmc_${C}_b$B.log" 2>&1 || exit $?
         cd "$R"
     done
 done
 step prefill
 timeout -k 10 300 python tools/prefill_gemm_bench.py > "$O/prefill.log" 2>&1 || exit $?
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_prefill" -o run -- python3 "$R/tools/prefill_gemm_bench.py" --iters 10 > "$O/prof_prefill.log" 2>&1 || exit $?
+cd "$R" && python3 tools/prof_summary.py "$O/prof_prefill" > "$O/kernel_stats_prefill.txt" 2>&1 || exit $?
 tail -1 "$O/prefill.log"
 echo "== done"
