@@ -87,6 +87,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--warm", action="store_true",
                     help="launch the same op of layer-1 right before (code and inputs warm, weights cold)")
+    ap.add_argument("--hot", action="store_true",
+                    help="launch the same op of the SAME layer right before (weights in L2 / Infinity Cache)")
     args = ap.parse_args()
     lib = _lib.load()
     for fn in ("wf_debug_stamps_decode", "wf_debug_stamps_attn"):
@@ -120,6 +122,8 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             if args.warm:
                 dec.launch_op(args.layer - 1, op)
+            if args.hot:
+                dec.launch_op(args.layer, op)
             e0.record()
             dec.launch_op(args.layer, op)
             e1.record()

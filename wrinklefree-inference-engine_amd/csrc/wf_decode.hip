@@ -572,11 +572,11 @@ __global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm(GemvArgs a) {
 // wave-instruction, whatever the bytes used). Lane (l16, q), block kb, half h: A = 16 codes of
 // k = 128 kb + 16 h + 4 q + jj + 32 g at [4g + jj]; B dword h = I2_S bytes [32 kb + 16 h + 4 q, +4)
 // of its column, decoded into the 4 groups g by shift 6 - 2g -- the same k for both operands.
-template <int TMT, int TNT, int NB, int MODE>
-__global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm_t(GemvArgs a) {
-    constexpr int EPT = TMT * TNT / kDgWaves;  // epilogue tiles per wave
-    static_assert(EPT * kDgWaves == TMT * TNT, "whole epilogue tiles per wave");
-    __shared__ v4i_t red[kDgWaves][TMT * TNT][64];
+template <int TMT, int TNT, int NB, int MODE, int NW = kDgWaves>
+__global__ __launch_bounds__(NW * 64) void k_dec_gemm_t(GemvArgs a) {
+    constexpr int EPT = TMT * TNT / NW;  // epilogue tiles per wave
+    static_assert(EPT * NW == TMT * TNT, "whole epilogue tiles per wave");
+    __shared__ v4i_t red[NW][TMT * TNT][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
     const int ct0 = blockIdx.x * TNT, rt0 = blockIdx.y * TMT;
     const int nkb = a.K >> 7;
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm_t(GemvArgs a) {
             }
         }
     };
-    const int cnt = (nkb - wave + kDgWaves - 1) / kDgWaves;
+    const int cnt = (nkb - wave + NW - 1) / NW;
     WF_STAMP(0);
     EpiDec<MODE> e{&a};
     int er0[EPT], ec0[EPT];
@@ -634,7 +634,7 @@ __global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm_t(GemvArgs a) {
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b)
-        if (b < cnt) load(fa[b], fw[b], wave + kDgWaves * b);
+        if (b < cnt) load(fa[b], fw[b], wave + NW * b);
 #pragma unroll
     for (int x = 0; x < EPT; ++x) e.load_rope(ec0[x], l16, ein[x]);
     WF_STAMP(1);
@@ -645,7 +645,7 @@ __global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm_t(GemvArgs a) {
             if (t < cnt) {
                 mma(fa[b], fw[b]);
                 if (t == 0) WF_STAMP(2);
-                if (t + NB < cnt) load(fa[b], fw[b], wave + kDgWaves * (t + NB));
+                if (t + NB < cnt) load(fa[b], fw[b], wave + NW * (t + NB));
             }
         }
     }
@@ -661,7 +661,7 @@ __global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm_t(GemvArgs a) {
         const int tile = wave * EPT + x;
         v4i_t sum = red[0][tile][lane];
 #pragma unroll
-        for (int w = 1; w < kDgWaves; ++w) sum += red[w][tile][lane];
+        for (int w = 1; w < NW; ++w) sum += red[w][tile][lane];
         e.apply(er0[x], ec0[x], sum, l16, q, ein[x]);
     }
     WF_STAMP(5);
@@ -1166,8 +1166,10 @@ template <int MODE, int LPR>
 int launch_gemv_fmt(int fmt, const GemvArgs& ga, hipStream_t st) {
     if (fmt == WF_FMT_I2S_MFMA) {  // batched decode on the matrix-core tile layouts
         if (ga.N >= 8192) {  // wide layers (gate|up): 128-column tiles halve the code re-reads
+            // 4 waves per block (64 KiB of LDS, two blocks per CU): the 108 x 4 blocks of the 2B
+            // gate|up at batch 128 are resident in one round (8 waves + 128 KiB took two rounds)
             const dim3 grid((ga.N + 127) / 128, (ga.B + 31) / 32);
-            hipLaunchKernelGGL((k_dec_gemm_t<2, 8, 2, MODE>), grid, dim3(kDgWaves * 64), 0, st, ga);
+            hipLaunchKernelGGL((k_dec_gemm_t<2, 8, 3, MODE, 4>), grid, dim3(4 * 64), 0, st, ga);
             return check_launch("dec_gemm_t");
         }
         const dim3 grid(ga.N / 64 + ((ga.N & 63) ? 1 : 0), (ga.B + 31) / 32);
