@@ -477,7 +477,10 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
 typedef short v8s_t __attribute__((ext_vector_type(8)));
 typedef float v4f_t __attribute__((ext_vector_type(4)));
 constexpr int kAttnMfmaMaxGrp = 8;
-template <bool DB, bool RR>
+// WREC: one partial record per WAVE instead of per block -- grid.x = kAttnPartSplits / 4, the 8
+// waves of (b, g) take the 32-key tiles round-robin (wave r: tiles r, r + 8, ...) and each writes
+// its own (m, l, o) record: no LDS merge or barrier, and a wave streams several tiles per launch.
+template <bool DB, bool RR, bool WREC = false>
 __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* __restrict__ q, int64_t q_sb,
                                                    const uint16_t* __restrict__ K, const uint16_t* __restrict__ Vt,
                                                    int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv, int S,
@@ -485,7 +488,7 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
                                                    float2* __restrict__ ml_out, float* __restrict__ o_out,
                                                    const int32_t* __restrict__ pt, int pps, int npages, int64_t kv_pgs) {
     constexpr int D = 128;
-    const int s = blockIdx.x, g = blockIdx.y, b = blockIdx.z;
+    const int s = WREC ? 4 * (int)blockIdx.x + (int)(threadIdx.x >> 6) : (int)blockIdx.x, g = blockIdx.y, b = blockIdx.z;
     const int grp = Hq / Hkv, hq0 = g * grp;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
     const int Sb = min(seq_lens[b], S);
@@ -493,8 +496,8 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
     // takes tiles 4 s + w + 32 i, so per-wave tile counts differ by at most one and a block's four
     // waves finish together (a contiguous split per block left wave 0 with twice the tiles)
     const int T = ((Sb + kAttnPartSplits - 1) / kAttnPartSplits + 31) / 32 * 32;
-    const int kStride = RR ? 32 * 4 * kAttnPartSplits : 128;
-    const int t1 = RR ? Sb : min(s * T + T, Sb);
+    const int kStride = WREC ? 32 * kAttnPartSplits : (RR ? 32 * 4 * kAttnPartSplits : 128);
+    const int t1 = (RR || WREC) ? Sb : min(s * T + T, Sb);
     __shared__ float sm_m[4][kAttnMfmaMaxGrp], sm_l[4][kAttnMfmaMaxGrp];
     __shared__ __attribute__((aligned(16))) float sm_o[4][kAttnMfmaMaxGrp][D];
     // dense: (sequence, kv head) slab of S / 32 blocks; paged: block j of sequence b in page
@@ -508,7 +511,7 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
     v4f_t acc[8];
 #pragma unroll
     for (int n = 0; n < 8; ++n) acc[n] = v4f_t{0.f, 0.f, 0.f, 0.f};
-    int base = RR ? 32 * (4 * s + wave) : s * T + 32 * wave;
+    int base = WREC ? 32 * s : (RR ? 32 * (4 * s + wave) : s * T + 32 * wave);
     if (base < t1) {
         v8s_t qf[4];
         {
@@ -609,6 +612,19 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
     WF_STAMP(1);
     l_run += __shfl_xor(l_run, 16, 64);
     l_run += __shfl_xor(l_run, 32, 64);
+    if constexpr (WREC) {  // this wave's record s of each of its group's heads
+        const int64_t rec0 = (int64_t)(b * Hq + hq0) * kAttnPartSplits + s;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int h = 4 * q4 + r;
+            if (h < grp) {
+#pragma unroll
+                for (int n = 0; n < 8; ++n) o_out[(rec0 + (int64_t)h * kAttnPartSplits) * D + 16 * n + l16] = acc[n][r];
+            }
+        }
+        if (q4 == 0 && l16 < grp) ml_out[rec0 + (int64_t)l16 * kAttnPartSplits] = make_float2(m_run, l_run);
+        return;
+    }
     if (q4 == 0 && l16 < grp) {
         sm_m[wave][l16] = m_run;
         sm_l[wave][l16] = l_run;
@@ -664,7 +680,14 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
             return WF_EINVAL;
         }
         static const int variant = getenv("WF_ATTN_VARIANT") ? atoi(getenv("WF_ATTN_VARIANT")) : 0;
-        if (variant == 1)
+        const dim3 wgrid(kAttnPartSplits / 4, Hkv, B);
+        if (variant == 3)
+            hipLaunchKernelGGL((k_attn_mfma<false, false, true>), wgrid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq,
+                               Hkv, S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs);
+        else if (variant == 4)
+            hipLaunchKernelGGL((k_attn_mfma<true, false, true>), wgrid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq,
+                               Hkv, S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs);
+        else if (variant == 1)
             hipLaunchKernelGGL((k_attn_mfma<false, true>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv,
                                S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs);
         else if (variant == 2)
