@@ -27,6 +27,10 @@
 #include "wf_mfma.h"
 
 namespace wf {
+int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
+                      int64_t kv_sh, int Hq, int Hkv, const int32_t* row_pos, const int32_t* row_slot, int M,
+                      float sm_scale, const int32_t* pt, int pps, int npages, int64_t kv_pgs, uint16_t* out,
+                      int64_t o_rs, hipStream_t st);
 int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
                               float2* ml, float* o, hipStream_t st, bool kv_tiled, const int32_t* pt = nullptr,
@@ -72,6 +76,8 @@ struct GemvArgs {
     const int32_t* pt;
     int pps, npages;
     int64_t kv_pgs;
+    // prefill: row m of the GEMM is a token of KV slot row_slot[m] (nullptr: row m = slot m)
+    const int32_t* row_slot;
 };
 
 // Reference correction (direct_inference_full.py:201-208) for one output:
@@ -423,13 +429,14 @@ struct EpiDec {
                         g.out[(int64_t)m * g.out_stride + head * 128 + d] = f2bf(y);
                     } else {
                         const int kvh = head - g.Hq - (proj == 2 ? g.Hkv : 0);
-                        if (g.pt) {  // paged: block pos >> 5 lives in page pt[m][pos >> 5]
-                            const int pg = min(max(g.pt[(int64_t)m * g.pps + (pos >> 5)], 0), g.npages - 1);
+                        const int slot = g.row_slot ? g.row_slot[m] : m;
+                        if (g.pt) {  // paged: block pos >> 5 lives in page pt[slot][pos >> 5]
+                            const int pg = min(max(g.pt[(int64_t)slot * g.pps + (pos >> 5)], 0), g.npages - 1);
                             uint16_t* cache = (proj == 1 ? g.kc : g.vc) + pg * g.kv_pgs + (int64_t)kvh * 4096;
                             cache[proj == 1 ? k_tile_off(pos & 31, d) : v_tile_off(pos & 31, d)] = f2bf(y);
                             continue;
                         }
-                        uint16_t* cache = (proj == 1 ? g.kc : g.vc) + (int64_t)m * g.kv_b_stride + (int64_t)kvh * g.S * 128;
+                        uint16_t* cache = (proj == 1 ? g.kc : g.vc) + (int64_t)slot * g.kv_b_stride + (int64_t)kvh * g.S * 128;
                         if (g.kv_t) cache[proj == 1 ? k_tile_off(pos, d) : v_tile_off(pos, d)] = f2bf(y);
                         else cache[(int64_t)pos * 128 + d] = f2bf(y);
                     }
@@ -666,6 +673,25 @@ __global__ __launch_bounds__(NW * 64) void k_dec_gemm_t(GemvArgs a) {
     }
     WF_STAMP(5);
     WF_STAMP_DRAIN(6);
+}
+
+// Prefill GEMM (rows = prompt tokens) on the tile layouts with the decode step's fused epilogues:
+// the wf_mfma.h 128 x 256 tile main loop (pgemm_tile), then EpiDec<MODE> per 16 x 16 fragment
+// (correction, RoPE + K/V cache write through row_slot, residual, ReLU^2 * up).
+template <int MODE>
+__global__ __launch_bounds__(512) void k_pgemm_fused(GemvArgs a, int nbm, int nbn) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kPgStages * kPgStage];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+    const int wr = wave >> 2, wc = wave & 3;
+    int bm, bn;
+    pg_tile_of(blockIdx.x, nbm, nbn, bm, bn);
+    v4i_t acc[4][4];
+    pgemm_tile<kPgStages>(a.w, a.q8, a.B, a.N, a.K, bm, bn, lds, acc);
+    EpiDec<MODE> e{&a};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e.apply(bm * 128 + (4 * wr + i) * 16, bn * 256 + (4 * wc + j) * 16, acc[i][j], l16, q);
 }
 
 // One wave per 16 x 16 output tile: lane (l16, q) sums the nsplit int32 partials of rows
@@ -1112,6 +1138,13 @@ struct wf_model {
     int64_t q8_stride = 0;
     int kv_tiled = 0;  // batched MFMA decode: K/V caches in the tile layouts (include/wf_bitnet.h)
     uint16_t* embed_t = nullptr;  // batched LM head: the tied embedding in the fragment layout (copy)
+    // prefill workspace (wf_model_prefill_reserve): rows of prompt tokens
+    int pf_rows = 0;
+    uint16_t *pf_h_a = nullptr, *pf_h_b = nullptr, *pf_q = nullptr, *pf_attn = nullptr, *pf_act = nullptr;
+    int8_t* pf_q8 = nullptr;
+    float* pf_sf = nullptr;
+    int* pf_asum = nullptr;
+    int32_t* pf_seq = nullptr;
     hipStream_t cap = nullptr;
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
@@ -1458,7 +1491,8 @@ int wf_model_destroy(wf_model* m) {
     if (m->graph) (void)hipGraphDestroy(m->graph);
     if (m->cap) (void)hipStreamDestroy(m->cap);
     void* ptrs[] = {m->seq_lens, m->h_a, m->h_b, m->qbuf, m->part_ml, m->part_o, m->hn, m->act, m->q8, m->dec_ws,
-                    m->act_sf, m->act_sum, m->tickets, m->am_part, m->embed_t};
+                    m->act_sf, m->act_sum, m->tickets, m->am_part, m->embed_t, m->pf_h_a, m->pf_h_b, m->pf_q,
+                    m->pf_attn, m->pf_act, m->pf_q8, m->pf_sf, m->pf_asum, m->pf_seq};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete[] m->d.wscale;
@@ -1475,6 +1509,119 @@ int wf_model_launch_op(wf_model* m, int layer, int op, void* stream) {
     WF_REQUIRE(m, "model_launch_op: null model");
     WF_REQUIRE(layer >= 0 && layer < m->d.layers, "model_launch_op: layer %d out of range", layer);
     return run_op(m, layer, op, as_stream(stream));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Prefill: the prompt tokens of any KV slots as GEMM rows (BASELINE configs[2]). Per layer:
+// row norm + quantize (tile order) -> fused prefill GEMM (k_pgemm_fused) for QKV (+ RoPE, K/V
+// rows written into each token's slot / position), causal attention (k_attn_prefill), row norm ->
+// O (+ residual), row norm -> gate|up (ReLU^2 * up), row norm -> down (+ residual). The float
+// sequence per token is the decode step's (same epilogues, same row norm); attention sums over the
+// whole prefix in one pass instead of the decode step's 8 merged splits.
+// ---------------------------------------------------------------------------------------------
+int wf_model_prefill_reserve(wf_model* m, int rows) {
+    WF_REQUIRE(m && rows > 0, "model_prefill_reserve: bad arguments");
+    const wf_model_desc& d = m->d;
+    WF_REQUIRE(m->kv_tiled && d.wfmt == WF_FMT_I2S_MFMA && d.head_dim == 128 && d.n_heads == 4 * d.n_kv_heads,
+               "model_prefill: needs the batched matrix-core decoder (batch >= %d, I2_S weights), head_dim 128 "
+               "and 4 query heads per kv head",
+               kDecMfmaMinB);
+    rows = (rows + 15) / 16 * 16;
+    if (rows <= m->pf_rows) return WF_OK;
+    void* old[] = {m->pf_h_a, m->pf_h_b, m->pf_q, m->pf_attn, m->pf_act, m->pf_q8, m->pf_sf, m->pf_asum, m->pf_seq};
+    for (void* p : old)
+        if (p) (void)hipFree(p);
+    m->pf_rows = 0;
+    const size_t H = d.hidden, I = d.inter, R = rows;
+    hipError_t e = hipSuccess;
+#define WF_PA(ptr, bytes) \
+    if (e == hipSuccess) e = hipMalloc((void**)&(ptr), (bytes))
+    WF_PA(m->pf_h_a, 2 * R * H);
+    WF_PA(m->pf_h_b, 2 * R * H);
+    WF_PA(m->pf_q, 2 * R * H);
+    WF_PA(m->pf_attn, 2 * R * H);
+    WF_PA(m->pf_act, 2 * R * I);
+    WF_PA(m->pf_q8, R * (H > I ? H : I));
+    WF_PA(m->pf_sf, sizeof(float) * R);
+    WF_PA(m->pf_asum, sizeof(int) * R);
+    WF_PA(m->pf_seq, sizeof(int32_t) * R);
+#undef WF_PA
+    if (e != hipSuccess) {
+        set_error("model_prefill_reserve: %s", hipGetErrorString(e));
+        return WF_EHIP;
+    }
+    m->pf_rows = rows;
+    return WF_OK;
+}
+
+extern "C++" {
+static void prefill_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, const uint16_t* nw, int K, int rows,
+                            hipStream_t st) {
+    const float eps = m->d.eps;
+    if (norm_ppt(K) == 1)
+        hipLaunchKernelGGL((k_rownorm<1, false, true>), dim3(rows), dim3(kNT), 0, st, x, xs, nw, K, eps, m->pf_q8, (int64_t)0,
+                           m->pf_sf, m->pf_asum, (uint16_t*)nullptr, (int64_t)0);
+    else
+        hipLaunchKernelGGL((k_rownorm<2, false, true>), dim3(rows), dim3(kNT), 0, st, x, xs, nw, K, eps, m->pf_q8, (int64_t)0,
+                           m->pf_sf, m->pf_asum, (uint16_t*)nullptr, (int64_t)0);
+}
+
+template <int MODE>
+static void prefill_gemm(const GemvArgs& a, hipStream_t st) {
+    const int nbm = (a.B + 127) / 128, nbn = (a.N + 255) / 256;
+    hipLaunchKernelGGL((k_pgemm_fused<MODE>), dim3(nbm * nbn), dim3(512), 0, st, a, nbm, nbn);
+}
+}  // extern "C++"
+
+int wf_model_prefill(wf_model* m, const int32_t* tokens, const int32_t* row_slot, const int32_t* row_pos, int rows,
+                     void* stream) {
+    WF_REQUIRE(m && tokens && row_slot && row_pos, "model_prefill: null argument");
+    WF_REQUIRE(rows > 0 && rows <= m->pf_rows, "model_prefill: %d rows exceed the reserved %d (wf_model_prefill_reserve)",
+               rows, m->pf_rows);
+    WF_REQUIRE(rows % 4 == 0, "model_prefill: rows must come in aligned groups of 4 of one slot (got %d rows)", rows);
+    const wf_model_desc& d = m->d;
+    hipStream_t st = as_stream(stream);
+    const int H = d.hidden, I = d.inter, D = d.head_dim;
+    hipLaunchKernelGGL(k_embed, dim3(rows), dim3(256), 0, st, d.embed, tokens, H, d.vocab, m->pf_h_a, row_pos, m->pf_seq);
+    int rc;
+    for (int l = 0; l < d.layers; ++l) {
+        const float* wsh = d.wscale + 7 * l;
+        GemvArgs a = base_args(m, l);
+        a.B = rows;
+        a.q8 = m->pf_q8;
+        a.act_sf = m->pf_sf;
+        a.act_sum = m->pf_asum;
+        a.positions = row_pos;
+        a.row_slot = row_slot;
+        // QKV (+ RoPE, K/V rows into the cache)
+        prefill_rownorm(m, m->pf_h_a, H, d.ln_in + (int64_t)l * H, H, rows, st);
+        a.w = d.w_qkv + (int64_t)l * m->qkv_rows * (H / 4); a.N = m->qkv_rows; a.K = H;
+        a.ws0 = wsh[0]; a.ws1 = wsh[1]; a.ws2 = wsh[2]; a.out = m->pf_q; a.out_stride = H;
+        prefill_gemm<MODE_QKV>(a, st);
+        // causal attention over each token's slot prefix
+        const bool paged = d.page_table != nullptr;
+        if ((rc = prefill_attention(m->pf_q, H, a.kc, a.vc, paged ? 0 : a.kv_b_stride, paged ? 32 * D : (int64_t)d.max_seq * D,
+                                    d.n_heads, d.n_kv_heads, row_pos, row_slot, rows, 1.0f / sqrtf((float)D), a.pt,
+                                    a.pps, a.npages, a.kv_pgs, m->pf_attn, H, st)))
+            return rc;
+        // O (+ residual)
+        prefill_rownorm(m, m->pf_attn, H, d.attn_sub + (int64_t)l * H, H, rows, st);
+        a.w = d.w_o + (int64_t)l * H * (H / 4); a.N = H; a.K = H; a.ws0 = wsh[3];
+        a.resid = m->pf_h_a; a.out = m->pf_h_b; a.out_stride = H;
+        prefill_gemm<MODE_O>(a, st);
+        // gate|up
+        prefill_rownorm(m, m->pf_h_b, H, d.ln_post + (int64_t)l * H, H, rows, st);
+        a.w = d.w_gu + (int64_t)l * 2 * I * (H / 4); a.N = 2 * I; a.K = H; a.ws0 = wsh[4]; a.ws1 = wsh[5];
+        a.out = m->pf_act; a.out_stride = I;
+        prefill_gemm<MODE_GU>(a, st);
+        // down (+ residual)
+        prefill_rownorm(m, m->pf_act, I, d.ffn_sub + (int64_t)l * I, I, rows, st);
+        a.w = d.w_d + (int64_t)l * H * (I / 4); a.N = H; a.K = I; a.ws0 = wsh[6];
+        a.resid = m->pf_h_b; a.out = m->pf_h_a; a.out_stride = H;
+        prefill_gemm<MODE_DN>(a, st);
+        if ((rc = check_launch("prefill layer"))) return rc;
+    }
+    return WF_OK;
 }
 
 int64_t wf_bitnet_linear_ws_bytes(int M, int K) {

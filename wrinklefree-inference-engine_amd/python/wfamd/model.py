@@ -312,6 +312,52 @@ class BitNetDecoder:
         self._pt_host[b] = 0
         self.page_table[b].zero_()
 
+    def prefill(self, seqs, chunk_rows: int = 4096) -> None:
+        """Prompt pass (include/wf_bitnet.h wf_model_prefill): `seqs` = iterable of (slot, tokens,
+        start); token i of a slot is processed at position start + i and its K/V lands in the
+        slot's cache (pages reserved on demand). Rows are packed per slot, padded to a multiple of 4
+        by repeating the slot's last token, and run `chunk_rows` at a time. The decode state
+        (tokens / positions / logits) is left alone: see admit()."""
+        tok, slot, pos = [], [], []
+        for b, toks, start in seqs:
+            toks = [int(t) for t in toks]
+            n = len(toks)
+            if n == 0:
+                continue
+            if start + n > self.cfg.max_seq:
+                raise ValueError(f"slot {b}: positions up to {start + n} exceed max_seq {self.cfg.max_seq}")
+            if self.paged:
+                self.reserve(b, start + n)
+            pad = (-n) % 4
+            tok += toks + [toks[-1]] * pad
+            pos += list(range(start, start + n)) + [start + n - 1] * pad
+            slot += [int(b)] * (n + pad)
+        rows = len(tok)
+        if rows == 0:
+            return
+        chunk_rows = max(4, chunk_rows // 4 * 4)
+        call("wf_model_prefill_reserve", self._h, min(rows, chunk_rows))
+        t = torch.tensor(tok, dtype=torch.int32, device=self.dev)
+        sl = torch.tensor(slot, dtype=torch.int32, device=self.dev)
+        ps = torch.tensor(pos, dtype=torch.int32, device=self.dev)
+        st = torch.cuda.current_stream().cuda_stream
+        for r0 in range(0, rows, chunk_rows):
+            n = min(rows - r0, chunk_rows)
+            call("wf_model_prefill", self._h, t[r0:].data_ptr(), sl[r0:].data_ptr(), ps[r0:].data_ptr(), n, st)
+        self._pf_keep = (t, sl, ps)  # alive until the stream has consumed them
+
+    def admit(self, b: int, prompt) -> None:
+        """Start sequence `prompt` in slot b: prefill all but its last token, then the next decode
+        step runs the last token at position len - 1 (scripts/direct_inference_full.py's loop)."""
+        prompt = [int(x) for x in prompt]
+        if not prompt:
+            raise ValueError("empty prompt")
+        self.prefill([(b, prompt[:-1], 0)])
+        if self.paged:
+            self.reserve(b, len(prompt))
+        self.tokens[b] = prompt[-1]
+        self.positions[b] = len(prompt) - 1
+
     def set_state(self, tokens, positions) -> None:
         self.tokens.copy_(torch.as_tensor(tokens, dtype=torch.int32))
         self.positions.copy_(torch.as_tensor(positions, dtype=torch.int32))
