@@ -215,10 +215,11 @@ int wf_model_launch_op(wf_model* m, int layer, int op, void* stream);
  * decode loop): run prompt tokens of any KV slots through all layers as GEMM rows and write their
  * K/V into the cache (dense planes or pages). Batched matrix-core decoders only (batch >= 16, I2_S
  * weights), head_dim 128, 4 query heads per kv head. Row r: token tokens[r] of slot row_slot[r] at
- * position row_pos[r] (device int32 arrays); every aligned group of 4 rows belongs to one slot
- * (pad a sequence by repeating its last row); a slot's earlier positions must already be in the
+ * position row_pos[r] (device int32 arrays); every aligned group of WF_PREFILL_ROW_GROUP rows
+ * belongs to one slot (pad a sequence by repeating its last row); a slot's earlier positions must already be in the
  * cache (earlier rows of the same call count). Does not touch tokens / positions / logits: the
  * decode step then runs the prompt's last token. reserve() allocates the row workspace once. */
+#define WF_PREFILL_ROW_GROUP 8
 int wf_model_prefill_reserve(wf_model* m, int rows);
 int wf_model_prefill(wf_model* m, const int32_t* tokens, const int32_t* row_slot, const int32_t* row_pos, int rows,
                      void* stream);

@@ -43,4 +43,10 @@ timeout -k 10 300 python tools/prefill_gemm_bench.py > "$O/prefill.log" 2>&1 || 
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_prefill" -o run -- python3 "$R/tools/prefill_gemm_bench.py" --iters 10 > "$O/prof_prefill.log" 2>&1 || exit $?
 cd "$R" && python3 tools/prof_summary.py "$O/prof_prefill" > "$O/kernel_stats_prefill.txt" 2>&1 || exit $?
 tail -1 "$O/prefill.log"
+step prefill-e2e
+timeout -k 10 300 python tools/prefill_bench.py > "$O/prefill_e2e.log" 2>&1 || exit $?
+timeout -k 10 300 python tools/prefill_bench.py --paged >> "$O/prefill_e2e.log" 2>&1 || exit $?
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_prefill_e2e" -o run -- python3 "$R/tools/prefill_bench.py" --iters 1 > "$O/prof_prefill_e2e.log" 2>&1 || exit $?
+cd "$R" && python3 tools/prof_summary.py "$O/prof_prefill_e2e" > "$O/kernel_stats_prefill_e2e.txt" 2>&1 || exit $?
+grep workload "$O/prefill_e2e.log"
 echo "== done"

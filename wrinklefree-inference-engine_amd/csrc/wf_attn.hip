@@ -658,42 +658,47 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
 // ---------------------------------------------------------------------------------------------
 // Prefill (causal) attention on the tile-layout K/V caches, after the prefill QKV GEMM has written
 // the prompt's K/V rows: query row m (a prompt token of KV slot row_slot[m] at position
-// row_pos[m]) attends to keys [0, row_pos[m]] of its slot. Block = (16 rows, kv head g) = 4 waves;
-// wave w takes rows 16 blockIdx.x + 4 w + tk, tk < 4, and the group's 4 query heads: MFMA column
-// c = 4 tk + h (the decode kernel's head columns, now all 16 used). The host packs every aligned
-// group of 4 rows from one slot (padding with repeats of a sequence's last token). Per 32-key tile:
-// the decode kernel's QK / online softmax / P.V (P as bf16 hi + lo), with a per-column causal limit;
-// V rows past the wave's last position are zeroed (stale pages). Each wave streams its whole key
+// row_pos[m]) attends to keys [0, row_pos[m]] of its slot. Block = (4 waves, kv head g); a wave
+// takes RPW = 4 CG consecutive rows as CG column groups: MFMA column c = 4 tk + h of group u is
+// token 4u + tk with query head h of the group (the decode kernel's head columns, all 16 used),
+// and every K/V fragment it loads feeds all CG groups. The host packs every aligned group of
+// kPrefillRowGroup rows from one slot (padding with repeats of a sequence's last token). Per 32-key tile:
+// the decode kernel's QK / online softmax / P.V with a per-column causal limit, P rounded to bf16
+// for the P.V MFMA (as a bf16 flash SDPA does; the decode kernel keeps hi + lo) and the
+// accumulator rescale skipped while no column's running max moves; V rows past the wave's last
+// position are zeroed (stale pages). Each wave streams its whole key
 // range and writes the normalised output rows bf16(o / l) (no split partials).
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void k_attn_prefill(const uint16_t* __restrict__ q, int64_t q_rs,
+template <int CG, int OCC>
+__global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __restrict__ q, int64_t q_rs,
                                                          const uint16_t* __restrict__ K, const uint16_t* __restrict__ Vt,
                                                          int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv,
                                                          const int32_t* __restrict__ row_pos,
                                                          const int32_t* __restrict__ row_slot, int M, float sm_scale,
                                                          const int32_t* __restrict__ pt, int pps, int npages,
                                                          int64_t kv_pgs, uint16_t* __restrict__ out, int64_t o_rs) {
-    constexpr int D = 128;
+    constexpr int D = 128, RPW = 4 * CG;  // rows per wave: CG column groups of 4 tokens x 4 heads
     const int g = blockIdx.y, hq0 = g * 4;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
-    const int r0 = blockIdx.x * 16 + wave * 4;  // this wave's 4 rows
-    if (r0 >= M) return;                       // whole wave
+    const int r0 = (blockIdx.x * 4 + wave) * RPW;  // this wave's rows
+    if (r0 >= M) return;                            // whole wave
     const int slot = row_slot[r0];
-    // column l16 = (token l16 >> 2, head l16 & 3); its causal limit (keys < lim_c)
-    const int my_row = min(r0 + (l16 >> 2), M - 1);
-    const int lim_c = row_pos[my_row] + 1;
-    int lim_w = 0;
+    int lim_c[CG], lim_w = 0;  // column l16 of group u = (token 4u + (l16 >> 2), head l16 & 3)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) lim_w = max(lim_w, row_pos[min(r0 + t, M - 1)] + 1);
+    for (int u = 0; u < CG; ++u) lim_c[u] = row_pos[min(r0 + 4 * u + (l16 >> 2), M - 1)] + 1;
+#pragma unroll
+    for (int t = 0; t < RPW; ++t) lim_w = max(lim_w, row_pos[min(r0 + t, M - 1)] + 1);
     const uint16_t* Kb = K + (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;
     const uint16_t* Vb = Vt + (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;
     const int32_t* ptb = pt ? pt + (int64_t)slot * pps : nullptr;
 
-    v8s_t qf[4];
-    {
-        const uint16_t* qp = q + (int64_t)my_row * q_rs + (int64_t)(hq0 + (l16 & 3)) * D + 8 * q4;
+    v8s_t qf[CG][4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) qf[c] = __builtin_bit_cast(v8s_t, *reinterpret_cast<const uint4*>(qp + 32 * c));
+    for (int u = 0; u < CG; ++u) {
+        const int row = min(r0 + 4 * u + (l16 >> 2), M - 1);
+        const uint16_t* qp = q + (int64_t)row * q_rs + (int64_t)(hq0 + (l16 & 3)) * D + 8 * q4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) qf[u][c] = __builtin_bit_cast(v8s_t, *reinterpret_cast<const uint4*>(qp + 32 * c));
     }
     auto load = [&](uint4 (&kr)[2][4], uint4 (&vr)[8], int bs) {
         const int64_t blk = ptb ? (int64_t)min(max(ptb[__builtin_amdgcn_readfirstlane(bs) >> 5], 0), npages - 1) * kv_pgs
@@ -705,85 +710,98 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill(const uint16_t* __restr
 #pragma unroll
         for (int n = 0; n < 8; ++n) vr[n] = *reinterpret_cast<const uint4*>(Vb + blk + n * 512);
     };
-    float m_run = -INFINITY, l_run = 0.f;
-    v4f_t acc[8];
+    float m_run[CG], l_run[CG];
+    v4f_t acc[CG][8];
 #pragma unroll
-    for (int n = 0; n < 8; ++n) acc[n] = v4f_t{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < CG; ++u) {
+        m_run[u] = -INFINITY;
+        l_run[u] = 0.f;
+#pragma unroll
+        for (int n = 0; n < 8; ++n) acc[u][n] = v4f_t{0.f, 0.f, 0.f, 0.f};
+    }
     uint4 kA[2][4], vA[8];
     load(kA, vA, 0);
     for (int bs = 0; bs < lim_w; bs += 32) {
-        v4f_t sc[2];
+        v8s_t ph[CG];
+        float ar[CG][4];
+        bool resc[CG];
 #pragma unroll
-        for (int tau = 0; tau < 2; ++tau) {
-            sc[tau] = v4f_t{0.f, 0.f, 0.f, 0.f};
+        for (int u = 0; u < CG; ++u) {
+            v4f_t sc[2];
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
-                sc[tau] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8s_t, kA[tau][c]), qf[c], sc[tau],
-                                                                  0, 0, 0);
+            for (int tau = 0; tau < 2; ++tau) {
+                sc[tau] = v4f_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    sc[tau] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8s_t, kA[tau][c]), qf[u][c],
+                                                                      sc[tau], 0, 0, 0);
+            }
+            const int lim = lim_c[u] - bs - 8 * q4;  // valid keys of column l16 among this lane's 8
+            float x[8], mx = -INFINITY;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                x[e] = e < lim ? sc[e >> 2][e & 3] * sm_scale : -INFINITY;
+                mx = fmaxf(mx, x[e]);
+            }
+            mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            // key 0 is valid for every column, so m_run is finite after the first tile; a later tile
+            // with no valid key for a column leaves it unchanged (alpha = 1, p = 0)
+            const float mnew = fmaxf(m_run[u], mx);
+            const float alpha = __expf(m_run[u] - mnew);
+            m_run[u] = mnew;
+            float p[8], ps = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                p[e] = __expf(x[e] - mnew);
+                ps += p[e];
+            }
+            l_run[u] = l_run[u] * alpha + ps;
+            uint32_t hi[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) hi[j] = pk_bf16(p[2 * j], p[2 * j + 1]);
+            ph[u] = __builtin_bit_cast(v8s_t, make_uint4(hi[0], hi[1], hi[2], hi[3]));
+            resc[u] = __any(alpha != 1.0f);  // the running max moved for some column: rescale acc
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ar[u][r] = __shfl(alpha, 4 * q4 + r, 64);
         }
-        const int lim = lim_c - bs - 8 * q4;  // valid keys of column l16 among this lane's 8
-        float x[8], mx = -INFINITY;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            x[e] = e < lim ? sc[e >> 2][e & 3] * sm_scale : -INFINITY;
-            mx = fmaxf(mx, x[e]);
-        }
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        // key 0 is valid for every column, so m_run is finite after the first tile; a later tile
-        // with no valid key for a column leaves it unchanged (alpha = 1, p = 0)
-        const float mnew = fmaxf(m_run, mx);
-        const float alpha = __expf(m_run - mnew);
-        m_run = mnew;
-        float p[8], ps = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            p[e] = __expf(x[e] - mnew);
-            ps += p[e];
-        }
-        l_run = l_run * alpha + ps;
-        uint32_t hi[4], lo[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            hi[j] = pk_bf16(p[2 * j], p[2 * j + 1]);
-            lo[j] = pk_bf16(p[2 * j] - bf_lo(hi[j]), p[2 * j + 1] - bf_hi(hi[j]));
-        }
-        const v8s_t ph = __builtin_bit_cast(v8s_t, make_uint4(hi[0], hi[1], hi[2], hi[3]));
-        const v8s_t pl = __builtin_bit_cast(v8s_t, make_uint4(lo[0], lo[1], lo[2], lo[3]));
-        float ar[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ar[r] = __shfl(alpha, 4 * q4 + r, 64);
         const int limv = lim_w - bs - 8 * q4;  // V rows past every column's limit: zero (stale)
         uint32_t vm[4] = {~0u, ~0u, ~0u, ~0u};
         if (limv < 8) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) vm[j] = (2 * j < limv ? 0xffffu : 0u) | (2 * j + 1 < limv ? 0xffff0000u : 0u);
         }
-        uint4 vcur[8];
+        v8s_t vf[8];
 #pragma unroll
-        for (int n = 0; n < 8; ++n) vcur[n] = vA[n];
+        for (int n = 0; n < 8; ++n)
+            vf[n] = __builtin_bit_cast(v8s_t, make_uint4(vA[n].x & vm[0], vA[n].y & vm[1], vA[n].z & vm[2], vA[n].w & vm[3]));
         if (bs + 32 < lim_w) load(kA, vA, bs + 32);  // next tile in flight during the P.V MFMAs
 #pragma unroll
-        for (int n = 0; n < 8; ++n) {
+        for (int u = 0; u < CG; ++u)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[n][r] *= ar[r];
-            const uint4 v = make_uint4(vcur[n].x & vm[0], vcur[n].y & vm[1], vcur[n].z & vm[2], vcur[n].w & vm[3]);
-            const v8s_t vf = __builtin_bit_cast(v8s_t, v);
-            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vf, acc[n], 0, 0, 0);
-            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vf, acc[n], 0, 0, 0);
-        }
+            for (int n = 0; n < 8; ++n) {
+                if (resc[u]) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[u][n][r] *= ar[u][r];
+                }
+                acc[u][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph[u], vf[n], acc[u][n], 0, 0, 0);
+            }
     }
-    l_run += __shfl_xor(l_run, 16, 64);
-    l_run += __shfl_xor(l_run, 32, 64);
-    // acc rows 4 q4 + r = column (token q4, head r); its l sits in lane 4 q4 + r
-    const int row = r0 + q4;
+    // acc[u] rows 4 q4 + r = column (token 4u + q4, head r); its l sits in lane 4 q4 + r
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const float inv = 1.0f / __shfl(l_run, 4 * q4 + r, 64);
-        if (row < M) {
+    for (int u = 0; u < CG; ++u) {
+        float lr = l_run[u];
+        lr += __shfl_xor(lr, 16, 64);
+        lr += __shfl_xor(lr, 32, 64);
+        const int row = r0 + 4 * u + q4;
 #pragma unroll
-            for (int n = 0; n < 8; ++n)
-                out[(int64_t)row * o_rs + (int64_t)(hq0 + r) * D + 16 * n + l16] = f2bf(rbf(acc[n][r] * inv));
+        for (int r = 0; r < 4; ++r) {
+            const float inv = 1.0f / __shfl(lr, 4 * q4 + r, 64);
+            if (row < M) {
+#pragma unroll
+                for (int n = 0; n < 8; ++n)
+                    out[(int64_t)row * o_rs + (int64_t)(hq0 + r) * D + 16 * n + l16] = f2bf(rbf(acc[u][n][r] * inv));
+            }
         }
     }
 }
@@ -796,8 +814,11 @@ int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const 
         set_error("prefill_attention: GQA group %d != 4 not supported", Hq / Hkv);
         return WF_EINVAL;
     }
-    hipLaunchKernelGGL(k_attn_prefill, dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v, kv_sb, kv_sh, Hq, Hkv,
-                       row_pos, row_slot, M, sm_scale, pt, pps, npages, kv_pgs, out, o_rs);
+    // one column group per wave at 2 waves / SIMD: measured faster than two groups per wave
+    // (spills at 256 VGPRs, or 1 wave / SIMD without them) -- the kernel is latency-bound per tile
+    constexpr int CG = 1;
+    hipLaunchKernelGGL((k_attn_prefill<CG, 2>), dim3((M + 16 * CG - 1) / (16 * CG), Hkv), dim3(256), 0, st, q, q_rs, k,
+                       v, kv_sb, kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale, pt, pps, npages, kv_pgs, out, o_rs);
     return check_launch("prefill_attention");
 }
 

@@ -319,6 +319,7 @@ __device__ __forceinline__ int64_t bf_tile_off(int r, int p, int H) {
 }
 
 constexpr int kAttnPartSplits = 8;
+constexpr int kPrefillRowGroup = WF_PREFILL_ROW_GROUP;  // prefill rows per slot-uniform group (include/wf_bitnet.h)
 
 // Matrix-core tile layouts of the K / V caches (batched decode; head_dim 128, S % 32 == 0), element
 // offsets within one (sequence, kv head) slab of S x 128 bf16. Key position t = 32 blk + o:

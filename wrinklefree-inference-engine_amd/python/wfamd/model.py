@@ -315,8 +315,8 @@ class BitNetDecoder:
     def prefill(self, seqs, chunk_rows: int = 4096) -> None:
         """Prompt pass (include/wf_bitnet.h wf_model_prefill): `seqs` = iterable of (slot, tokens,
         start); token i of a slot is processed at position start + i and its K/V lands in the
-        slot's cache (pages reserved on demand). Rows are packed per slot, padded to a multiple of 4
-        by repeating the slot's last token, and run `chunk_rows` at a time. The decode state
+        slot's cache (pages reserved on demand). Rows are packed per slot, padded to a multiple of
+        WF_PREFILL_ROW_GROUP by repeating the slot's last token, and run `chunk_rows` at a time. The decode state
         (tokens / positions / logits) is left alone: see admit()."""
         tok, slot, pos = [], [], []
         for b, toks, start in seqs:
@@ -328,14 +328,15 @@ class BitNetDecoder:
                 raise ValueError(f"slot {b}: positions up to {start + n} exceed max_seq {self.cfg.max_seq}")
             if self.paged:
                 self.reserve(b, start + n)
-            pad = (-n) % 4
+            pad = (-n) % _lib.WF_PREFILL_ROW_GROUP
             tok += toks + [toks[-1]] * pad
             pos += list(range(start, start + n)) + [start + n - 1] * pad
             slot += [int(b)] * (n + pad)
         rows = len(tok)
         if rows == 0:
             return
-        chunk_rows = max(4, chunk_rows // 4 * 4)
+        g = _lib.WF_PREFILL_ROW_GROUP
+        chunk_rows = max(g, chunk_rows // g * g)
         call("wf_model_prefill_reserve", self._h, min(rows, chunk_rows))
         t = torch.tensor(tok, dtype=torch.int32, device=self.dev)
         sl = torch.tensor(slot, dtype=torch.int32, device=self.dev)
