@@ -146,6 +146,22 @@ def test_decoder_page_pool_semantics():
     assert sorted(ids.tolist()) == list(range(64)) and ids.tolist() != list(range(64))
 
 
+def test_prefill_row_packing():
+    """wf_model_prefill's row contract (include/wf_bitnet.h): every aligned group of
+    WF_PREFILL_ROW_GROUP rows is one slot, positions consecutive from `start`, pads repeat the last row."""
+    from wfamd import _lib
+    from wfamd.model import pack_prefill_rows
+    g = _lib.WF_PREFILL_ROW_GROUP
+    seqs = [(3, [5, 6, 7], 0), (0, [], 4), (7, list(range(100, 100 + g + 1)), 10), (1, [9] * g, 2)]
+    tok, slot, pos = pack_prefill_rows(seqs)
+    assert len(tok) == len(slot) == len(pos) == 4 * g
+    for r0 in range(0, len(tok), g):
+        assert len(set(slot[r0:r0 + g])) == 1
+    assert tok[:3] == [5, 6, 7] and pos[:3] == [0, 1, 2] and set(tok[3:g]) == {7} and set(pos[3:g]) == {2}
+    assert slot[g:3 * g] == [7] * 2 * g and pos[g:2 * g + 1] == list(range(10, 10 + g + 1))
+    assert pos[2 * g + 1:3 * g] == [10 + g] * (g - 1) and tok[3 * g:] == [9] * g and pos[3 * g:] == list(range(2, 2 + g))
+
+
 def test_model_layout_permutations():
     from wfamd.model import gate_up_interleave, qkv_row_permutation
     p = qkv_row_permutation(3, 128)

@@ -13,6 +13,7 @@
 #include "wf_common.h"
 #include "wf_device.h"
 #include "wf_norm.h"
+#include "wf_mfma.h"
 
 namespace wf {
 
@@ -806,6 +807,151 @@ __global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __res
     }
 }
 
+// The same prefill attention with the K/V tiles staged once per block in LDS: the block's 4 waves
+// (16 consecutive rows of one slot: kPrefillRowGroup = 16) need the same tiles, so each wave DMAs
+// a quarter of every 16 KiB tile (4 x 1 KiB LDS-DMA, inline asm: hipcc does not drain the ring
+// before the fragment reads) into a P-slot ring, with P - 2 tiles in flight beyond the one being
+// read; the fragments come from LDS (contiguous KiB per wave-instruction). 4x less L2 / MALL
+// traffic than every wave loading its own copy, and a deeper pipeline than registers allow.
+constexpr int kPfStages = 4;  // 64 KiB ring + page ids: two blocks per CU
+constexpr int kPfMaxTiles = 256;  // 32-key tiles per sequence (max_seq <= 8192)
+template <int P>
+__global__ __launch_bounds__(256, 2) void k_attn_prefill_lds(const uint16_t* __restrict__ q, int64_t q_rs,
+                                                             const uint16_t* __restrict__ K,
+                                                             const uint16_t* __restrict__ Vt, int64_t kv_sb,
+                                                             int64_t kv_sh, int Hq, int Hkv,
+                                                             const int32_t* __restrict__ row_pos,
+                                                             const int32_t* __restrict__ row_slot, int M,
+                                                             float sm_scale, const int32_t* __restrict__ pt, int pps,
+                                                             int npages, int64_t kv_pgs, uint16_t* __restrict__ out,
+                                                             int64_t o_rs) {
+    constexpr int D = 128;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[P * 16384];
+    __shared__ int s_page[kPfMaxTiles];  // the block's page ids (LDS reads: no vmcnt in the loop)
+    const int g = blockIdx.y, hq0 = g * 4;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
+    const int rb = blockIdx.x * 16;
+    if (rb >= M) return;  // whole block
+    const int r0 = rb + wave * 4;
+    const int slot = __builtin_amdgcn_readfirstlane(row_slot[rb]);  // uniform: page ids are scalar loads
+    const int lim_c = row_pos[min(r0 + (l16 >> 2), M - 1)] + 1;
+    int lim_b = 0;
+    for (int t = 0; t < 16; ++t) lim_b = max(lim_b, row_pos[min(rb + t, M - 1)] + 1);
+    const int ntiles_v = (lim_b + 31) >> 5;
+    v8s_t qf[4];
+    {
+        const uint16_t* qp = q + (int64_t)min(r0 + (l16 >> 2), M - 1) * q_rs + (int64_t)(hq0 + (l16 & 3)) * D + 8 * q4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) qf[c] = __builtin_bit_cast(v8s_t, *reinterpret_cast<const uint4*>(qp + 32 * c));
+    }
+    // wait for q here, before the ring's asm DMAs exist: hipcc cannot count those, and a wait for q
+    // placed inside the loop would drain the ring every tile
+#pragma unroll
+    for (int c = 0; c < 4; ++c) asm volatile("" : "+v"(qf[c]));
+    const int ntiles = __builtin_amdgcn_readfirstlane(ntiles_v);
+    const uint16_t* Kg = K + (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;
+    const uint16_t* Vg = Vt + (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;
+    if (pt) {
+        for (int t = threadIdx.x; t < ntiles; t += 256) s_page[t] = min(max(pt[(int64_t)slot * pps + t], 0), npages - 1);
+        __syncthreads();
+    }
+    auto issue = [&](int t) {  // wave w DMAs pieces 4w .. 4w + 3 of tile t (K fragments 0..7, V 8..15)
+        const int64_t blk = pt ? (int64_t)s_page[t] * kv_pgs : (int64_t)t * 4096;
+        uint8_t* st = ring + (t % P) * 16384;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int j = wave * 4 + jj;
+            glds16_asm((j < 8 ? Kg : Vg) + blk + (j & 7) * 512, st + j * 1024);
+        }
+    };
+    float m_run = -INFINITY, l_run = 0.f;
+    v4f_t acc[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[n] = v4f_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < P - 1; ++t)
+        if (t < ntiles) issue(t);
+    for (int t = 0; t < ntiles; ++t) {
+        if (t + P - 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (P - 2)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (t + P - 1 < ntiles) issue(t + P - 1);  // the slot of tile t - 1, read before this barrier
+        const uint8_t* st = ring + (t % P) * 16384;
+        uint4 kr[2][4], vr[8];
+#pragma unroll
+        for (int tau = 0; tau < 2; ++tau)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) kr[tau][c] = *reinterpret_cast<const uint4*>(st + (tau * 4 + c) * 1024 + lane * 16);
+#pragma unroll
+        for (int n = 0; n < 8; ++n) vr[n] = *reinterpret_cast<const uint4*>(st + (8 + n) * 1024 + lane * 16);
+        const int bs = 32 * t;
+        v4f_t sc[2];
+#pragma unroll
+        for (int tau = 0; tau < 2; ++tau) {
+            sc[tau] = v4f_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                sc[tau] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8s_t, kr[tau][c]), qf[c], sc[tau],
+                                                                  0, 0, 0);
+        }
+        const int lim = lim_c - bs - 8 * q4;
+        float x[8], mx = -INFINITY;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            x[e] = e < lim ? sc[e >> 2][e & 3] * sm_scale : -INFINITY;
+            mx = fmaxf(mx, x[e]);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mnew = fmaxf(m_run, mx);  // finite: key 0 is valid for every column
+        const float alpha = __expf(m_run - mnew);
+        m_run = mnew;
+        float p[8], ps = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            p[e] = __expf(x[e] - mnew);
+            ps += p[e];
+        }
+        l_run = l_run * alpha + ps;
+        uint32_t hi[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hi[j] = pk_bf16(p[2 * j], p[2 * j + 1]);
+        const v8s_t ph = __builtin_bit_cast(v8s_t, make_uint4(hi[0], hi[1], hi[2], hi[3]));
+        const bool resc = __any(alpha != 1.0f);
+        float ar[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ar[r] = __shfl(alpha, 4 * q4 + r, 64);
+        const int limv = lim_b - bs - 8 * q4;  // V rows past the block's last position: zero (stale)
+        uint32_t vm[4] = {~0u, ~0u, ~0u, ~0u};
+        if (limv < 8) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) vm[j] = (2 * j < limv ? 0xffffu : 0u) | (2 * j + 1 < limv ? 0xffff0000u : 0u);
+        }
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+            if (resc) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[n][r] *= ar[r];
+            }
+            const v8s_t vf =
+                __builtin_bit_cast(v8s_t, make_uint4(vr[n].x & vm[0], vr[n].y & vm[1], vr[n].z & vm[2], vr[n].w & vm[3]));
+            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vf, acc[n], 0, 0, 0);
+        }
+    }
+    l_run += __shfl_xor(l_run, 16, 64);
+    l_run += __shfl_xor(l_run, 32, 64);
+    const int row = r0 + q4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float inv = 1.0f / __shfl(l_run, 4 * q4 + r, 64);
+        if (row < M) {
+#pragma unroll
+            for (int n = 0; n < 8; ++n)
+                out[(int64_t)row * o_rs + (int64_t)(hq0 + r) * D + 16 * n + l16] = f2bf(rbf(acc[n][r] * inv));
+        }
+    }
+}
+
 int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                       int64_t kv_sh, int Hq, int Hkv, const int32_t* row_pos, const int32_t* row_slot, int M,
                       float sm_scale, const int32_t* pt, int pps, int npages, int64_t kv_pgs, uint16_t* out,
@@ -814,11 +960,19 @@ int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const 
         set_error("prefill_attention: GQA group %d != 4 not supported", Hq / Hkv);
         return WF_EINVAL;
     }
-    // one column group per wave at 2 waves / SIMD: measured faster than two groups per wave
-    // (spills at 256 VGPRs, or 1 wave / SIMD without them) -- the kernel is latency-bound per tile
-    constexpr int CG = 1;
-    hipLaunchKernelGGL((k_attn_prefill<CG, 2>), dim3((M + 16 * CG - 1) / (16 * CG), Hkv), dim3(256), 0, st, q, q_rs, k,
-                       v, kv_sb, kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale, pt, pps, npages, kv_pgs, out, o_rs);
+    if (pps > kPfMaxTiles && getenv("WF_PF_ATTN") && atoi(getenv("WF_PF_ATTN")) == 2) {
+        set_error("prefill_attention: the LDS-staged kernel supports max_seq <= %d", 32 * kPfMaxTiles);
+        return WF_EINVAL;
+    }
+    // registers-only kernel by default; the LDS-staged one (WF_PF_ATTN=2, study) measured the same
+    // speed at 8 x 2048 (66.8 vs 66.0 ms per prefill) with 4x less L2 traffic
+    static const int var = getenv("WF_PF_ATTN") ? atoi(getenv("WF_PF_ATTN")) : 0;
+    if (var == 2)
+        hipLaunchKernelGGL((k_attn_prefill_lds<kPfStages>), dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v,
+                           kv_sb, kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale, pt, pps, npages, kv_pgs, out, o_rs);
+    else
+        hipLaunchKernelGGL((k_attn_prefill<1, 2>), dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v, kv_sb,
+                           kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale, pt, pps, npages, kv_pgs, out, o_rs);
     return check_launch("prefill_attention");
 }
 

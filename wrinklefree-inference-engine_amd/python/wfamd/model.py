@@ -189,6 +189,23 @@ def from_kv_tiles(kt: torch.Tensor, vt: torch.Tensor):
     return k.reshape(*lead, S, D).contiguous(), v.reshape(*lead, S, D).contiguous()
 
 
+def pack_prefill_rows(seqs, group: int = _lib.WF_PREFILL_ROW_GROUP):
+    """(slot, tokens, start) triples -> the row arrays of wf_model_prefill (tokens, slots,
+    positions): each slot's tokens at positions start, start + 1, ..., padded to a multiple of
+    `group` rows by repeating its last (token, position) -- a repeat recomputes the same K/V row, so
+    the pad is harmless -- so that every aligned group of `group` rows belongs to one slot."""
+    tok, slot, pos = [], [], []
+    for b, toks, start in seqs:
+        n = len(toks)
+        if n == 0:
+            continue
+        pad = (-n) % group
+        tok += list(toks) + [toks[-1]] * pad
+        pos += list(range(start, start + n)) + [start + n - 1] * pad
+        slot += [b] * (n + pad)
+    return tok, slot, pos
+
+
 class PagePool:
     """Host-side free list of KV pages, with the semantics of sgl_kernel.kvcache.KVCacheManager's
     allocator (tests/test_kv_cache_cpp.py:283-373: allocate_pages(n) -> int32 ids, empty when the
@@ -318,20 +335,13 @@ class BitNetDecoder:
         slot's cache (pages reserved on demand). Rows are packed per slot, padded to a multiple of
         WF_PREFILL_ROW_GROUP by repeating the slot's last token, and run `chunk_rows` at a time. The decode state
         (tokens / positions / logits) is left alone: see admit()."""
-        tok, slot, pos = [], [], []
+        seqs = [(int(b), [int(t) for t in toks], int(start)) for b, toks, start in seqs]
         for b, toks, start in seqs:
-            toks = [int(t) for t in toks]
-            n = len(toks)
-            if n == 0:
-                continue
-            if start + n > self.cfg.max_seq:
-                raise ValueError(f"slot {b}: positions up to {start + n} exceed max_seq {self.cfg.max_seq}")
-            if self.paged:
-                self.reserve(b, start + n)
-            pad = (-n) % _lib.WF_PREFILL_ROW_GROUP
-            tok += toks + [toks[-1]] * pad
-            pos += list(range(start, start + n)) + [start + n - 1] * pad
-            slot += [int(b)] * (n + pad)
+            if start + len(toks) > self.cfg.max_seq:
+                raise ValueError(f"slot {b}: positions up to {start + len(toks)} exceed max_seq {self.cfg.max_seq}")
+            if self.paged and toks:
+                self.reserve(b, start + len(toks))
+        tok, slot, pos = pack_prefill_rows(seqs)
         rows = len(tok)
         if rows == 0:
             return
