@@ -49,6 +49,8 @@ def parse():
                          "config 4), on paged KV")
     ap.add_argument("--paged", action="store_true", help="paged KV (32-token pages; batch >= 16)")
     ap.add_argument("--no-gemv", action="store_true", help="skip the standalone GEMV benchmark")
+    ap.add_argument("--kv", choices=["bf16", "fp8"], default="bf16",
+                    help="K/V cache element type (fp8 = OCP e4m3fn, batch >= 16; scale 1.0)")
     return ap.parse_args()
 
 
@@ -256,7 +258,8 @@ def main():
         ctxs = np.full(B, ctx, dtype=np.int64)
     num_pages = int(sum((c + total + 1 + 31) // 32 for c in ctxs)) if paged else 0
     w = synthetic_weights(cfg, seed=0, device="cuda")
-    dec = BitNetDecoder(cfg, w, batch=B, wfmt=wfmt, num_pages=num_pages, page_seed=0 if paged else None)
+    dec = BitNetDecoder(cfg, w, batch=B, wfmt=wfmt, num_pages=num_pages, page_seed=0 if paged else None,
+                        kv_dtype=args.kv)
     del w
     torch.cuda.empty_cache()
     if paged:
@@ -281,7 +284,7 @@ def main():
         traffic = None
         pmc = ROOT / "profiles" / ("pmc_traffic.json" if B < 16 else f"pmc_traffic_b{B}.json")
         # the PMC files are measured on the fixed-context workload (tools/profile_round.sh)
-        if pmc.exists() and args.ctx_dist == "fixed":
+        if pmc.exists() and args.ctx_dist == "fixed" and args.kv == "bf16":
             try:
                 traffic = json.loads(pmc.read_text()).get(dom_name, {}).get("hbm_bytes_per_launch")
             except Exception:
@@ -289,7 +292,8 @@ def main():
         roof = {"bound": "hbm", "achieved": dom["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom_name,
                 "bytes_per_launch": dom["bytes"], "us_per_launch": dom["us"]}
-    step_bytes = cfg.weight_bytes_per_token(wfmt) + B * cfg.kv_bytes_per_token(ctx + total // 2)
+    kv_esz = 1 if args.kv == "fp8" else 2
+    step_bytes = cfg.weight_bytes_per_token(wfmt) + B * cfg.kv_bytes_per_token(ctx + total // 2) * kv_esz // 2
     gemv = None if (args.no_gemv or B != 1) else gemv_bench()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -311,7 +315,7 @@ def main():
                        "model": "bitnet-b1.58-2B-4T (random init)", "global_batch": B * world, "seq_len": ctx,
                        "parallelism": f"replicas{world}", "weights": "ternary " + ("TQ ~1.6-bit" if wfmt else "I2_S 2-bit"),
                        "activations": "int8 per-token", "lm_head": "bf16",
-                       "kv": "bf16, paged (32-token pages)" if paged else "bf16",
+                       "kv": args.kv + (", paged (32-token pages)" if paged else ""),
                        **({"ctx_mean": ctx, "ctx_min": int(ctxs.min()), "ctx_max": int(ctxs.max())}
                           if args.ctx_dist == "uniform" else {})},
             "step_hbm_gbs": round(step_bytes / (ms_step / 1000.0) / 1e9, 1),

@@ -190,6 +190,14 @@ typedef struct {
      * page_table == NULL keeps the dense layout. */
     const int32_t* page_table;
     int num_pages;
+    /* FP8 K/V (optional; same decoders as paged KV): kv_fp8 = 1 stores K and V as OCP e4m3fn bytes,
+     * code = e4m3(clamp(v / scale, +-448)) (RNE), in the same tile layouts / pages with one byte per
+     * element -- half the attention bytes. kv_scale: HOST [layers][2] (K, V) scales (NULL = 1.0),
+     * copied at create; the attention widens codes to bf16 exactly and folds the scales into the
+     * score scale and the partial sums. The reference's INT8/"FP8" KVCache option
+     * (kv_cache/kv_cache.py:159-218) is the analogue; quality bar cosine >= 0.998 vs bf16 K/V. */
+    int kv_fp8;
+    const float* kv_scale;
 } wf_model_desc;
 
 typedef struct wf_model wf_model;

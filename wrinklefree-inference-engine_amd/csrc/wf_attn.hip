@@ -481,14 +481,60 @@ constexpr int kAttnMfmaMaxGrp = 8;
 // WREC: one partial record per WAVE instead of per block -- grid.x = kAttnPartSplits / 4, the 8
 // waves of (b, g) take the 32-key tiles round-robin (wave r: tiles r, r + 8, ...) and each writes
 // its own (m, l, o) record: no LDS merge or barrier, and a wave streams several tiles per launch.
-template <bool DB, bool RR, bool WREC = false>
+// FP8 (OCP e4m3fn) K/V caches: a fragment is 8 one-byte keys / dims (8 bytes per lane, 512
+// contiguous bytes per wave-instruction), widened to bf16 in registers (exact: every e4m3 value is
+// a bf16 value). The per-layer scales are folded into the score scale (K) and the partial records
+// (V), so the arithmetic after the widening is the bf16 path's.
+typedef __bf16 v2bf_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 fp8x8_to_bf16(uint2 r) {
+    const v2bf_t a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(r.x, 1.0f, false);
+    const v2bf_t b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(r.x, 1.0f, true);
+    const v2bf_t c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(r.y, 1.0f, false);
+    const v2bf_t d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(r.y, 1.0f, true);
+    return make_uint4(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, c),
+                      __builtin_bit_cast(uint32_t, d));
+}
+template <bool KV8>
+struct KvFrag {
+    using T = uint4;  // 8 bf16
+    __device__ static __forceinline__ T ld(const uint16_t* base, int64_t elem) {
+        return *reinterpret_cast<const uint4*>(base + elem);
+    }
+    __device__ static __forceinline__ uint4 bf(const T& t) { return t; }
+    // zero the keys >= lim of a V fragment (8 keys)
+    __device__ static __forceinline__ T mask(const T& t, int lim) {
+        if (lim >= 8) return t;
+        uint32_t vm[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) vm[j] = (2 * j < lim ? 0xffffu : 0u) | (2 * j + 1 < lim ? 0xffff0000u : 0u);
+        return make_uint4(t.x & vm[0], t.y & vm[1], t.z & vm[2], t.w & vm[3]);
+    }
+};
+template <>
+struct KvFrag<true> {
+    using T = uint2;  // 8 fp8
+    __device__ static __forceinline__ T ld(const uint16_t* base, int64_t elem) {
+        return *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(base) + elem);
+    }
+    __device__ static __forceinline__ uint4 bf(const T& t) { return fp8x8_to_bf16(t); }
+    __device__ static __forceinline__ T mask(const T& t, int lim) {
+        if (lim >= 8) return t;
+        const uint64_t m = lim <= 0 ? 0ull : (~0ull >> (8 * (8 - lim)));
+        return make_uint2(t.x & (uint32_t)m, t.y & (uint32_t)(m >> 32));
+    }
+};
+
+template <bool DB, bool RR, bool WREC = false, bool KV8 = false>
 __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* __restrict__ q, int64_t q_sb,
                                                    const uint16_t* __restrict__ K, const uint16_t* __restrict__ Vt,
                                                    int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv, int S,
                                                    const int32_t* __restrict__ seq_lens, float sm_scale,
                                                    float2* __restrict__ ml_out, float* __restrict__ o_out,
-                                                   const int32_t* __restrict__ pt, int pps, int npages, int64_t kv_pgs) {
+                                                   const int32_t* __restrict__ pt, int pps, int npages, int64_t kv_pgs,
+                                                   float v_scale) {
     constexpr int D = 128;
+    using KF = KvFrag<KV8>;
+    using FT = typename KF::T;
     const int s = WREC ? 4 * (int)blockIdx.x + (int)(threadIdx.x >> 6) : (int)blockIdx.x, g = blockIdx.y, b = blockIdx.z;
     const int grp = Hq / Hkv, hq0 = g * grp;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
@@ -503,8 +549,8 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
     __shared__ __attribute__((aligned(16))) float sm_o[4][kAttnMfmaMaxGrp][D];
     // dense: (sequence, kv head) slab of S / 32 blocks; paged: block j of sequence b in page
     // pt[b][j] (kv_sb = 0, kv_sh = the kv head stride inside a page)
-    const uint16_t* Kb = K + b * kv_sb + g * kv_sh + lane * 8;
-    const uint16_t* Vb = Vt + b * kv_sb + g * kv_sh + lane * 8;
+    // (element offsets: the fragment loaders scale them by the element size)
+    const int64_t kvo = b * kv_sb + g * kv_sh + lane * 8;
     const int32_t* ptb = pt ? pt + (int64_t)b * pps : nullptr;
     WF_STAMP(0);
 
@@ -524,27 +570,26 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
                 qf[c] = __builtin_bit_cast(v8s_t, t);
             }
         }
-        auto load = [&](uint4 (&kr)[2][4], uint4 (&vr)[8], int bs) {
+        auto load = [&](FT (&kr)[2][4], FT (&vr)[8], int bs) {
             // 32 keys x 128 dims per tile block (bs is wave-uniform: the page id is a scalar load)
             const int64_t blk = ptb ? (int64_t)min(max(ptb[__builtin_amdgcn_readfirstlane(bs) >> 5], 0), npages - 1) * kv_pgs
                                     : (int64_t)(bs >> 5) * 4096;
 #pragma unroll
             for (int tau = 0; tau < 2; ++tau)
 #pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    kr[tau][c] = *reinterpret_cast<const uint4*>(Kb + blk + (tau * 4 + c) * 512);
+                for (int c = 0; c < 4; ++c) kr[tau][c] = KF::ld(K, kvo + blk + (tau * 4 + c) * 512);
 #pragma unroll
-            for (int n = 0; n < 8; ++n) vr[n] = *reinterpret_cast<const uint4*>(Vb + blk + n * 512);
+            for (int n = 0; n < 8; ++n) vr[n] = KF::ld(Vt, kvo + blk + n * 512);
         };
-        auto compute = [&](const uint4 (&kr)[2][4], const uint4 (&vr)[8], int bs) {
+        auto compute = [&](const FT (&kr)[2][4], const FT (&vr)[8], int bs) {
             v4f_t sc[2];
 #pragma unroll
             for (int tau = 0; tau < 2; ++tau) {
                 sc[tau] = v4f_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
-                    sc[tau] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8s_t, kr[tau][c]), qf[c],
-                                                                      sc[tau], 0, 0, 0);
+                    sc[tau] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8s_t, KF::bf(kr[tau][c])),
+                                                                      qf[c], sc[tau], 0, 0, 0);
             }
             const int lim = t1 - bs - 8 * q4;  // valid keys among this lane's 8
             float x[8], mx = -INFINITY;
@@ -576,25 +621,19 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
             float ar[4];  // rescale factor of output row (head) 4 q4 + r
 #pragma unroll
             for (int r = 0; r < 4; ++r) ar[r] = __shfl(alpha, 4 * q4 + r, 64);
-            uint32_t vm[4] = {~0u, ~0u, ~0u, ~0u};
-            if (lim < 8) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) vm[j] = (2 * j < lim ? 0xffffu : 0u) | (2 * j + 1 < lim ? 0xffff0000u : 0u);
-            }
 #pragma unroll
             for (int n = 0; n < 8; ++n) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) acc[n][r] *= ar[r];
-                const uint4 v = make_uint4(vr[n].x & vm[0], vr[n].y & vm[1], vr[n].z & vm[2], vr[n].w & vm[3]);
-                const v8s_t vf = __builtin_bit_cast(v8s_t, v);
+                const v8s_t vf = __builtin_bit_cast(v8s_t, KF::bf(KF::mask(vr[n], lim)));
                 acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vf, acc[n], 0, 0, 0);
                 acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vf, acc[n], 0, 0, 0);
             }
         };
-        uint4 kA[2][4], vA[8];
+        FT kA[2][4], vA[8];
         load(kA, vA, base);
         if constexpr (DB) {
-            uint4 kB[2][4], vB[8];
+            FT kB[2][4], vB[8];
             for (; base < t1; base += 2 * kStride) {
                 const int nb = base + kStride;
                 if (nb < t1) load(kB, vB, nb);
@@ -613,6 +652,12 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
     WF_STAMP(1);
     l_run += __shfl_xor(l_run, 16, 64);
     l_run += __shfl_xor(l_run, 32, 64);
+    if constexpr (KV8) {  // o = v_scale * sum p v8 (the partial records carry the V scale)
+#pragma unroll
+        for (int n = 0; n < 8; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[n][r] *= v_scale;
+    }
     if constexpr (WREC) {  // this wave's record s of each of its group's heads
         const int64_t rec0 = (int64_t)(b * Hq + hq0) * kAttnPartSplits + s;
 #pragma unroll
@@ -670,15 +715,18 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
 // position are zeroed (stale pages). Each wave streams its whole key
 // range and writes the normalised output rows bf16(o / l) (no split partials).
 // ---------------------------------------------------------------------------------------------
-template <int CG, int OCC>
+template <int CG, int OCC, bool KV8 = false>
 __global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __restrict__ q, int64_t q_rs,
                                                          const uint16_t* __restrict__ K, const uint16_t* __restrict__ Vt,
                                                          int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv,
                                                          const int32_t* __restrict__ row_pos,
                                                          const int32_t* __restrict__ row_slot, int M, float sm_scale,
                                                          const int32_t* __restrict__ pt, int pps, int npages,
-                                                         int64_t kv_pgs, uint16_t* __restrict__ out, int64_t o_rs) {
-    constexpr int D = 128, RPW = 4 * CG;  // rows per wave: CG column groups of 4 tokens x 4 heads
+                                                         int64_t kv_pgs, uint16_t* __restrict__ out, int64_t o_rs,
+                                                         float v_scale) {
+    constexpr int D = 128, RPW = 4 * CG;
+    using KF = KvFrag<KV8>;
+    using FT = typename KF::T;  // rows per wave: CG column groups of 4 tokens x 4 heads
     const int g = blockIdx.y, hq0 = g * 4;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
     const int r0 = (blockIdx.x * 4 + wave) * RPW;  // this wave's rows
@@ -689,8 +737,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __res
     for (int u = 0; u < CG; ++u) lim_c[u] = row_pos[min(r0 + 4 * u + (l16 >> 2), M - 1)] + 1;
 #pragma unroll
     for (int t = 0; t < RPW; ++t) lim_w = max(lim_w, row_pos[min(r0 + t, M - 1)] + 1);
-    const uint16_t* Kb = K + (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;
-    const uint16_t* Vb = Vt + (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;
+    const int64_t kvo = (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;  // element offset
     const int32_t* ptb = pt ? pt + (int64_t)slot * pps : nullptr;
 
     v8s_t qf[CG][4];
@@ -701,15 +748,15 @@ __global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __res
 #pragma unroll
         for (int c = 0; c < 4; ++c) qf[u][c] = __builtin_bit_cast(v8s_t, *reinterpret_cast<const uint4*>(qp + 32 * c));
     }
-    auto load = [&](uint4 (&kr)[2][4], uint4 (&vr)[8], int bs) {
+    auto load = [&](FT (&kr)[2][4], FT (&vr)[8], int bs) {
         const int64_t blk = ptb ? (int64_t)min(max(ptb[__builtin_amdgcn_readfirstlane(bs) >> 5], 0), npages - 1) * kv_pgs
                                 : (int64_t)(bs >> 5) * 4096;
 #pragma unroll
         for (int tau = 0; tau < 2; ++tau)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) kr[tau][c] = *reinterpret_cast<const uint4*>(Kb + blk + (tau * 4 + c) * 512);
+            for (int c = 0; c < 4; ++c) kr[tau][c] = KF::ld(K, kvo + blk + (tau * 4 + c) * 512);
 #pragma unroll
-        for (int n = 0; n < 8; ++n) vr[n] = *reinterpret_cast<const uint4*>(Vb + blk + n * 512);
+        for (int n = 0; n < 8; ++n) vr[n] = KF::ld(Vt, kvo + blk + n * 512);
     };
     float m_run[CG], l_run[CG];
     v4f_t acc[CG][8];
@@ -720,7 +767,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __res
 #pragma unroll
         for (int n = 0; n < 8; ++n) acc[u][n] = v4f_t{0.f, 0.f, 0.f, 0.f};
     }
-    uint4 kA[2][4], vA[8];
+    FT kA[2][4], vA[8];
     load(kA, vA, 0);
     for (int bs = 0; bs < lim_w; bs += 32) {
         v8s_t ph[CG];
@@ -734,8 +781,8 @@ __global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __res
                 sc[tau] = v4f_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
-                    sc[tau] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8s_t, kA[tau][c]), qf[u][c],
-                                                                      sc[tau], 0, 0, 0);
+                    sc[tau] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8s_t, KF::bf(kA[tau][c])),
+                                                                      qf[u][c], sc[tau], 0, 0, 0);
             }
             const int lim = lim_c[u] - bs - 8 * q4;  // valid keys of column l16 among this lane's 8
             float x[8], mx = -INFINITY;
@@ -767,15 +814,9 @@ __global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __res
             for (int r = 0; r < 4; ++r) ar[u][r] = __shfl(alpha, 4 * q4 + r, 64);
         }
         const int limv = lim_w - bs - 8 * q4;  // V rows past every column's limit: zero (stale)
-        uint32_t vm[4] = {~0u, ~0u, ~0u, ~0u};
-        if (limv < 8) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) vm[j] = (2 * j < limv ? 0xffffu : 0u) | (2 * j + 1 < limv ? 0xffff0000u : 0u);
-        }
         v8s_t vf[8];
 #pragma unroll
-        for (int n = 0; n < 8; ++n)
-            vf[n] = __builtin_bit_cast(v8s_t, make_uint4(vA[n].x & vm[0], vA[n].y & vm[1], vA[n].z & vm[2], vA[n].w & vm[3]));
+        for (int n = 0; n < 8; ++n) vf[n] = __builtin_bit_cast(v8s_t, KF::bf(KF::mask(vA[n], limv)));
         if (bs + 32 < lim_w) load(kA, vA, bs + 32);  // next tile in flight during the P.V MFMAs
 #pragma unroll
         for (int u = 0; u < CG; ++u)
@@ -787,6 +828,14 @@ __global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __res
                 }
                 acc[u][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph[u], vf[n], acc[u][n], 0, 0, 0);
             }
+    }
+    if constexpr (KV8) {
+#pragma unroll
+        for (int u = 0; u < CG; ++u)
+#pragma unroll
+            for (int n = 0; n < 8; ++n)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[u][n][r] *= v_scale;
     }
     // acc[u] rows 4 q4 + r = column (token 4u + q4, head r); its l sits in lane 4 q4 + r
 #pragma unroll
@@ -955,7 +1004,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_lds(const uint16_t* __r
 int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                       int64_t kv_sh, int Hq, int Hkv, const int32_t* row_pos, const int32_t* row_slot, int M,
                       float sm_scale, const int32_t* pt, int pps, int npages, int64_t kv_pgs, uint16_t* out,
-                      int64_t o_rs, hipStream_t st) {
+                      int64_t o_rs, hipStream_t st, int kv8, float k_scale, float v_scale) {
     if (Hq != 4 * Hkv) {
         set_error("prefill_attention: GQA group %d != 4 not supported", Hq / Hkv);
         return WF_EINVAL;
@@ -967,19 +1016,23 @@ int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const 
     // registers-only kernel by default; the LDS-staged one (WF_PF_ATTN=2, study) measured the same
     // speed at 8 x 2048 (66.8 vs 66.0 ms per prefill) with 4x less L2 traffic
     static const int var = getenv("WF_PF_ATTN") ? atoi(getenv("WF_PF_ATTN")) : 0;
-    if (var == 2)
+    if (kv8)
+        hipLaunchKernelGGL((k_attn_prefill<1, 2, true>), dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v, kv_sb,
+                           kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale * k_scale, pt, pps, npages, kv_pgs, out, o_rs,
+                           v_scale);
+    else if (var == 2)
         hipLaunchKernelGGL((k_attn_prefill_lds<kPfStages>), dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v,
                            kv_sb, kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale, pt, pps, npages, kv_pgs, out, o_rs);
     else
         hipLaunchKernelGGL((k_attn_prefill<1, 2>), dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v, kv_sb,
-                           kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale, pt, pps, npages, kv_pgs, out, o_rs);
+                           kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale, pt, pps, npages, kv_pgs, out, o_rs, 1.0f);
     return check_launch("prefill_attention");
 }
 
 int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
                               float2* ml, float* o, hipStream_t st, bool kv_tiled, const int32_t* pt, int pps,
-                              int npages, int64_t kv_pgs) {
+                              int npages, int64_t kv_pgs, int kv8, float k_scale, float v_scale) {
     const int grp = Hq / Hkv;
     if (grp > 8) {
         set_error("decode_attention_partials: GQA group %d > 8", grp);
@@ -1001,22 +1054,27 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
             return WF_EINVAL;
         }
         static const int variant = getenv("WF_ATTN_VARIANT") ? atoi(getenv("WF_ATTN_VARIANT")) : 0;
+        if (kv8) {  // FP8 caches: the default schedule, K scale folded into the score scale
+            hipLaunchKernelGGL((k_attn_mfma<false, false, false, true>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
+                               kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale, ml, o, pt, pps, npages, kv_pgs, v_scale);
+            return check_launch("decode_attention_partials");
+        }
         const dim3 wgrid(kAttnPartSplits / 4, Hkv, B);
         if (variant == 3)
             hipLaunchKernelGGL((k_attn_mfma<false, false, true>), wgrid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq,
-                               Hkv, S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs);
+                               Hkv, S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs, 1.0f);
         else if (variant == 4)
             hipLaunchKernelGGL((k_attn_mfma<true, false, true>), wgrid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq,
-                               Hkv, S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs);
+                               Hkv, S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs, 1.0f);
         else if (variant == 1)
             hipLaunchKernelGGL((k_attn_mfma<false, true>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv,
-                               S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs);
+                               S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs, 1.0f);
         else if (variant == 2)
             hipLaunchKernelGGL((k_attn_mfma<true, false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv,
-                               S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs);
+                               S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs, 1.0f);
         else
             hipLaunchKernelGGL((k_attn_mfma<false, false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq,
-                               Hkv, S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs);
+                               Hkv, S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs, 1.0f);
         return check_launch("decode_attention_partials");
     }
 #define WF_AP(GV)                                                                                                   \

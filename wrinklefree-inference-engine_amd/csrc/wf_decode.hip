@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <new>
 
 #include "wf_common.h"
@@ -30,11 +31,12 @@ namespace wf {
 int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                       int64_t kv_sh, int Hq, int Hkv, const int32_t* row_pos, const int32_t* row_slot, int M,
                       float sm_scale, const int32_t* pt, int pps, int npages, int64_t kv_pgs, uint16_t* out,
-                      int64_t o_rs, hipStream_t st);
+                      int64_t o_rs, hipStream_t st, int kv8, float k_scale, float v_scale);
 int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
                               float2* ml, float* o, hipStream_t st, bool kv_tiled, const int32_t* pt = nullptr,
-                              int pps = 0, int npages = 0, int64_t kv_pgs = 0);
+                              int pps = 0, int npages = 0, int64_t kv_pgs = 0, int kv8 = 0, float k_scale = 1.f,
+                              float v_scale = 1.f);
 
 enum { MODE_QKV = 0, MODE_O = 1, MODE_GU = 2, MODE_DN = 3, MODE_LINEAR = 4 };  // LINEAR: BitNetLinear drop-in
 constexpr int kNT = 512;  // threads per GEMV / row-norm block (8 waves: 2 per SIMD hide the input-stage latency)
@@ -78,7 +80,15 @@ struct GemvArgs {
     int64_t kv_pgs;
     // prefill: row m of the GEMM is a token of KV slot row_slot[m] (nullptr: row m = slot m)
     const int32_t* row_slot;
+    // FP8 (e4m3fn) K/V cache: stored code = e4m3(clamp(y / scale, +-448)), RNE
+    int kv8;
+    float k_inv, v_inv;
 };
+
+__device__ __forceinline__ uint8_t to_fp8(float y) {
+    const float c = fminf(fmaxf(y, -448.f), 448.f);
+    return (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(c, c, 0, false) & 0xffu);
+}
 
 // Reference correction (direct_inference_full.py:201-208) for one output:
 // raw = fl32(S * f(ws)); c = f(ws * act_sum); out = fl32(fl32(raw - c) * f(s))
@@ -430,6 +440,19 @@ struct EpiDec {
                     } else {
                         const int kvh = head - g.Hq - (proj == 2 ? g.Hkv : 0);
                         const int slot = g.row_slot ? g.row_slot[m] : m;
+                        if (g.kv8) {  // FP8 tile-layout cache (element offsets are byte offsets)
+                            uint8_t* c8 = reinterpret_cast<uint8_t*>(proj == 1 ? g.kc : g.vc);
+                            int64_t off;
+                            if (g.pt) {
+                                const int pg = min(max(g.pt[(int64_t)slot * g.pps + (pos >> 5)], 0), g.npages - 1);
+                                off = pg * g.kv_pgs + (int64_t)kvh * 4096 + (proj == 1 ? k_tile_off(pos & 31, d) : v_tile_off(pos & 31, d));
+                            } else {
+                                off = (int64_t)slot * g.kv_b_stride + (int64_t)kvh * g.S * 128 +
+                                      (proj == 1 ? k_tile_off(pos, d) : v_tile_off(pos, d));
+                            }
+                            c8[off] = to_fp8(y * (proj == 1 ? g.k_inv : g.v_inv));
+                            continue;
+                        }
                         if (g.pt) {  // paged: block pos >> 5 lives in page pt[slot][pos >> 5]
                             const int pg = min(max(g.pt[(int64_t)slot * g.pps + (pos >> 5)], 0), g.npages - 1);
                             uint16_t* cache = (proj == 1 ? g.kc : g.vc) + pg * g.kv_pgs + (int64_t)kvh * 4096;
@@ -1234,6 +1257,7 @@ struct wf_model {
     int64_t q8_stride = 0;
     int kv_tiled = 0;  // batched MFMA decode: K/V caches in the tile layouts (include/wf_bitnet.h)
     uint16_t* embed_t = nullptr;  // batched LM head: the tied embedding in the fragment layout (copy)
+    float* kv_scale = nullptr;    // host copy of the FP8 K/V scales [layers][2] (1.0 when bf16)
     // prefill workspace (wf_model_prefill_reserve): rows of prompt tokens
     int pf_rows = 0;
     uint16_t *pf_h_a = nullptr, *pf_h_b = nullptr, *pf_q = nullptr, *pf_attn = nullptr, *pf_act = nullptr;
@@ -1383,8 +1407,13 @@ GemvArgs base_args(const wf_model* m, int l) {
     a.pps = d.max_seq / 32;
     a.npages = d.num_pages;
     a.kv_pgs = (int64_t)d.n_kv_heads * 32 * d.head_dim;
-    a.kc = m->k_cache + l * kvl;
-    a.vc = m->v_cache + l * kvl;
+    // FP8 caches hold one byte per element: the layer offset is in bytes, the kernels index bytes
+    const int64_t esz = d.kv_fp8 ? 1 : 2;
+    a.kc = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(m->k_cache) + l * kvl * esz);
+    a.vc = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(m->v_cache) + l * kvl * esz);
+    a.kv8 = d.kv_fp8;
+    a.k_inv = d.kv_fp8 ? 1.0f / m->kv_scale[2 * l] : 1.0f;
+    a.v_inv = d.kv_fp8 ? 1.0f / m->kv_scale[2 * l + 1] : 1.0f;
     a.kv_b_stride = (int64_t)d.n_kv_heads * d.max_seq * d.head_dim;
     a.kv_t = m->kv_tiled;
     return a;
@@ -1424,10 +1453,12 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             if (a.pt)  // paged pool: kv head stride 32 * D inside a page
                 return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, 0, 32 * D, B, d.n_heads,
                                                  d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D), m->part_ml,
-                                                 m->part_o, st, true, a.pt, a.pps, a.npages, a.kv_pgs);
+                                                 m->part_o, st, true, a.pt, a.pps, a.npages, a.kv_pgs, d.kv_fp8,
+                                                 m->kv_scale[2 * l], m->kv_scale[2 * l + 1]);
             return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, a.kv_b_stride, (int64_t)S * D,
                                              B, d.n_heads, d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D),
-                                             m->part_ml, m->part_o, st, m->kv_tiled != 0);
+                                             m->part_ml, m->part_o, st, m->kv_tiled != 0, nullptr, 0, 0, 0, d.kv_fp8,
+                                             d.kv_fp8 ? m->kv_scale[2 * l] : 1.f, d.kv_fp8 ? m->kv_scale[2 * l + 1] : 1.f);
         case WF_OP_O:  // h_b = h_a + o_proj(rms_norm(attn_sub_norm)(attn))
             a.w = d.w_o + (int64_t)l * H * wrow_bytes(d.wfmt, H); a.N = H; a.K = H; a.ws0 = wsh[3];
             a.resid = m->h_a; a.out = m->h_b; a.out_stride = H;
@@ -1546,6 +1577,20 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_ALLOC(m->h_b, 2 * (size_t)B * d.hidden);
     WF_ALLOC(m->qbuf, 2 * (size_t)B * d.hidden);
     m->kv_tiled = (B >= kDecMfmaMinB && (d.wfmt == WF_FMT_I2S || d.wfmt == WF_FMT_I2S_MFMA) && d.max_seq % 32 == 0) ? 1 : 0;
+    m->kv_scale = new float[2 * d.layers];
+    for (int i = 0; i < 2 * d.layers; ++i) m->kv_scale[i] = (d.kv_fp8 && d.kv_scale) ? d.kv_scale[i] : 1.0f;
+    if (d.kv_fp8 && !(m->kv_tiled && d.head_dim == 128)) {
+        set_error("model_create: FP8 K/V needs the batched matrix-core decoder (batch >= %d, I2_S, head_dim 128, "
+                  "max_seq %% 32 == 0)", kDecMfmaMinB);
+        wf_model_destroy(m);
+        return WF_EINVAL;
+    }
+    for (int i = 0; i < 2 * d.layers; ++i)
+        if (!(m->kv_scale[i] > 0.f) || !std::isfinite(m->kv_scale[i])) {
+            set_error("model_create: FP8 K/V scales must be positive and finite");
+            wf_model_destroy(m);
+            return WF_EINVAL;
+        }
     if (d.page_table && !(m->kv_tiled && d.head_dim == 128 && d.num_pages >= 1)) {
         set_error("model_create: paged KV needs batch >= %d, I2_S weights, head_dim 128, max_seq %% 32 == 0 and "
                   "num_pages >= 1", kDecMfmaMinB);
@@ -1592,6 +1637,7 @@ int wf_model_destroy(wf_model* m) {
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete[] m->d.wscale;
+    delete[] m->kv_scale;
     delete m;
     return WF_OK;
 }
@@ -1701,7 +1747,8 @@ int wf_model_prefill(wf_model* m, const int32_t* tokens, const int32_t* row_slot
         const bool paged = d.page_table != nullptr;
         if ((rc = prefill_attention(m->pf_q, H, a.kc, a.vc, paged ? 0 : a.kv_b_stride, paged ? 32 * D : (int64_t)d.max_seq * D,
                                     d.n_heads, d.n_kv_heads, row_pos, row_slot, rows, 1.0f / sqrtf((float)D), a.pt,
-                                    a.pps, a.npages, a.kv_pgs, m->pf_attn, H, st)))
+                                    a.pps, a.npages, a.kv_pgs, m->pf_attn, H, st, d.kv_fp8,
+                                    d.kv_fp8 ? m->kv_scale[2 * l] : 1.f, d.kv_fp8 ? m->kv_scale[2 * l + 1] : 1.f)))
             return rc;
         // O (+ residual)
         prefill_rownorm(m, m->pf_attn, H, d.attn_sub + (int64_t)l * H, H, rows, st);

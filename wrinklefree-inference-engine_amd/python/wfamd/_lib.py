@@ -74,7 +74,8 @@ class WFModelDesc(C.Structure):
                [(n, C.c_void_p) for n in ("embed", "final_norm", "rope_cos", "rope_sin", "ln_in", "ln_post",
                                           "attn_sub", "ffn_sub", "w_qkv", "w_o", "w_gu", "w_d", "wscale",
                                           "tokens", "positions", "logits", "k_cache", "v_cache")] + \
-               [("debug_flags", C.c_int), ("page_table", C.c_void_p), ("num_pages", C.c_int)]
+               [("debug_flags", C.c_int), ("page_table", C.c_void_p), ("num_pages", C.c_int),
+                ("kv_fp8", C.c_int), ("kv_scale", C.c_void_p)]
 
 
 class KernelError(RuntimeError):

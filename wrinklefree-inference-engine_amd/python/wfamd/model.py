@@ -189,6 +189,17 @@ def from_kv_tiles(kt: torch.Tensor, vt: torch.Tensor):
     return k.reshape(*lead, S, D).contiguous(), v.reshape(*lead, S, D).contiguous()
 
 
+def to_fp8_codes(x: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+    """bf16/fp32 values -> OCP e4m3fn codes (uint8) of clamp(x / scale, +-448), round to nearest even:
+    what the decode step's cache epilogue stores for an FP8 K/V cache."""
+    y = (x.float() / scale).clamp(-448.0, 448.0)
+    return y.to(torch.float8_e4m3fn).view(torch.uint8)
+
+
+def from_fp8_codes(c: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+    return c.view(torch.float8_e4m3fn).float() * scale
+
+
 def pack_prefill_rows(seqs, group: int = _lib.WF_PREFILL_ROW_GROUP):
     """(slot, tokens, start) triples -> the row arrays of wf_model_prefill (tokens, slots,
     positions): each slot's tokens at positions start, start + 1, ..., padded to a multiple of
@@ -245,7 +256,7 @@ class BitNetDecoder:
 
     def __init__(self, cfg: BitNetConfig, weights: Dict[str, torch.Tensor], batch: int = 1,
                  wfmt: int = WF_FMT_I2S, device="cuda", debug_flags: int = 0, num_pages: int = 0,
-                 page_seed: Optional[int] = None):
+                 page_seed: Optional[int] = None, kv_dtype: str = "bf16", kv_scale=None):
         self.cfg, self.batch, self.wfmt = cfg, batch, wfmt
         self.dev = torch.device(device)
         # batch >= 16 on I2_S runs the matrix-core GEMMs on their tile layout (same bytes, re-tiled)
@@ -278,8 +289,18 @@ class BitNetDecoder:
             self.page_table = torch.zeros((B, cfg.max_seq // 32), dtype=torch.int32, device=self.dev)
         else:
             kv_shape = (L, B, cfg.n_kv_heads, cfg.max_seq, cfg.head_dim)
-        self.k_cache = torch.zeros(kv_shape, dtype=torch.bfloat16, device=self.dev)
-        self.v_cache = torch.zeros(kv_shape, dtype=torch.bfloat16, device=self.dev)
+        if kv_dtype not in ("bf16", "fp8"):
+            raise ValueError(f"kv_dtype must be 'bf16' or 'fp8', got {kv_dtype!r}")
+        self.kv_fp8 = kv_dtype == "fp8"
+        if self.kv_fp8 and not self.kv_tiled:
+            raise ValueError("FP8 K/V needs the batched matrix-core decoder (batch >= 16, I2_S, max_seq % 32 == 0)")
+        # FP8: OCP e4m3fn codes as uint8, per-layer (K, V) scales (include/wf_bitnet.h kv_fp8)
+        sc = np.ones((L, 2), dtype=np.float32) if kv_scale is None else np.broadcast_to(
+            np.asarray(kv_scale, dtype=np.float32), (L, 2)).copy()
+        self.kv_scale = torch.from_numpy(np.ascontiguousarray(sc))
+        kv_dt = torch.uint8 if self.kv_fp8 else torch.bfloat16
+        self.k_cache = torch.zeros(kv_shape, dtype=kv_dt, device=self.dev)
+        self.v_cache = torch.zeros(kv_shape, dtype=kv_dt, device=self.dev)
         d = WFModelDesc()
         d.hidden, d.layers, d.n_heads, d.n_kv_heads = cfg.hidden, L, cfg.n_heads, cfg.n_kv_heads
         d.head_dim, d.inter, d.vocab, d.max_seq, d.batch = cfg.head_dim, cfg.inter, cfg.vocab, cfg.max_seq, B
@@ -295,6 +316,8 @@ class BitNetDecoder:
         d.debug_flags = int(debug_flags)
         if self.paged:
             d.page_table, d.num_pages = self.page_table.data_ptr(), int(num_pages)
+        if self.kv_fp8:
+            d.kv_fp8, d.kv_scale = 1, self.kv_scale.data_ptr()
         self._desc = d
         h = C.c_void_p()
         call("wf_model_create", C.addressof(d), C.addressof(h))
@@ -378,6 +401,12 @@ class BitNetDecoder:
         order; in the tile layouts whole 32-key blocks)."""
         g = torch.Generator(device=self.dev).manual_seed(seed)
         D = self.cfg.head_dim
+        if self.kv_fp8:  # random finite e4m3 codes (the whole store: stale rows are never read)
+            for l in range(self.cfg.layers):
+                for c in (self.k_cache, self.v_cache):
+                    c[l].copy_(torch.randn(c[l].shape, generator=g, device=self.dev).to(torch.float8_e4m3fn)
+                               .view(torch.uint8))
+            return
         for l in range(self.cfg.layers):
             for c in (self.k_cache, self.v_cache):
                 if self.paged:
@@ -392,10 +421,14 @@ class BitNetDecoder:
         """Write logical K/V [B, Hkv, n, D] into positions [0, n) of a layer (any storage layout).
         Paged: only the first lengths[b] (default n) positions of sequence b, on pages reserved for them."""
         n = k.shape[2]
+        if self.kv_fp8:  # the stored codes: e4m3(clamp(x / scale)), as the step's cache epilogue writes
+            ks, vs = (float(x) for x in self.kv_scale[layer])
+            k = to_fp8_codes(k, ks)
+            v = to_fp8_codes(v, vs)
         if self.paged:
             B, H, _, D = k.shape
             nblk = (n + 31) // 32
-            kp = torch.zeros(B, H, nblk * 32, D, dtype=torch.bfloat16, device=self.dev)
+            kp = torch.zeros(B, H, nblk * 32, D, dtype=k.dtype, device=self.dev)
             vp = torch.zeros_like(kp)
             kp[:, :, :n].copy_(k)
             vp[:, :, :n].copy_(v)
@@ -443,7 +476,7 @@ class BitNetDecoder:
             _lib.WF_OP_O: self.w_o[0].numel() + B * (2 * h + 4 * h),
             _lib.WF_OP_GATE_UP: self.w_gu[0].numel() + B * (2 * h + 2 * i),
             _lib.WF_OP_DOWN: self.w_d[0].numel() + B * (2 * i + 4 * h),
-            _lib.WF_OP_ATTN: B * (2 * kv * 2 * ctx + 2 * 2 * h),
+            _lib.WF_OP_ATTN: B * (2 * kv * (1 if self.kv_fp8 else 2) * ctx + 2 * 2 * h),
             _lib.WF_OP_LM_HEAD: self.embed.numel() * 2 + B * (2 * h + 2 * cfg.vocab),
         }
         return int(per_layer.get(op, 0))
