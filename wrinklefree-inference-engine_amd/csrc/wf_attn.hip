@@ -1054,9 +1054,25 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
             return WF_EINVAL;
         }
         static const int variant = getenv("WF_ATTN_VARIANT") ? atoi(getenv("WF_ATTN_VARIANT")) : 0;
-        if (kv8) {  // FP8 caches: the default schedule, K scale folded into the score scale
-            hipLaunchKernelGGL((k_attn_mfma<false, false, false, true>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
-                               kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale, ml, o, pt, pps, npages, kv_pgs, v_scale);
+        static const int variant8 = getenv("WF_ATTN_VARIANT8") ? atoi(getenv("WF_ATTN_VARIANT8")) : 0;
+        if (kv8) {  // FP8 caches: K scale folded into the score scale
+            const dim3 wg(kAttnPartSplits / 4, Hkv, B);
+            if (variant8 == 4)
+                hipLaunchKernelGGL((k_attn_mfma<true, false, true, true>), wg, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
+                                   kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale, ml, o, pt, pps, npages, kv_pgs,
+                                   v_scale);
+            else if (variant8 == 3)
+                hipLaunchKernelGGL((k_attn_mfma<false, false, true, true>), wg, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
+                                   kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale, ml, o, pt, pps, npages, kv_pgs,
+                                   v_scale);
+            else if (variant8 == 2)
+                hipLaunchKernelGGL((k_attn_mfma<true, false, false, true>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
+                                   kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale, ml, o, pt, pps, npages, kv_pgs,
+                                   v_scale);
+            else
+                hipLaunchKernelGGL((k_attn_mfma<false, false, false, true>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
+                                   kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale, ml, o, pt, pps, npages, kv_pgs,
+                                   v_scale);
             return check_launch("decode_attention_partials");
         }
         const dim3 wgrid(kAttnPartSplits / 4, Hkv, B);
