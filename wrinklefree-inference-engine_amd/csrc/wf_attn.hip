@@ -524,7 +524,10 @@ struct KvFrag<true> {
     }
 };
 
-template <bool DB, bool RR, bool WREC = false, bool KV8 = false>
+// PAIR: records of 2 waves -- grid.x = kAttnPartSplits / 2, the 16 waves of (b, g) take the
+// tiles round-robin and each block merges its wave pairs (0, 1) and (2, 3) into 2 records: half the
+// per-tile block overheads of the 4-wave records, twice the waves per sequence of WREC.
+template <bool DB, bool RR, bool WREC = false, bool KV8 = false, bool PAIR = false>
 __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* __restrict__ q, int64_t q_sb,
                                                    const uint16_t* __restrict__ K, const uint16_t* __restrict__ Vt,
                                                    int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv, int S,
@@ -536,6 +539,7 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
     using KF = KvFrag<KV8>;
     using FT = typename KF::T;
     const int s = WREC ? 4 * (int)blockIdx.x + (int)(threadIdx.x >> 6) : (int)blockIdx.x, g = blockIdx.y, b = blockIdx.z;
+    static_assert(!(PAIR && (WREC || RR)), "one schedule");
     const int grp = Hq / Hkv, hq0 = g * grp;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
     const int Sb = min(seq_lens[b], S);
@@ -543,8 +547,9 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
     // takes tiles 4 s + w + 32 i, so per-wave tile counts differ by at most one and a block's four
     // waves finish together (a contiguous split per block left wave 0 with twice the tiles)
     const int T = ((Sb + kAttnPartSplits - 1) / kAttnPartSplits + 31) / 32 * 32;
-    const int kStride = WREC ? 32 * kAttnPartSplits : (RR ? 32 * 4 * kAttnPartSplits : 128);
-    const int t1 = (RR || WREC) ? Sb : min(s * T + T, Sb);
+    const int kStride = PAIR ? 32 * 2 * kAttnPartSplits
+                              : (WREC ? 32 * kAttnPartSplits : (RR ? 32 * 4 * kAttnPartSplits : 128));
+    const int t1 = (RR || WREC || PAIR) ? Sb : min(s * T + T, Sb);
     __shared__ float sm_m[4][kAttnMfmaMaxGrp], sm_l[4][kAttnMfmaMaxGrp];
     __shared__ __attribute__((aligned(16))) float sm_o[4][kAttnMfmaMaxGrp][D];
     // dense: (sequence, kv head) slab of S / 32 blocks; paged: block j of sequence b in page
@@ -558,7 +563,7 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
     v4f_t acc[8];
 #pragma unroll
     for (int n = 0; n < 8; ++n) acc[n] = v4f_t{0.f, 0.f, 0.f, 0.f};
-    int base = WREC ? 32 * s : (RR ? 32 * (4 * s + wave) : s * T + 32 * wave);
+    int base = PAIR ? 32 * (4 * s + wave) : (WREC ? 32 * s : (RR ? 32 * (4 * s + wave) : s * T + 32 * wave));
     if (base < t1) {
         v8s_t qf[4];
         {
@@ -681,6 +686,22 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
         for (int r = 0; r < 4; ++r)
             if (4 * q4 + r < grp) sm_o[wave][4 * q4 + r][16 * n + l16] = acc[n][r];
     __syncthreads();
+    if constexpr (PAIR) {  // waves (2p, 2p + 1) -> record 2 blockIdx.x + p
+        for (int idx = threadIdx.x; idx < 2 * grp * (D / 4); idx += 256) {
+            const int p = idx / (grp * (D / 4)), hd = idx % (grp * (D / 4));
+            const int h = hd / (D / 4), d = (hd % (D / 4)) * 4;
+            const float m0 = sm_m[2 * p][h], m1 = sm_m[2 * p + 1][h], mx = fmaxf(m0, m1);
+            const float a0 = m0 == -INFINITY ? 0.f : __expf(m0 - mx), a1 = m1 == -INFINITY ? 0.f : __expf(m1 - mx);
+            const float ls = sm_l[2 * p][h] * a0 + sm_l[2 * p + 1][h] * a1;
+            const float4 o0 = *reinterpret_cast<const float4*>(&sm_o[2 * p][h][d]);
+            const float4 o1 = *reinterpret_cast<const float4*>(&sm_o[2 * p + 1][h][d]);
+            const int64_t rec = (int64_t)(b * Hq + hq0 + h) * kAttnPartSplits + 2 * s + p;
+            *reinterpret_cast<float4*>(o_out + rec * D + d) =
+                make_float4(o0.x * a0 + o1.x * a1, o0.y * a0 + o1.y * a1, o0.z * a0 + o1.z * a1, o0.w * a0 + o1.w * a1);
+            if (d == 0) ml_out[rec] = make_float2(mx, ls);
+        }
+        return;
+    }
     for (int idx = threadIdx.x; idx < grp * (D / 4); idx += 256) {
         const int h = idx / (D / 4), d = (idx % (D / 4)) * 4;
         float mx = -INFINITY;
@@ -1057,7 +1078,11 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
         static const int variant8 = getenv("WF_ATTN_VARIANT8") ? atoi(getenv("WF_ATTN_VARIANT8")) : 0;
         if (kv8) {  // FP8 caches: K scale folded into the score scale
             const dim3 wg(kAttnPartSplits / 4, Hkv, B);
-            if (variant8 == 4)
+            if (variant8 == 5)
+                hipLaunchKernelGGL((k_attn_mfma<false, false, false, true, true>), dim3(kAttnPartSplits / 2, Hkv, B),
+                                   dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale,
+                                   ml, o, pt, pps, npages, kv_pgs, v_scale);
+            else if (variant8 == 4)
                 hipLaunchKernelGGL((k_attn_mfma<true, false, true, true>), wg, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
                                    kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale, ml, o, pt, pps, npages, kv_pgs,
                                    v_scale);
@@ -1076,7 +1101,11 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
             return check_launch("decode_attention_partials");
         }
         const dim3 wgrid(kAttnPartSplits / 4, Hkv, B);
-        if (variant == 3)
+        if (variant == 5)
+            hipLaunchKernelGGL((k_attn_mfma<false, false, false, false, true>), dim3(kAttnPartSplits / 2, Hkv, B),
+                               dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, ml, o, pt,
+                               pps, npages, kv_pgs, 1.0f);
+        else if (variant == 3)
             hipLaunchKernelGGL((k_attn_mfma<false, false, true>), wgrid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq,
                                Hkv, S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs, 1.0f);
         else if (variant == 4)
