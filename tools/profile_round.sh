@@ -26,27 +26,41 @@ tail -1 "$O/bench_b128.log" | cut -c1-200
 step bench-b128-uniform-paged
 timeout -k 10 600 python bench.py --batch 128 --steps 100 --warmup 10 --no-cpu-baseline --ctx-dist uniform > "$O/bench_b128u.log" 2>&1 || exit $?
 tail -1 "$O/bench_b128u.log" | cut -c1-200
+step bench-b128-fp8
+timeout -k 10 600 python bench.py --batch 128 --steps 100 --warmup 10 --no-cpu-baseline --kv fp8 > "$O/bench_b128_fp8.log" 2>&1 || exit $?
+tail -1 "$O/bench_b128_fp8.log" | cut -c1-200
+timeout -k 10 600 python bench.py --batch 128 --steps 100 --warmup 10 --no-cpu-baseline --kv fp8 --ctx-dist uniform > "$O/bench_b128u_fp8.log" 2>&1 || exit $?
+tail -1 "$O/bench_b128u_fp8.log" | cut -c1-200
+step bench-b1-tq
+timeout -k 10 600 python bench.py --steps 200 --warmup 10 --no-cpu-baseline --no-gemv --wfmt tq > "$O/bench_b1_tq.log" 2>&1 || exit $?
+tail -1 "$O/bench_b1_tq.log" | cut -c1-200
 for B in 1 128; do
     step "rocprof b$B"
     cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof_b$B" -o run -- \
         python3 "$R/bench.py" --batch $B --steps 100 --warmup 10 --no-cpu-baseline --no-gemv > "$O/prof_b$B.log" 2>&1 || exit $?
     cd "$R" && python3 tools/prof_summary.py "$O/prof_b$B" > "$O/kernel_stats_b$B.txt" 2>&1 || exit $?
+    rm -rf "$O/prof_b$B"  # raw traces: gpurun_out/ must stay under 64 MiB
     for C in FETCH_SIZE WRITE_SIZE; do
         step "pmc $C b$B"
         cd /tmp && timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$O/pmc_${C}_b$B" -o run -- \
             python3 "$R/bench.py" --batch $B --steps 20 --warmup 5 --no-cpu-baseline --no-op-timing --no-gemv > "$O/pmc_${C}_b$B.log" 2>&1 || exit $?
         cd "$R"
     done
+    STEM=pmc_traffic; [ $B -gt 1 ] && STEM=pmc_traffic_b$B
+    python3 tools/pmc_traffic.py "$O/pmc_FETCH_SIZE_b$B" "$O/pmc_WRITE_SIZE_b$B" "$TAG" $STEM > /dev/null || exit $?
+    cp profiles/$STEM.json "$O/" && rm -rf "$O/pmc_FETCH_SIZE_b$B" "$O/pmc_WRITE_SIZE_b$B"
 done
 step prefill
 timeout -k 10 300 python tools/prefill_gemm_bench.py > "$O/prefill.log" 2>&1 || exit $?
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_prefill" -o run -- python3 "$R/tools/prefill_gemm_bench.py" --iters 10 > "$O/prof_prefill.log" 2>&1 || exit $?
 cd "$R" && python3 tools/prof_summary.py "$O/prof_prefill" > "$O/kernel_stats_prefill.txt" 2>&1 || exit $?
+rm -rf "$O/prof_prefill"
 tail -1 "$O/prefill.log"
 step prefill-e2e
 timeout -k 10 300 python tools/prefill_bench.py > "$O/prefill_e2e.log" 2>&1 || exit $?
 timeout -k 10 300 python tools/prefill_bench.py --paged >> "$O/prefill_e2e.log" 2>&1 || exit $?
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_prefill_e2e" -o run -- python3 "$R/tools/prefill_bench.py" --iters 1 > "$O/prof_prefill_e2e.log" 2>&1 || exit $?
 cd "$R" && python3 tools/prof_summary.py "$O/prof_prefill_e2e" > "$O/kernel_stats_prefill_e2e.txt" 2>&1 || exit $?
+rm -rf "$O/prof_prefill_e2e"
 grep workload "$O/prefill_e2e.log"
 echo "== done"
