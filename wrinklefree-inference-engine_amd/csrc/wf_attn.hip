@@ -453,7 +453,8 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
             os[0] += ov.x * a; os[1] += ov.y * a; os[2] += ov.z * a; os[3] += ov.w * a;
         }
         const int64_t rec = (int64_t)(b * Hq + hq0 + h) * kAttnPartSplits + s;
-        *reinterpret_cast<float4*>(o_out + rec * D + d) = make_float4(os[0], os[1], os[2], os[3]);
+        *reinterpret_cast<float4*>(o_out + part_o_off(rec / kAttnPartSplits, (int)(rec % kAttnPartSplits), d)) =
+            make_float4(os[0], os[1], os[2], os[3]);
         if (d == 0) ml_out[rec] = make_float2(mx, ls);
     }
     WF_STAMP(2);
@@ -670,7 +671,7 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
             const int h = 4 * q4 + r;
             if (h < grp) {
 #pragma unroll
-                for (int n = 0; n < 8; ++n) o_out[(rec0 + (int64_t)h * kAttnPartSplits) * D + 16 * n + l16] = acc[n][r];
+                for (int n = 0; n < 8; ++n) o_out[part_o_off((int64_t)b * Hq + hq0 + h, s, 16 * n + l16)] = acc[n][r];
             }
         }
         if (q4 == 0 && l16 < grp) ml_out[rec0 + (int64_t)l16 * kAttnPartSplits] = make_float2(m_run, l_run);
@@ -696,7 +697,7 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
             const float4 o0 = *reinterpret_cast<const float4*>(&sm_o[2 * p][h][d]);
             const float4 o1 = *reinterpret_cast<const float4*>(&sm_o[2 * p + 1][h][d]);
             const int64_t rec = (int64_t)(b * Hq + hq0 + h) * kAttnPartSplits + 2 * s + p;
-            *reinterpret_cast<float4*>(o_out + rec * D + d) =
+            *reinterpret_cast<float4*>(o_out + part_o_off(rec / kAttnPartSplits, (int)(rec % kAttnPartSplits), d)) =
                 make_float4(o0.x * a0 + o1.x * a1, o0.y * a0 + o1.y * a1, o0.z * a0 + o1.z * a1, o0.w * a0 + o1.w * a1);
             if (d == 0) ml_out[rec] = make_float2(mx, ls);
         }
@@ -716,7 +717,8 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
             os[0] += ov.x * a; os[1] += ov.y * a; os[2] += ov.z * a; os[3] += ov.w * a;
         }
         const int64_t rec = (int64_t)(b * Hq + hq0 + h) * kAttnPartSplits + s;
-        *reinterpret_cast<float4*>(o_out + rec * D + d) = make_float4(os[0], os[1], os[2], os[3]);
+        *reinterpret_cast<float4*>(o_out + part_o_off(rec / kAttnPartSplits, (int)(rec % kAttnPartSplits), d)) =
+            make_float4(os[0], os[1], os[2], os[3]);
         if (d == 0) ml_out[rec] = make_float2(mx, ls);
     }
     WF_STAMP(2);

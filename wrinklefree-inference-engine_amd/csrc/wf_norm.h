@@ -319,6 +319,15 @@ __device__ __forceinline__ int64_t bf_tile_off(int r, int p, int H) {
 }
 
 constexpr int kAttnPartSplits = 8;
+// Float offset of element d of split s's unnormalised o in the decode-attention partials of (b, h)
+// (bh = b * Hq + h; head_dim 128): [bh][split][half = (d >> 2) & 1][d >> 3][4]. The merging reader
+// (AttnRow) gives each thread the 8-wide piece d0 = 8 t of every split and loads it as two halves:
+// for one (split, half) the threads of a wave read consecutive 16-byte slots -- one contiguous KiB
+// per wave-instruction (the plain [bh][split][d] order left every other 16-byte slot of each line
+// to the next instruction). (m, l) records stay [bh][split].
+__device__ __forceinline__ int64_t part_o_off(int64_t bh, int s, int d) {
+    return ((bh * kAttnPartSplits + s) * 2 + ((d >> 2) & 1)) * 64 + (d >> 3) * 4 + (d & 3);
+}
 constexpr int kPrefillRowGroup = WF_PREFILL_ROW_GROUP;  // prefill rows per slot-uniform group (include/wf_bitnet.h)
 
 // Matrix-core tile layouts of the K / V caches (batched decode; head_dim 128, S % 32 == 0), element
@@ -353,9 +362,8 @@ struct AttnRow {
             for (int u = 0; u < kAttnPartSplits / 2; ++u) ml[i][u] = reinterpret_cast<const float4*>(ml_in + rec)[u];
 #pragma unroll
             for (int u = 0; u < kAttnPartSplits; ++u) {
-                const float* r = o_in + (rec + u) * D + d0;
-                oa[i][u] = *reinterpret_cast<const float4*>(r);
-                ob[i][u] = *reinterpret_cast<const float4*>(r + 4);
+                oa[i][u] = *reinterpret_cast<const float4*>(o_in + part_o_off(b * Hq + h, u, d0));
+                ob[i][u] = *reinterpret_cast<const float4*>(o_in + part_o_off(b * Hq + h, u, d0 + 4));
             }
         }
     }
