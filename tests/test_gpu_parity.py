@@ -741,6 +741,41 @@ def test_fp8_kv_prefill():
     assert cos.mean().item() >= 0.995 and cos.min().item() >= 0.99, cos
 
 
+def test_prefill_fp8_paged_argument_errors():
+    """The new entry points fail loudly on contract violations (ValueError for WF_EINVAL, as the
+    reference's shape checks; nothing silently ignored): prefill on a batch-1 decoder, rows not in whole groups, FP8 / paged K/V on a
+    decoder without the matrix-core path, bad FP8 scales, tiled GEMM shape checks."""
+    import ctypes as C
+    from wfamd import _lib, ops
+    from wfamd.model import BitNetConfig, BitNetDecoder, synthetic_weights
+    cfg = BitNetConfig(hidden=512, layers=1, n_heads=4, n_kv_heads=1, head_dim=128, inter=768, vocab=1024,
+                       max_seq=256)
+    w = synthetic_weights(cfg, seed=1)
+    d1 = BitNetDecoder(cfg, w, batch=1)
+    with pytest.raises(ValueError):  # C-ABI WF_EINVAL -> ValueError (wfamd._lib.check)
+        d1.prefill([(0, [1, 2, 3], 0)])
+    with pytest.raises(ValueError):
+        BitNetDecoder(cfg, w, batch=4, kv_dtype="fp8")
+    with pytest.raises(ValueError):
+        BitNetDecoder(cfg, w, batch=4, num_pages=64)
+    with pytest.raises(ValueError):
+        BitNetDecoder(cfg, w, batch=16, kv_dtype="fp8", kv_scale=(0.0, 1.0))
+    d16 = BitNetDecoder(cfg, w, batch=16)
+    with pytest.raises(ValueError):
+        d16.prefill([(0, list(range(300)), 0)])  # beyond max_seq
+    _lib.call("wf_model_prefill_reserve", d16._h, 32)
+    t = torch.zeros(20, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    with pytest.raises(ValueError):
+        _lib.call("wf_model_prefill", d16._h, t.data_ptr(), t.data_ptr(), t.data_ptr(), 20, st)  # not whole groups
+    with pytest.raises(ValueError):
+        _lib.call("wf_model_prefill", d16._h, t.data_ptr(), t.data_ptr(), t.data_ptr(), 64, st)  # > reserved rows
+    wq = torch.zeros(24, 32, dtype=torch.uint8, device="cuda")  # N = 24: not a multiple of 16
+    a = ops.codes_to_tiles(torch.zeros(16, 128, dtype=torch.int8, device="cuda"))
+    with pytest.raises(ValueError):
+        ops.bitnet_gemm_tiled(wq, a, 1.0, 16)
+
+
 def test_mfma_tile_format_roundtrip_and_gemv(orc):
     """WF_FMT_I2S_MFMA is a bijection of I2_S (device repack both ways; include/wf_bitnet.h layout)."""
     from wfamd import ops
