@@ -1024,6 +1024,211 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_lds(const uint16_t* __r
     }
 }
 
+// Prefill attention with the keys split over the block's waves: block = one row group
+// (kPrefillRowGroup = 16 consecutive rows of one slot) x kv head g. Every wave holds all 64 query
+// columns of the group (CG = 4 column groups of 4 tokens x 4 heads) and streams key tiles w, w + 4,
+// w + 8, ... in registers (its next K tile in flight during the softmax, the next V tile during the
+// P.V), so a K/V fragment is loaded once per block and feeds 4 MFMAs -- the row-split kernel above
+// runs one QK -> softmax -> P.V chain per 16 columns. The four partial (max, sum, o) sets merge
+// through LDS in fixed wave order (flash-decoding's combine inside the block); a wave with no valid
+// key for a column contributes 0. A column's result depends only on its own key range, so chunked
+// prefill stays bit-exact.
+template <bool KV8>
+__global__ __launch_bounds__(256, 1) void k_attn_prefill_ks(const uint16_t* __restrict__ q, int64_t q_rs,
+                                                            const uint16_t* __restrict__ K,
+                                                            const uint16_t* __restrict__ Vt, int64_t kv_sb,
+                                                            int64_t kv_sh, const int32_t* __restrict__ row_pos,
+                                                            const int32_t* __restrict__ row_slot, int M,
+                                                            float sm_scale, const int32_t* __restrict__ pt, int pps,
+                                                            int npages, int64_t kv_pgs, uint16_t* __restrict__ out,
+                                                            int64_t o_rs, float v_scale) {
+    constexpr int D = 128, CG = 4, kOs = D + 4;
+    using KF = KvFrag<KV8>;
+    using FT = typename KF::T;
+    __shared__ float s_ml[4][CG][2][16];                                // (wave, group, max | sum, column)
+    __shared__ __attribute__((aligned(16))) float s_o[CG][3][16][kOs];  // group u's o from the other waves
+    const int g = blockIdx.y, hq0 = g * 4;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
+    const int rb = blockIdx.x * 16;
+    if (rb >= M) return;  // whole block
+    const int slot = row_slot[rb];
+    const int kmax = 32 * pps;  // keys a slot holds
+    int lim_c[CG], lim_b = 0;   // column l16 of group u = (token 4u + (l16 >> 2), head l16 & 3)
+#pragma unroll
+    for (int u = 0; u < CG; ++u) lim_c[u] = min(row_pos[min(rb + 4 * u + (l16 >> 2), M - 1)] + 1, kmax);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) lim_b = max(lim_b, min(row_pos[min(rb + t, M - 1)] + 1, kmax));
+    const int ntiles = (lim_b + 31) >> 5;
+    const int64_t kvo = (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;  // element offset
+    const int32_t* ptb = pt ? pt + (int64_t)slot * pps : nullptr;
+    v8s_t qf[CG][4];
+#pragma unroll
+    for (int u = 0; u < CG; ++u) {
+        const uint16_t* qp =
+            q + (int64_t)min(rb + 4 * u + (l16 >> 2), M - 1) * q_rs + (int64_t)(hq0 + (l16 & 3)) * D + 8 * q4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) qf[u][c] = __builtin_bit_cast(v8s_t, *reinterpret_cast<const uint4*>(qp + 32 * c));
+    }
+    auto blk_of = [&](int t) -> int64_t {  // element offset of key tile t (wave-uniform t)
+        return ptb ? (int64_t)min(max(ptb[__builtin_amdgcn_readfirstlane(t)], 0), npages - 1) * kv_pgs
+                   : (int64_t)t * 4096;
+    };
+    auto load_k = [&](FT (&kr)[2][4], int64_t blk) {
+#pragma unroll
+        for (int tau = 0; tau < 2; ++tau)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) kr[tau][c] = KF::ld(K, kvo + blk + (tau * 4 + c) * 512);
+    };
+    auto load_v = [&](FT (&vr)[8], int64_t blk) {
+#pragma unroll
+        for (int n = 0; n < 8; ++n) vr[n] = KF::ld(Vt, kvo + blk + n * 512);
+    };
+    float m_run[CG], l_run[CG];
+    v4f_t acc[CG][8];
+#pragma unroll
+    for (int u = 0; u < CG; ++u) {
+        m_run[u] = -INFINITY;
+        l_run[u] = 0.f;
+#pragma unroll
+        for (int n = 0; n < 8; ++n) acc[u][n] = v4f_t{0.f, 0.f, 0.f, 0.f};
+    }
+    FT kA[2][4], vA[8];
+    if (wave < ntiles) {
+        const int64_t b0 = blk_of(wave);
+        load_k(kA, b0);
+        load_v(vA, b0);
+    }
+    for (int t = wave; t < ntiles; t += 4) {
+        const int bs = 32 * t;
+        const bool more = t + 4 < ntiles;
+        const int64_t nblk = more ? blk_of(t + 4) : 0;
+        uint4 kb[2][4];
+#pragma unroll
+        for (int tau = 0; tau < 2; ++tau)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) kb[tau][c] = KF::bf(kA[tau][c]);
+        v4f_t sc[CG][2];
+#pragma unroll
+        for (int u = 0; u < CG; ++u)
+#pragma unroll
+            for (int tau = 0; tau < 2; ++tau) {
+                sc[u][tau] = v4f_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    sc[u][tau] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8s_t, kb[tau][c]), qf[u][c],
+                                                                         sc[u][tau], 0, 0, 0);
+            }
+        if (more) load_k(kA, nblk);  // the wave's next K tile, in flight during the softmax and the P.V
+        v8s_t ph[CG];
+        float ar[CG][4];
+        bool resc[CG];
+#pragma unroll
+        for (int u = 0; u < CG; ++u) {
+            const int lim = lim_c[u] - bs - 8 * q4;  // valid keys of column l16 among this lane's 8
+            float x[8], mx = -INFINITY;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                x[e] = e < lim ? sc[u][e >> 2][e & 3] * sm_scale : -INFINITY;
+                mx = fmaxf(mx, x[e]);
+            }
+            mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            // this wave may hold no valid key of a column yet (only wave 0 sees key 0): m stays
+            // -inf, p = 0 and acc = 0 (exp against 0, not -inf - -inf)
+            const float mnew = fmaxf(m_run[u], mx);
+            const float mref = mnew == -INFINITY ? 0.f : mnew;
+            const float alpha = __expf(m_run[u] - mref);
+            m_run[u] = mnew;
+            float p[8], ps = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                p[e] = __expf(x[e] - mref);
+                ps += p[e];
+            }
+            l_run[u] = l_run[u] * alpha + ps;
+            uint32_t hi[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) hi[j] = pk_bf16(p[2 * j], p[2 * j + 1]);
+            ph[u] = __builtin_bit_cast(v8s_t, make_uint4(hi[0], hi[1], hi[2], hi[3]));
+            resc[u] = __any(alpha != 1.0f);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ar[u][r] = __shfl(alpha, 4 * q4 + r, 64);
+        }
+        const int limv = lim_b - bs - 8 * q4;  // V rows past the group's last position: zero (stale)
+        v8s_t vf[8];
+#pragma unroll
+        for (int n = 0; n < 8; ++n) vf[n] = __builtin_bit_cast(v8s_t, KF::bf(KF::mask(vA[n], limv)));
+        if (more) load_v(vA, nblk);  // next V tile, in flight during the P.V and the next QK
+#pragma unroll
+        for (int u = 0; u < CG; ++u)
+#pragma unroll
+            for (int n = 0; n < 8; ++n) {
+                if (resc[u]) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[u][n][r] *= ar[u][r];
+                }
+                acc[u][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph[u], vf[n], acc[u][n], 0, 0, 0);
+            }
+    }
+    // combine: column c = 4 q4 + r of group u is acc[u][*][r]; its (m, l) sit at s_ml[w][u][*][c]
+#pragma unroll
+    for (int u = 0; u < CG; ++u) {
+        float lr = l_run[u];
+        lr += __shfl_xor(lr, 16, 64);
+        lr += __shfl_xor(lr, 32, 64);
+        if (q4 == 0) {
+            s_ml[wave][u][0][l16] = m_run[u];
+            s_ml[wave][u][1][l16] = lr;
+        }
+    }
+    __syncthreads();
+    float fw[CG][4];  // this wave's weight exp(m_w - m) per (group, column)
+#pragma unroll
+    for (int u = 0; u < CG; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int c = 4 * q4 + r;
+            const float m = fmaxf(fmaxf(s_ml[0][u][0][c], s_ml[1][u][0][c]), fmaxf(s_ml[2][u][0][c], s_ml[3][u][0][c]));
+            const float mw = s_ml[wave][u][0][c];
+            fw[u][r] = mw == -INFINITY ? 0.f : __expf(mw - m);
+        }
+#pragma unroll
+    for (int u = 0; u < CG; ++u) {
+        if (u == wave) continue;
+        const int si = wave - (wave > u);
+#pragma unroll
+        for (int n = 0; n < 8; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s_o[u][si][4 * q4 + r][16 * n + l16] = acc[u][n][r] * fw[u][r];
+    }
+    __syncthreads();
+    // wave w finishes group w: the four weighted partials summed in wave order 0..3
+#pragma unroll
+    for (int u = 0; u < CG; ++u) {
+        if (u != wave) continue;
+        const int row = rb + 4 * u + q4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int c = 4 * q4 + r;
+            const float m = fmaxf(fmaxf(s_ml[0][u][0][c], s_ml[1][u][0][c]), fmaxf(s_ml[2][u][0][c], s_ml[3][u][0][c]));
+            float l = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const float mw = s_ml[w][u][0][c];
+                l += mw == -INFINITY ? 0.f : s_ml[w][u][1][c] * __expf(mw - m);
+            }
+            const float inv = (KV8 ? v_scale : 1.0f) / l;
+#pragma unroll
+            for (int n = 0; n < 8; ++n) {
+                float o = 0.f;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) o += w == u ? acc[u][n][r] * fw[u][r] : s_o[u][w - (w > u)][c][16 * n + l16];
+                if (row < M) out[(int64_t)row * o_rs + (int64_t)(hq0 + r) * D + 16 * n + l16] = f2bf(rbf(o * inv));
+            }
+        }
+    }
+}
+
 int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                       int64_t kv_sh, int Hq, int Hkv, const int32_t* row_pos, const int32_t* row_slot, int M,
                       float sm_scale, const int32_t* pt, int pps, int npages, int64_t kv_pgs, uint16_t* out,
@@ -1036,10 +1241,20 @@ int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const 
         set_error("prefill_attention: the LDS-staged kernel supports max_seq <= %d", 32 * kPfMaxTiles);
         return WF_EINVAL;
     }
-    // registers-only kernel by default; the LDS-staged one (WF_PF_ATTN=2, study) measured the same
-    // speed at 8 x 2048 (66.8 vs 66.0 ms per prefill) with 4x less L2 traffic
+    // default: the row-split register kernel. Studies: WF_PF_ATTN=2 its LDS-staged variant (the same
+    // speed at 8 x 2048 with 4x less L2 traffic); 3 the keys split over the block's waves
+    // (k_attn_prefill_ks: parity-green, 758 vs 454 us per layer at 8 x 2048 -- one wave per SIMD,
+    // 512 registers with spills, so the per-tile QK -> softmax -> P.V chain is not hidden)
     static const int var = getenv("WF_PF_ATTN") ? atoi(getenv("WF_PF_ATTN")) : 0;
-    if (kv8)
+    if (var == 3) {
+        const dim3 grid((M + 15) / 16, Hkv);
+        if (kv8)
+            hipLaunchKernelGGL((k_attn_prefill_ks<true>), grid, dim3(256), 0, st, q, q_rs, k, v, kv_sb, kv_sh, row_pos,
+                               row_slot, M, sm_scale * k_scale, pt, pps, npages, kv_pgs, out, o_rs, v_scale);
+        else
+            hipLaunchKernelGGL((k_attn_prefill_ks<false>), grid, dim3(256), 0, st, q, q_rs, k, v, kv_sb, kv_sh, row_pos,
+                               row_slot, M, sm_scale, pt, pps, npages, kv_pgs, out, o_rs, 1.0f);
+    } else if (kv8)
         hipLaunchKernelGGL((k_attn_prefill<1, 2, true>), dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v, kv_sb,
                            kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale * k_scale, pt, pps, npages, kv_pgs, out, o_rs,
                            v_scale);
