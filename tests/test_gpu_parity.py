@@ -793,3 +793,26 @@ def test_mfma_tile_format_roundtrip_and_gemv(orc):
             off = 32 * kb + 16 * h + 4 * (lane >> 4)
             assert mfn[t] == p[row, off:off + 4].view(np.uint32)[0]
         assert np.array_equal(ops.mfma_to_i2s(mf).cpu().numpy(), p)
+
+
+@pytest.mark.parametrize("variant", ["2", "3"])
+def test_prefill_attention_study_variants(variant):
+    """The opt-in prefill attention kernels (WF_PF_ATTN=2: LDS-staged k_attn_prefill_lds, bf16 only;
+    3: keys split over the block's waves, k_attn_prefill_ks, bf16 and FP8) pass the same prefill
+    parity tests as the default kernel. The choice is read once per process, so the tests run in a
+    child process with the variable set."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    tests = ["test_prefill_matches_teacher_forced_decode", "test_prefill_in_pieces_equals_one_shot"]
+    if variant == "3":
+        tests.append("test_fp8_kv_prefill")  # the FP8 instantiation of the keys-split kernel
+    env = dict(os.environ, WF_PF_ATTN=variant)
+    sel = " or ".join(tests)
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
+                        str(root / "tests" / "test_gpu_parity.py"), "-k", sel],
+                       env=env, cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert f"{len(tests)} passed" in r.stdout, r.stdout[-2000:]

@@ -1047,6 +1047,8 @@ __global__ __launch_bounds__(256, 1) void k_attn_prefill_ks(const uint16_t* __re
     using FT = typename KF::T;
     __shared__ float s_ml[4][CG][2][16];                                // (wave, group, max | sum, column)
     __shared__ __attribute__((aligned(16))) float s_o[CG][3][16][kOs];  // group u's o from the other waves
+    // ~103 KB of static LDS: needs gfx950's 160 KiB per CU (one block per CU, launch bounds (256, 1))
+    static_assert(sizeof(s_o) + sizeof(s_ml) <= 160 * 1024, "k_attn_prefill_ks exceeds the gfx950 LDS");
     const int g = blockIdx.y, hq0 = g * 4;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
     const int rb = blockIdx.x * 16;
@@ -1229,23 +1231,36 @@ __global__ __launch_bounds__(256, 1) void k_attn_prefill_ks(const uint16_t* __re
     }
 }
 
-int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
-                      int64_t kv_sh, int Hq, int Hkv, const int32_t* row_pos, const int32_t* row_slot, int M,
-                      float sm_scale, const int32_t* pt, int pps, int npages, int64_t kv_pgs, uint16_t* out,
-                      int64_t o_rs, hipStream_t st, int kv8, float k_scale, float v_scale) {
+// Prefill attention kernel, chosen once per process from WF_PF_ATTN (unset / any other value: the
+// row-split register kernel k_attn_prefill; 2: its LDS-staged variant k_attn_prefill_lds, same speed
+// at 8 x 2048 with 4x less L2 traffic; 3: the keys split over the block's waves, k_attn_prefill_ks,
+// 758 vs 454 us per layer at 8 x 2048 -- one wave per SIMD, 512 registers with spills, so the
+// per-tile QK -> softmax -> P.V chain is not hidden). The guard and the launch read this one value.
+int prefill_attention_variant() {
+    static const int var = getenv("WF_PF_ATTN") ? atoi(getenv("WF_PF_ATTN")) : 0;
+    return var;
+}
+
+// Contract of prefill_attention, checked by wf_model_prefill before its first launch (so a refused
+// call leaves the cache untouched).
+int prefill_attention_check(int Hq, int Hkv, int pps) {
     if (Hq != 4 * Hkv) {
         set_error("prefill_attention: GQA group %d != 4 not supported", Hq / Hkv);
         return WF_EINVAL;
     }
-    if (pps > kPfMaxTiles && getenv("WF_PF_ATTN") && atoi(getenv("WF_PF_ATTN")) == 2) {
+    if (pps > kPfMaxTiles && prefill_attention_variant() == 2) {
         set_error("prefill_attention: the LDS-staged kernel supports max_seq <= %d", 32 * kPfMaxTiles);
         return WF_EINVAL;
     }
-    // default: the row-split register kernel. Studies: WF_PF_ATTN=2 its LDS-staged variant (the same
-    // speed at 8 x 2048 with 4x less L2 traffic); 3 the keys split over the block's waves
-    // (k_attn_prefill_ks: parity-green, 758 vs 454 us per layer at 8 x 2048 -- one wave per SIMD,
-    // 512 registers with spills, so the per-tile QK -> softmax -> P.V chain is not hidden)
-    static const int var = getenv("WF_PF_ATTN") ? atoi(getenv("WF_PF_ATTN")) : 0;
+    return WF_OK;
+}
+
+int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
+                      int64_t kv_sh, int Hq, int Hkv, const int32_t* row_pos, const int32_t* row_slot, int M,
+                      float sm_scale, const int32_t* pt, int pps, int npages, int64_t kv_pgs, uint16_t* out,
+                      int64_t o_rs, hipStream_t st, int kv8, float k_scale, float v_scale) {
+    if (int rc = prefill_attention_check(Hq, Hkv, pps)) return rc;
+    const int var = prefill_attention_variant();
     if (var == 3) {
         const dim3 grid((M + 15) / 16, Hkv);
         if (kv8)

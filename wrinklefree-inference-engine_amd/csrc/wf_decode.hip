@@ -28,6 +28,7 @@
 #include "wf_mfma.h"
 
 namespace wf {
+int prefill_attention_check(int Hq, int Hkv, int pps);
 int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                       int64_t kv_sh, int Hq, int Hkv, const int32_t* row_pos, const int32_t* row_slot, int M,
                       float sm_scale, const int32_t* pt, int pps, int npages, int64_t kv_pgs, uint16_t* out,
@@ -1745,8 +1746,12 @@ int wf_model_prefill(wf_model* m, const int32_t* tokens, const int32_t* row_slot
     const wf_model_desc& d = m->d;
     hipStream_t st = as_stream(stream);
     const int H = d.hidden, I = d.inter, D = d.head_dim;
-    hipLaunchKernelGGL(k_embed, dim3(rows), dim3(256), 0, st, d.embed, tokens, H, d.vocab, m->pf_h_a, row_pos, m->pf_seq);
     int rc;
+    {  // every contract check before the first launch: a refused call leaves the K/V cache untouched
+        const GemvArgs a0 = base_args(m, 0);
+        if ((rc = prefill_attention_check(d.n_heads, d.n_kv_heads, d.page_table ? a0.pps : d.max_seq / 32))) return rc;
+    }
+    hipLaunchKernelGGL(k_embed, dim3(rows), dim3(256), 0, st, d.embed, tokens, H, d.vocab, m->pf_h_a, row_pos, m->pf_seq);
     for (int l = 0; l < d.layers; ++l) {
         const float* wsh = d.wscale + 7 * l;
         GemvArgs a = base_args(m, l);
