@@ -993,99 +993,102 @@ __global__ __launch_bounds__(kNT) void k_rownorm(const uint16_t* __restrict__ x,
     }
 }
 
-// The same row norm + quantizer with ONE wave per row, for prefill's thousands of rows (a
-// throughput job: no block barriers, 4 rows per 256-thread block; at decode batch sizes the
-// 512-thread block is faster -- its latency chain is spread over 8 waves). Bit-identical to
-// k_rownorm<PPT, false, TL>: lane l plays thread 64 v + l (v < 8) of the 512-thread tree, so every
-// per-thread fma chain, every wave's DPP reduction and the 8-way tree over the waves are the same
-// operations in the same order (max and the integer code sum are order-free).
-// Prefill row norm (thousands of rows): k_rownorm's 512-thread tree for R rows per block, so its
-// two block-wide reductions pay one barrier each for all R rows instead of one per row.
-// Bit-identical to k_rownorm<PPT, false, true> row by row (same per-thread pieces, same DPP + 8-way
-// tree). Measured at 16384 rows: 77 -> 76 us (K 2560), 116 -> 99 us (K 6912); a variant that
-// assembled 16-row tiles in LDS for contiguous stores, and a wave-per-row variant, were slower.
-template <int PPT, int R>
-__global__ __launch_bounds__(kNT) void k_rownorm_multi(const uint16_t* __restrict__ x, int64_t xs,
+// Prefill row norm (thousands of rows): block = 8 consecutive rows = one half of a 16-row code
+// tile, one wave per row, no block-wide reductions. A wave replays k_rownorm's 512-thread tree for
+// its row (bit-identical codes, scale and code sum): lane l holds pieces 8 (64 j + l), j < NP, i.e.
+// piece j of "thread" 64 (j % 8) + l; the eight per-thread fma chains are kept apart, each goes
+// through the same wave_sum, and tree_sum<8> adds them in wave order (max and the integer code sum
+// are order-free). Codes land row-major in LDS (row stride K + 16 bytes); after one barrier the
+// block writes its half-tiles in the tile_code_pos layout as whole 128-byte lines (lane = one
+// 16-byte slot, its 4 dwords gathered by conflict-free ds_read_b32), so every line of the code
+// tensor is written by one block of one XCD (the former 4-rows-per-block kernel split each line
+// over four blocks' 4-byte stores: 76 us at K 2560, 98 us at K 6912 for 16384 rows).
+template <int NP>
+__global__ __launch_bounds__(512) void k_rownorm_tile8(const uint16_t* __restrict__ x, int64_t xs,
                                                        const uint16_t* __restrict__ nw, int K, float eps,
                                                        int8_t* __restrict__ q8, float* __restrict__ sf,
-                                                       int* __restrict__ asum_out, int rows) {
-    constexpr int NW = kNT / 64;
-    __shared__ float red[R][2 * NW];
-    __shared__ int red_i[R][NW];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, npk = K >> 3;
-    const int b0 = blockIdx.x * R;
-    uint4 xv[R][PPT], wv[PPT];
+                                                       int* __restrict__ asum_out) {
+    // LDS: the norm weight row (K bf16; kept out of the registers: two blocks per CU at K 6912),
+    // then the codes [8][K + 16]
+    extern __shared__ __attribute__((aligned(16))) int8_t s_dyn[];
+    uint16_t* s_nw = reinterpret_cast<uint16_t*>(s_dyn);
+    int8_t* s_codes = s_dyn + 2 * K;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, npk = K >> 3, KS = K + 16;
+    const int row = blockIdx.x * 8 + wave;
+    uint4 xv[NP];
 #pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-        const int p = min((int)threadIdx.x + kNT * i, npk - 1);
-        wv[i] = *reinterpret_cast<const uint4*>(nw + 8 * p);
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-            xv[r][i] = *reinterpret_cast<const uint4*>(x + (int64_t)min(b0 + r, rows - 1) * xs + 8 * p);
+    for (int j = 0; j < NP; ++j) {
+        const int pc = min(64 * j + lane, npk - 1);
+        xv[j] = *reinterpret_cast<const uint4*>(x + (int64_t)row * xs + 8 * pc);
     }
-    float y[R][PPT][8];
+    for (int p = threadIdx.x; p < npk; p += 512)
+        reinterpret_cast<uint4*>(s_nw)[p] = reinterpret_cast<const uint4*>(nw)[p];
+    float ss[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        float ss = 0.f;
+    for (int j = 0; j < NP; ++j) {
+        const bool valid = 64 * j + lane < npk;
+        const uint32_t w4[4] = {xv[j].x, xv[j].y, xv[j].z, xv[j].w};
 #pragma unroll
-        for (int i = 0; i < PPT; ++i) {
-            const bool valid = (int)threadIdx.x + kNT * i < npk;
-            const uint32_t w4[4] = {xv[r][i].x, xv[r][i].y, xv[r][i].z, xv[r][i].w};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                y[r][i][2 * j] = valid ? bf_lo(w4[j]) : 0.f;
-                y[r][i][2 * j + 1] = valid ? bf_hi(w4[j]) : 0.f;
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) ss = fmaf(y[r][i][j], y[r][i][j], ss);
+        for (int e = 0; e < 4; ++e) {
+            const float lo = valid ? bf_lo(w4[e]) : 0.f, hi = valid ? bf_hi(w4[e]) : 0.f;
+            ss[j & 7] = fmaf(lo, lo, ss[j & 7]);
+            ss[j & 7] = fmaf(hi, hi, ss[j & 7]);
         }
-        ss = wave_sum(ss);
-        if (lane == 0) red[r][wave] = ss;
     }
-    __syncthreads();
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const float rr = rbf(1.0f / sqrtf(tree_sum<NW>(red[r]) / (float)K + eps));
-        float m = 0.f;
+    for (int j = 0; j < NP; ++j) reg_fence(xv[j]);  // pass 2 unpacks again (no 8 NP floats kept live)
+    float W[8];
 #pragma unroll
-        for (int i = 0; i < PPT; ++i) {
-            const uint32_t n4[4] = {wv[i].x, wv[i].y, wv[i].z, wv[i].w};
+    for (int v = 0; v < 8; ++v) W[v] = wave_sum(ss[v]);
+    __syncthreads();  // s_nw complete
+    const float rr = rbf(1.0f / sqrtf(tree_sum<8>(W) / (float)K + eps));
+    float m = 0.f;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t a = pk_bf16(y[r][i][2 * j] * rr, y[r][i][2 * j + 1] * rr);
-                const uint32_t c = pk_bf16(bf_lo(a) * bf_lo(n4[j]), bf_hi(a) * bf_hi(n4[j]));
-                y[r][i][2 * j] = bf_lo(c);
-                y[r][i][2 * j + 1] = bf_hi(c);
-                m = fmaxf(m, fmaxf(fabsf(y[r][i][2 * j]), fabsf(y[r][i][2 * j + 1])));
-            }
+    for (int j = 0; j < NP; ++j) {  // xv[j] <- the normalised row, packed bf16 (0 past the row)
+        const bool valid = 64 * j + lane < npk;
+        const uint4 wv = reinterpret_cast<const uint4*>(s_nw)[min(64 * j + lane, npk - 1)];
+        const uint32_t w4[4] = {xv[j].x, xv[j].y, xv[j].z, xv[j].w}, n4[4] = {wv.x, wv.y, wv.z, wv.w};
+        uint32_t o4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t a = pk_bf16(bf_lo(w4[e]) * rr, bf_hi(w4[e]) * rr);
+            const uint32_t b = valid ? pk_bf16(bf_lo(a) * bf_lo(n4[e]), bf_hi(a) * bf_hi(n4[e])) : 0u;
+            m = fmaxf(m, fmaxf(fabsf(bf_lo(b)), fabsf(bf_hi(b))));
+            o4[e] = b;
         }
-        m = wave_max(m);
-        if (lane == 0) red[r][NW + wave] = m;
+        xv[j] = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+        if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // at most 4 norm-weight pieces in registers
+    }
+    // the codes pass re-reads the packed row (without the fence hipcc keeps all 8 NP floats live)
+#pragma unroll
+    for (int j = 0; j < NP; ++j) reg_fence(xv[j]);
+    const float s = (float)act_scale_from_max(wave_max(m));
+    const float inv = 1.0f / s;
+    int as = 0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        const uint32_t w4[4] = {xv[j].x, xv[j].y, xv[j].z, xv[j].w};
+        const float y[8] = {bf_lo(w4[0]), bf_hi(w4[0]), bf_lo(w4[1]), bf_hi(w4[1]),
+                            bf_lo(w4[2]), bf_hi(w4[2]), bf_lo(w4[3]), bf_hi(w4[3])};
+        const uint2 c = quant8(y, s, inv, as);
+        const int p = 64 * j + lane;
+        if (p < npk) *reinterpret_cast<uint2*>(s_codes + wave * KS + 8 * p) = c;
+    }
+    as = wave_sum_i(as);
+    if (lane == 0) {
+        sf[row] = s;
+        asum_out[row] = as;
     }
     __syncthreads();
-    float sr[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        float m = red[r][NW];
-#pragma unroll
-        for (int w = 1; w < NW; ++w) m = fmaxf(m, red[r][NW + w]);
-        sr[r] = (float)act_scale_from_max(m);
-        int as = 0;
-        if (b0 + r < rows) as = quant_row_tiled<PPT, kNT>(y[r], sr[r], npk, q8, b0 + r, K >> 7);
-        as = wave_sum_i(as);
-        if (lane == 0) red_i[r][wave] = as;
-    }
-    __syncthreads();
-    if (threadIdx.x < R && b0 + (int)threadIdx.x < rows) {
-        const int r = threadIdx.x;
-        int t = 0;
-        for (int w = 0; w < NW; ++w) t += red_i[r][w];
-        asum_out[b0 + r] = t;
-        float s = sr[0];
-#pragma unroll
-        for (int u = 1; u < R; ++u)
-            if (u == r) s = sr[u];
-        sf[b0 + r] = s;
+    // half-tiles (kb, h): 32 slots (r8, q) = 4 whole lines; lanes 0-31 one pair, 32-63 the next
+    const int nkb = K >> 7, half8 = blockIdx.x & 1, rt = blockIdx.x >> 1;
+    const int slot = threadIdx.x & 31, r8 = slot & 7, qq = slot >> 3;
+    for (int pr = threadIdx.x >> 5; pr < 2 * nkb; pr += 16) {
+        const int kb = pr >> 1, h = pr & 1;
+        const int8_t* src = s_codes + r8 * KS + 128 * kb + 16 * h + 4 * qq;
+        const uint4 v = make_uint4(*reinterpret_cast<const uint32_t*>(src), *reinterpret_cast<const uint32_t*>(src + 32),
+                                   *reinterpret_cast<const uint32_t*>(src + 64), *reinterpret_cast<const uint32_t*>(src + 96));
+        *reinterpret_cast<uint4*>(q8 + ((((int64_t)rt * nkb + kb) * 2 + h) << 10) + (((r8 + 8 * half8) + 16 * qq) << 4)) = v;
     }
 }
 
@@ -1718,15 +1721,24 @@ int wf_model_prefill_reserve(wf_model* m, int rows) {
 extern "C++" {
 static void prefill_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, const uint16_t* nw, int K, int rows,
                             hipStream_t st) {
-    const float eps = m->d.eps;
-    constexpr int R = 4;
-    const dim3 grid((rows + R - 1) / R);
-    if (norm_ppt(K) == 1)
-        hipLaunchKernelGGL((k_rownorm_multi<1, R>), grid, dim3(kNT), 0, st, x, xs, nw, K, eps, m->pf_q8, m->pf_sf,
-                           m->pf_asum, rows);
-    else
-        hipLaunchKernelGGL((k_rownorm_multi<2, R>), grid, dim3(kNT), 0, st, x, xs, nw, K, eps, m->pf_q8, m->pf_sf,
-                           m->pf_asum, rows);
+    // rows % 16 == 0 (wf_model_prefill); 8 rows per block
+    const dim3 grid(rows / 8);
+    const size_t lds = 2 * (size_t)K + 8 * (size_t)(K + 16);
+    const int np = (K / 8 + 63) / 64;
+#define WF_RN8(NPV) \
+    hipLaunchKernelGGL((k_rownorm_tile8<NPV>), grid, dim3(512), lds, st, x, xs, nw, K, m->d.eps, m->pf_q8, m->pf_sf, m->pf_asum)
+    if (np <= 5) {
+        WF_RN8(5);
+    } else if (np <= 14) {
+        WF_RN8(14);
+    } else {  // K up to 8192: 2 K + 8 (K + 16) bytes of LDS pass 64 KiB
+        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rownorm_tile8<16>),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                           2 * 8192 + 8 * (8192 + 16));
+        (void)attr;
+        WF_RN8(16);
+    }
+#undef WF_RN8
 }
 
 template <int MODE>
