@@ -699,6 +699,150 @@ __global__ __launch_bounds__(NW * 64) void k_dec_gemm_t(GemvArgs a) {
     WF_STAMP_DRAIN(6);
 }
 
+// Prefill q|k|v epilogue, staged through the (idle) LDS ring: the decode step's EpiDec<MODE_QKV>
+// float sequence, but (1) the per-row inputs (scale, code sum, position, slot, page) are loaded
+// once per row into LDS; (2) every wave writes its 16 fragments' corrected bf16 values into a
+// 128 x 256 LDS tile in the GEMM's column order (a 16-column tile = dims 8 tt .. +7 and 64 + 8 tt ..
+// +7 of one head: both RoPE halves of 8 dims are 32 contiguous LDS bytes); (3) the block then
+// writes whole pieces: q rows and K tile rows as 16-byte pieces of 8 dims (RoPE from 16-byte cos /
+// sin loads), V tile pieces of 8 consecutive keys of one dim (one 16-byte store when the 8 rows
+// are positions 8a .. 8a + 7 of one slot, else per element). The per-fragment form (scattered
+// 2-byte stores, two dependent loads per fragment) spilled its accumulators (272 B per lane).
+constexpr int kPfEpiRS = 256 * 2 + 16;  // LDS row stride of the staged tile (bytes)
+__device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int bn, const v4i_t (&acc)[4][4],
+                                                uint8_t* lds) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+    const int wr = wave >> 2, wc = wave & 3;
+    uint8_t* tile = lds;                                              // [128][kPfEpiRS]
+    float* s_sf = reinterpret_cast<float*>(lds + 128 * kPfEpiRS);     // [128]
+    int* s_as = reinterpret_cast<int*>(s_sf + 128);                    // [128]
+    int* s_pos = s_as + 128;                                           // [128] clamped position
+    int* s_slot = s_pos + 128;                                         // [128]
+    int* s_pg = s_slot + 128;                                          // [128] page of the position (paged)
+    __syncthreads();  // every wave is done with the ring
+    if (threadIdx.x < 128) {
+        const int mc = min(bm * 128 + (int)threadIdx.x, g.B - 1);
+        s_sf[threadIdx.x] = g.act_sf[mc];
+        s_as[threadIdx.x] = g.act_sum[mc];
+        const int pos = min(max(g.positions[mc], 0), g.S - 1);
+        const int slot = g.row_slot ? g.row_slot[mc] : mc;
+        s_pos[threadIdx.x] = pos;
+        s_slot[threadIdx.x] = slot;
+        s_pg[threadIdx.x] = g.pt ? min(max(g.pt[(int64_t)slot * g.pps + (pos >> 5)], 0), g.npages - 1) : 0;
+    }
+    __syncthreads();
+    const int head0 = bn * 2, nheads = g.Hq + 2 * g.Hkv;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int ct = 4 * wc + j, head = head0 + (ct >> 3);
+        const float ws = head < g.Hq ? g.ws0 : (head < g.Hq + g.Hkv ? g.ws1 : g.ws2);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int rl = (4 * wr + i) * 16 + 4 * q + r;
+                const float v = rbf(corrected(acc[i][j][r], ws, s_as[rl], s_sf[rl]));
+                const float nv = dpp_f<DPP_QP_1032>(v);  // column l16 ^ 1
+                if (!(l16 & 1)) *reinterpret_cast<uint32_t*>(tile + rl * kPfEpiRS + (16 * ct + l16) * 2) = pk_bf16(v, nv);
+            }
+        }
+    }
+    __syncthreads();
+    const int8_t kv8 = (int8_t)g.kv8;
+    // q and k heads: item = (row, column tile) -> 8 dims of each RoPE half
+    for (int it = threadIdx.x; it < 128 * 16; it += 512) {
+        const int rl = it >> 4, ct = it & 15, tt = ct & 7, head = head0 + (ct >> 3);
+        const int m = bm * 128 + rl;
+        if (m >= g.B || head >= g.Hq + g.Hkv) continue;
+        const uint4 lo = *reinterpret_cast<const uint4*>(tile + rl * kPfEpiRS + ct * 32);
+        const uint4 hi = *reinterpret_cast<const uint4*>(tile + rl * kPfEpiRS + ct * 32 + 16);
+        const int pos = s_pos[rl];
+        const uint4 cs = *reinterpret_cast<const uint4*>(g.rope_cos + (int64_t)pos * 64 + 8 * tt);
+        const uint4 sn = *reinterpret_cast<const uint4*>(g.rope_sin + (int64_t)pos * 64 + 8 * tt);
+        const uint32_t x1[4] = {lo.x, lo.y, lo.z, lo.w}, x2[4] = {hi.x, hi.y, hi.z, hi.w};
+        const uint32_t c4[4] = {cs.x, cs.y, cs.z, cs.w}, s4[4] = {sn.x, sn.y, sn.z, sn.w};
+        float y1[8], y2[8];  // RotaryEmbedding._rotate (direct_inference_full.py:58-70)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float a = (e & 1) ? bf_hi(x1[e >> 1]) : bf_lo(x1[e >> 1]);
+            const float b = (e & 1) ? bf_hi(x2[e >> 1]) : bf_lo(x2[e >> 1]);
+            const float c = (e & 1) ? bf_hi(c4[e >> 1]) : bf_lo(c4[e >> 1]);
+            const float sv = (e & 1) ? bf_hi(s4[e >> 1]) : bf_lo(s4[e >> 1]);
+            y1[e] = rbf(rbf(a * c) - rbf(b * sv));
+            y2[e] = rbf(rbf(a * sv) + rbf(b * c));
+        }
+        if (head < g.Hq) {
+            uint16_t* qo = g.out + (int64_t)m * g.out_stride + head * 128 + 8 * tt;
+            *reinterpret_cast<uint4*>(qo) = make_uint4(pk_bf16(y1[0], y1[1]), pk_bf16(y1[2], y1[3]),
+                                                       pk_bf16(y1[4], y1[5]), pk_bf16(y1[6], y1[7]));
+            *reinterpret_cast<uint4*>(qo + 64) = make_uint4(pk_bf16(y2[0], y2[1]), pk_bf16(y2[2], y2[3]),
+                                                            pk_bf16(y2[4], y2[5]), pk_bf16(y2[6], y2[7]));
+            continue;
+        }
+        const int kvh = head - g.Hq;
+        const int64_t base = g.pt ? (int64_t)s_pg[rl] * g.kv_pgs + (int64_t)kvh * 4096
+                                  : (int64_t)s_slot[rl] * g.kv_b_stride + (int64_t)kvh * g.S * 128;
+        const int t = g.pt ? (pos & 31) : pos;
+        const int64_t o1 = base + k_tile_off(t, 8 * tt), o2 = base + k_tile_off(t, 64 + 8 * tt);
+        if (kv8) {
+            uint8_t* c8 = reinterpret_cast<uint8_t*>(g.kc);
+            uint32_t b1[2] = {0u, 0u}, b2[2] = {0u, 0u};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                b1[e >> 2] |= (uint32_t)to_fp8(y1[e] * g.k_inv) << (8 * (e & 3));
+                b2[e >> 2] |= (uint32_t)to_fp8(y2[e] * g.k_inv) << (8 * (e & 3));
+            }
+            *reinterpret_cast<uint2*>(c8 + o1) = make_uint2(b1[0], b1[1]);
+            *reinterpret_cast<uint2*>(c8 + o2) = make_uint2(b2[0], b2[1]);
+        } else {
+            *reinterpret_cast<uint4*>(g.kc + o1) = make_uint4(pk_bf16(y1[0], y1[1]), pk_bf16(y1[2], y1[3]),
+                                                              pk_bf16(y1[4], y1[5]), pk_bf16(y1[6], y1[7]));
+            *reinterpret_cast<uint4*>(g.kc + o2) = make_uint4(pk_bf16(y2[0], y2[1]), pk_bf16(y2[2], y2[3]),
+                                                              pk_bf16(y2[4], y2[5]), pk_bf16(y2[6], y2[7]));
+        }
+    }
+    // v heads: item = (8-row group, dim) -> one V tile piece of 8 keys
+    for (int it = threadIdx.x; it < 16 * 256; it += 512) {
+        const int g8 = it >> 8, col = it & 255, d = col & 127, head = head0 + (col >> 7);
+        if (head < g.Hq + g.Hkv || head >= nheads) continue;
+        const int kvh = head - g.Hq - g.Hkv;
+        const int lc = 16 * ((col >> 7) * 8 + ((d & 63) >> 3)) + (d & 7) + (d >= 64 ? 8 : 0);  // staged column
+        uint16_t vv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vv[e] = *reinterpret_cast<const uint16_t*>(tile + (8 * g8 + e) * kPfEpiRS + lc * 2);
+        const int r0 = 8 * g8, m0 = bm * 128 + r0;
+        const int p0 = s_pos[r0], sl0 = s_slot[r0];
+        bool whole = m0 + 7 < g.B && (p0 & 7) == 0;
+#pragma unroll
+        for (int e = 1; e < 8; ++e) whole = whole && s_pos[r0 + e] == p0 + e && s_slot[r0 + e] == sl0;
+        if (whole) {
+            const int64_t base = g.pt ? (int64_t)s_pg[r0] * g.kv_pgs + (int64_t)kvh * 4096
+                                      : (int64_t)sl0 * g.kv_b_stride + (int64_t)kvh * g.S * 128;
+            const int64_t off = base + v_tile_off(g.pt ? (p0 & 31) : p0, d);
+            if (kv8) {
+                uint32_t b[2] = {0u, 0u};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) b[e >> 2] |= (uint32_t)to_fp8(bf2f(vv[e]) * g.v_inv) << (8 * (e & 3));
+                *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(g.vc) + off) = make_uint2(b[0], b[1]);
+            } else {
+                *reinterpret_cast<uint4*>(g.vc + off) = make_uint4(vv[0] | (uint32_t)vv[1] << 16, vv[2] | (uint32_t)vv[3] << 16,
+                                                                   vv[4] | (uint32_t)vv[5] << 16, vv[6] | (uint32_t)vv[7] << 16);
+            }
+            continue;
+        }
+        for (int e = 0; e < 8; ++e) {  // ragged group: per element
+            const int rl = r0 + e;
+            if (bm * 128 + rl >= g.B) break;
+            const int pos = s_pos[rl];
+            const int64_t base = g.pt ? (int64_t)s_pg[rl] * g.kv_pgs + (int64_t)kvh * 4096
+                                      : (int64_t)s_slot[rl] * g.kv_b_stride + (int64_t)kvh * g.S * 128;
+            const int64_t off = base + v_tile_off(g.pt ? (pos & 31) : pos, d);
+            if (kv8) reinterpret_cast<uint8_t*>(g.vc)[off] = to_fp8(bf2f(vv[e]) * g.v_inv);
+            else g.vc[off] = vv[e];
+        }
+    }
+}
+
 // Prefill GEMM (rows = prompt tokens) on the tile layouts with the decode step's fused epilogues:
 // the wf_mfma.h 128 x 256 tile main loop (pgemm_tile), then EpiDec<MODE> per 16 x 16 fragment
 // (correction, RoPE + K/V cache write through row_slot, residual, ReLU^2 * up).
@@ -714,15 +858,11 @@ __global__ __launch_bounds__(512) void k_pgemm_fused(GemvArgs a, int nbm, int nb
     // epilogue per row tile: the four column tiles' per-row inputs (scale, code sum, residual) are
     // all issued before the first store -- one round trip per row tile instead of per fragment
     // (stores in between would pin the loads behind them): o 159 -> 141, down 291 -> 274 us
-    EpiDec<MODE> e{&a};
-    if constexpr (MODE == MODE_QKV) {  // (the RoPE entries of 4 tiles at once cost more than they save)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                e.apply(bm * 128 + (4 * wr + i) * 16, bn * 256 + (4 * wc + j) * 16, acc[i][j], l16, q);
+    if constexpr (MODE == MODE_QKV) {
+        pf_qkv_epilogue(a, bm, bn, acc, lds);
         return;
     }
+    EpiDec<MODE> e{&a};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int r0 = bm * 128 + (4 * wr + i) * 16;
