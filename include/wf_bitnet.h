@@ -227,7 +227,7 @@ int wf_model_launch_op(wf_model* m, int layer, int op, void* stream);
  * belongs to one slot (pad a sequence by repeating its last row); a slot's earlier positions must already be in the
  * cache (earlier rows of the same call count). Does not touch tokens / positions / logits: the
  * decode step then runs the prompt's last token. reserve() allocates the row workspace once. */
-#define WF_PREFILL_ROW_GROUP 16
+#define WF_PREFILL_ROW_GROUP 32
 int wf_model_prefill_reserve(wf_model* m, int rows);
 int wf_model_prefill(wf_model* m, const int32_t* tokens, const int32_t* row_slot, const int32_t* row_pos, int rows,
                      void* stream);

@@ -795,20 +795,21 @@ def test_mfma_tile_format_roundtrip_and_gemv(orc):
         assert np.array_equal(ops.mfma_to_i2s(mf).cpu().numpy(), p)
 
 
-@pytest.mark.parametrize("variant", ["2", "3"])
+@pytest.mark.parametrize("variant", ["1", "2", "3"])
 def test_prefill_attention_study_variants(variant):
-    """The opt-in prefill attention kernels (WF_PF_ATTN=2: LDS-staged k_attn_prefill_lds, bf16 only;
-    3: keys split over the block's waves, k_attn_prefill_ks, bf16 and FP8) pass the same prefill
-    parity tests as the default kernel. The choice is read once per process, so the tests run in a
-    child process with the variable set."""
+    """The other prefill attention kernels (WF_PF_ATTN=1: the row-split register kernel
+    k_attn_prefill, which the default keeps for FP8 K/V; 2: its LDS-staged variant, bf16 only; 3:
+    keys split over the block's waves, k_attn_prefill_ks, bf16 and FP8) pass the same prefill
+    parity tests as the default flash-style kernel. The choice is read once per process, so the
+    tests run in a child process with the variable set."""
     import os
     import subprocess
     import sys
     from pathlib import Path
     root = Path(__file__).resolve().parents[1]
     tests = ["test_prefill_matches_teacher_forced_decode", "test_prefill_in_pieces_equals_one_shot"]
-    if variant == "3":
-        tests.append("test_fp8_kv_prefill")  # the FP8 instantiation of the keys-split kernel
+    if variant in ("1", "3"):
+        tests.append("test_fp8_kv_prefill")  # their FP8 instantiations
     env = dict(os.environ, WF_PF_ATTN=variant)
     sel = " or ".join(tests)
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",

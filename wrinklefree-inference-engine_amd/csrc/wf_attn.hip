@@ -880,7 +880,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __res
 }
 
 // The same prefill attention with the K/V tiles staged once per block in LDS: the block's 4 waves
-// (16 consecutive rows of one slot: kPrefillRowGroup = 16) need the same tiles, so each wave DMAs
+// (16 consecutive rows of one slot: half a kPrefillRowGroup) need the same tiles, so each wave DMAs
 // a quarter of every 16 KiB tile (4 x 1 KiB LDS-DMA, inline asm: hipcc does not drain the ring
 // before the fragment reads) into a P-slot ring, with P - 2 tiles in flight beyond the one being
 // read; the fragments come from LDS (contiguous KiB per wave-instruction). 4x less L2 / MALL
@@ -1024,8 +1024,199 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_lds(const uint16_t* __r
     }
 }
 
+// Prefill attention, flash style on 32 x 32 bf16 matrix cores (the default for bf16 K/V): block =
+// one row group of kPrefillRowGroup = 32 consecutive rows of one slot x kv head g; wave w takes
+// tokens 8 w .. 8 w + 7 x the group's 4 query heads = 32 query columns (column c = token 8 w + c / 4,
+// head c % 4). Per 32-key tile (staged once per block in a 4 x 16 KiB LDS ring by LDS-DMA, each
+// wave a quarter, P - 2 tiles in flight beyond the one being read):
+//   S^T (32 keys x 32 queries) = K . Q^T: 8 v_mfma_f32_32x32x16_bf16 (K fragments = 16 bytes of
+//       one key's 8 dims, ds_read_b128; Q^T fragments in registers for the whole key range);
+//   online softmax in log2 units: lane (c, h) holds keys j % 4 + 8 (j / 4) + 4 h of column c, so a
+//       column's max / sum needs one v_permlane32_swap, and the rescale factor is the lane's own;
+//   O^T (128 dims x 32 queries) += V^T . P^T: 8 MFMAs; P^T's fragments are the score lanes as they
+//       stand (keys permuted: k-slot i of lane half h = key 16 s + i % 4 + 8 (i / 4) + 4 h), V^T's
+//       fragments two 8-byte ds_reads of the V tile layout (keys contiguous per dim).
+// Per-column causal limit (masking only on diagonal tiles), P rounded to bf16 for the P.V MFMA (a
+// bf16 flash SDPA), V rows past the block's last position zeroed (stale pages). Heavy row groups
+// (late positions) are launched first. A column's result depends only on its own key range (tiles
+// past it add p = 0 at alpha = 1), so chunked prefill stays bit-exact.
+constexpr int kFaStages = 4;  // 64 KiB ring + page ids: two blocks per CU
+typedef __bf16 v8bf_t __attribute__((ext_vector_type(8)));
+typedef float v16f_t __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ float swap32_max(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float swap32_sum(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+template <int STUDY>
+__global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __restrict__ q, int64_t q_rs,
+                                                            const uint16_t* __restrict__ K,
+                                                            const uint16_t* __restrict__ Vt, int64_t kv_sb,
+                                                            int64_t kv_sh, const int32_t* __restrict__ row_pos,
+                                                            const int32_t* __restrict__ row_slot, int M,
+                                                            float sl2, const int32_t* __restrict__ pt, int pps,
+                                                            int npages, int64_t kv_pgs, uint16_t* __restrict__ out,
+                                                            int64_t o_rs) {
+    constexpr int D = 128, P = kFaStages;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[P * 16384];
+    __shared__ int s_page[kPfMaxTiles];
+    const int g = blockIdx.y, hq0 = g * 4;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
+    const int nrb = M / 32;
+    const int rb = (nrb - 1 - (int)blockIdx.x) * 32;  // late (heavy) row groups first
+    const int slot = __builtin_amdgcn_readfirstlane(row_slot[rb]);
+    const int qrow = rb + 8 * wave + (c >> 2);
+    const int lim_q = row_pos[qrow] + 1;  // keys [0, lim_q) of column c
+    int lim_b = 0;
+    for (int t = 0; t < 32; ++t) lim_b = max(lim_b, row_pos[rb + t] + 1);
+    lim_b = __builtin_amdgcn_readfirstlane(lim_b);
+    const float flq = (float)lim_q;  // positions < 2^24: exact
+    const int lim_w = (int)wave_max(flq), lim_min = (int)-wave_max(-flq);
+    v8bf_t qf[8];  // Q^T fragments: column c, dims 16 s + 8 h .. + 7
+    {
+        const uint16_t* qp = q + (int64_t)qrow * q_rs + (int64_t)(hq0 + (c & 3)) * D + 8 * h;
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2) qf[s2] = __builtin_bit_cast(v8bf_t, *reinterpret_cast<const uint4*>(qp + 16 * s2));
+    }
+    // wait for q before the ring's asm DMAs exist (hipcc cannot count those)
+#pragma unroll
+    for (int s2 = 0; s2 < 8; ++s2) asm volatile("" : "+v"(qf[s2]));
+    const int ntiles = (lim_b + 31) >> 5;
+    const uint16_t* Kg = K + (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;
+    const uint16_t* Vg = Vt + (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;
+    if (pt) {
+        for (int t = threadIdx.x; t < ntiles; t += 256) s_page[t] = min(max(pt[(int64_t)slot * pps + t], 0), npages - 1);
+        __syncthreads();
+    }
+    auto issue = [&](int t) {  // wave w DMAs pieces 4w .. 4w + 3 of tile t (K 0..7, V 8..15)
+        const int64_t blk = pt ? (int64_t)s_page[t] * kv_pgs : (int64_t)t * 4096;
+        uint8_t* st = ring + (t % P) * 16384;
+        if (STUDY == 2 && t >= P) return;  // study: no DMA after the first ring fill
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int j = wave * 4 + jj;
+            glds16_asm((j < 8 ? Kg : Vg) + blk + (j & 7) * 512, st + j * 1024);
+        }
+    };
+    float m_run = -INFINITY, l_run = 0.f;
+    v16f_t oacc[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) oacc[mt][e] = 0.f;
+    // K fragment offset of key c, dims 16 s + 8 h (k_tile_off * 2): (tau 16 + dg) 16 + row, x 16 bytes
+    const int koff = ((((c >> 2) & 1) * 16 + h) * 16 + 4 * (c >> 3) + (c & 3)) * 16;
+#pragma unroll
+    for (int t = 0; t < P - 1; ++t)
+        if (t < ntiles) issue(t);
+    for (int t = 0; t < ntiles; ++t) {
+        if (STUDY == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (t + P - 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (P - 2)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (t + P - 1 < ntiles) issue(t + P - 1);  // the slot of tile t - 1, read before this barrier
+        const int bs = 32 * t;
+        if (bs >= lim_w || STUDY == 1) continue;  // every column of this wave is done (wave-uniform)
+        const uint8_t* st = ring + (t % P) * 16384;
+        // all of the tile's K fragments in flight at once (hipcc otherwise issues two ds_reads per
+        // MFMA pair and waits for each), then the V fragments behind them: their LDS latency
+        // overlaps the QK MFMAs and the softmax
+        uint4 kf[8];
+        uint2 va[4][2], vb[4][2];
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2) kf[s2] = *reinterpret_cast<const uint4*>(st + koff + s2 * 512);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+            const int d = 32 * mt + c, n = d >> 4, l = d & 15;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const uint8_t* vp = st + 8192 + ((n * 4 + 2 * s2) * 16 + l) * 16 + 8 * h;
+                va[mt][s2] = *reinterpret_cast<const uint2*>(vp);
+                vb[mt][s2] = *reinterpret_cast<const uint2*>(vp + 256);
+            }
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2) reg_fence(kf[s2]);
+        v16f_t sacc;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) sacc[e] = 0.f;
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2)
+            sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf_t, kf[s2]), qf[s2], sacc, 0, 0, 0);
+        float x[16], mx = -INFINITY;
+        if (bs + 32 > lim_min) {  // diagonal tile: per-column limit
+            const int lim = lim_q - bs - 4 * h;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                x[j] = (j & 3) + 8 * (j >> 2) < lim ? sacc[j] * sl2 : -INFINITY;
+                mx = fmaxf(mx, x[j]);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                x[j] = sacc[j] * sl2;
+                mx = fmaxf(mx, x[j]);
+            }
+        }
+        mx = swap32_max(mx);
+        float mnew = fmaxf(m_run, mx);  // finite: key 0 is valid for every column
+        if (STUDY == 3 && m_run != -INFINITY && mx <= m_run + 8.0f) mnew = m_run;  // lazy rescale (study)
+        const float alpha = __builtin_amdgcn_exp2f(m_run - mnew);
+        m_run = mnew;
+        float ps = 0.f;
+        uint32_t pk[8];
+#pragma unroll
+        for (int j = 0; j < 16; j += 2) {
+            const float p0 = __builtin_amdgcn_exp2f(x[j] - mnew), p1 = __builtin_amdgcn_exp2f(x[j + 1] - mnew);
+            ps += p0;
+            ps += p1;
+            pk[j >> 1] = pk_bf16(p0, p1);
+        }
+        l_run = l_run * alpha + ps;
+        if (__any(alpha != 1.0f)) {
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) oacc[mt][e] *= alpha;
+        }
+        const v8bf_t pb0 = __builtin_bit_cast(v8bf_t, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+        const v8bf_t pb1 = __builtin_bit_cast(v8bf_t, make_uint4(pk[4], pk[5], pk[6], pk[7]));
+        const int limv = lim_b - bs - 4 * h;  // V keys past the block's last position: zero (stale)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                uint2 a = va[mt][s2], b = vb[mt][s2];
+                if (limv < 32) {  // keys 16 s2 + {0..3} and 16 s2 + 8 + {0..3} (+ 4 h)
+                    const int k0 = 16 * s2, k1 = 16 * s2 + 8;
+                    a.x &= (k0 < limv ? 0xffffu : 0u) | (k0 + 1 < limv ? 0xffff0000u : 0u);
+                    a.y &= (k0 + 2 < limv ? 0xffffu : 0u) | (k0 + 3 < limv ? 0xffff0000u : 0u);
+                    b.x &= (k1 < limv ? 0xffffu : 0u) | (k1 + 1 < limv ? 0xffff0000u : 0u);
+                    b.y &= (k1 + 2 < limv ? 0xffffu : 0u) | (k1 + 3 < limv ? 0xffff0000u : 0u);
+                }
+                const v8bf_t vf = __builtin_bit_cast(v8bf_t, make_uint4(a.x, a.y, b.x, b.y));
+                oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, s2 ? pb1 : pb0, oacc[mt], 0, 0, 0);
+            }
+        }
+    }
+    const float inv = 1.0f / swap32_sum(l_run);
+    if (qrow < M) {
+        uint16_t* orow = out + (int64_t)qrow * o_rs + (int64_t)(hq0 + (c & 3)) * D;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)  // dims 32 mt + 8 u + 4 h .. + 3
+                *reinterpret_cast<uint2*>(orow + 32 * mt + 8 * u + 4 * h) =
+                    make_uint2(pk_bf16(oacc[mt][4 * u] * inv, oacc[mt][4 * u + 1] * inv),
+                               pk_bf16(oacc[mt][4 * u + 2] * inv, oacc[mt][4 * u + 3] * inv));
+    }
+}
+
 // Prefill attention with the keys split over the block's waves: block = one row group
-// (kPrefillRowGroup = 16 consecutive rows of one slot) x kv head g. Every wave holds all 64 query
+// (16 consecutive rows of one slot: half a kPrefillRowGroup) x kv head g. Every wave holds all 64 query
 // columns of the group (CG = 4 column groups of 4 tokens x 4 heads) and streams key tiles w, w + 4,
 // w + 8, ... in registers (its next K tile in flight during the softmax, the next V tile during the
 // P.V), so a K/V fragment is loaded once per block and feeds 4 MFMAs -- the row-split kernel above
@@ -1231,11 +1422,11 @@ __global__ __launch_bounds__(256, 1) void k_attn_prefill_ks(const uint16_t* __re
     }
 }
 
-// Prefill attention kernel, chosen once per process from WF_PF_ATTN (unset / any other value: the
-// row-split register kernel k_attn_prefill; 2: its LDS-staged variant k_attn_prefill_lds, same speed
-// at 8 x 2048 with 4x less L2 traffic; 3: the keys split over the block's waves, k_attn_prefill_ks,
-// 758 vs 454 us per layer at 8 x 2048 -- one wave per SIMD, 512 registers with spills, so the
-// per-tile QK -> softmax -> P.V chain is not hidden). The guard and the launch read this one value.
+// Prefill attention kernel, chosen once per process from WF_PF_ATTN (unset / 0: the flash-style
+// 32 x 32 matrix-core kernel k_attn_prefill_fa for bf16 K/V, the row-split register kernel
+// k_attn_prefill for FP8 K/V; 1: the row-split kernel for both; 2: its LDS-staged variant
+// k_attn_prefill_lds; 3: the keys split over the block's waves, k_attn_prefill_ks -- one wave per
+// SIMD, 512 registers with spills). The guard and the launch read this one value.
 int prefill_attention_variant() {
     static const int var = getenv("WF_PF_ATTN") ? atoi(getenv("WF_PF_ATTN")) : 0;
     return var;
@@ -1261,7 +1452,17 @@ int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const 
                       int64_t o_rs, hipStream_t st, int kv8, float k_scale, float v_scale) {
     if (int rc = prefill_attention_check(Hq, Hkv, pps)) return rc;
     const int var = prefill_attention_variant();
-    if (var == 3) {
+    if ((var == 0 || var >= 10) && !kv8 && pps <= kPfMaxTiles && M % 32 == 0) {
+        const dim3 grid(M / 32, Hkv);
+        const float sl2 = sm_scale * 1.4426950408889634f;
+#define WF_FA(S) hipLaunchKernelGGL((k_attn_prefill_fa<S>), grid, dim3(256), 0, st, q, q_rs, k, v, kv_sb, kv_sh, row_pos, \
+                                    row_slot, M, sl2, pt, pps, npages, kv_pgs, out, o_rs)
+        if (var == 11) WF_FA(1);       // study: DMA + barriers only
+        else if (var == 12) WF_FA(2);  // study: compute on the first ring fill only
+        else if (var == 13) WF_FA(3);  // study: lazy rescale
+        else WF_FA(0);
+#undef WF_FA
+    } else if (var == 3) {
         const dim3 grid((M + 15) / 16, Hkv);
         if (kv8)
             hipLaunchKernelGGL((k_attn_prefill_ks<true>), grid, dim3(256), 0, st, q, q_rs, k, v, kv_sb, kv_sh, row_pos,

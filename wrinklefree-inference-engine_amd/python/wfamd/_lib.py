@@ -17,7 +17,7 @@ LIB_PATH = Path(os.environ.get("WF_BITNET_LIB", PKG_ROOT / "lib" / "libwfbitnet.
 WF_OK, WF_EINVAL, WF_EHIP, WF_ENOTSUP = 0, 1, 2, 3
 WF_F32, WF_BF16, WF_F16, WF_I8, WF_U8 = 0, 1, 2, 3, 4
 WF_FMT_I2S, WF_FMT_TQ, WF_FMT_I2S_MFMA = 0, 1, 2
-WF_PREFILL_ROW_GROUP = 16  # include/wf_bitnet.h
+WF_PREFILL_ROW_GROUP = 32  # include/wf_bitnet.h
 (WF_OP_EMBED, WF_OP_QKV, WF_OP_ATTN, WF_OP_O, WF_OP_GATE_UP, WF_OP_DOWN, WF_OP_LM_HEAD) = range(7)
 
 vp, i32, i64, f32 = C.c_void_p, C.c_int, C.c_int64, C.c_float
