@@ -328,7 +328,7 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
 // weight stream.
 // ---------------------------------------------------------------------------------------------
 constexpr int kAttnPartThreads = 256;
-template <int G>
+template <int G, int NS = kAttnPartSplits1>
 __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* __restrict__ q, int64_t q_sb,
                                                                 const uint16_t* __restrict__ K,
                                                                 const uint16_t* __restrict__ V, int64_t kv_sb,
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
     const int nh = (G == 1) ? 1 : grp;  // query heads of this block
     const int gid = threadIdx.x / LP, li = threadIdx.x % LP;
     const int Sb = min(seq_lens[b], S);
-    const int T = ((Sb + kAttnPartSplits - 1) / kAttnPartSplits + 15) / 16 * 16;
+    const int T = ((Sb + NS - 1) / NS + 15) / 16 * 16;
     const int t0 = s * T, t1 = min(t0 + T, Sb);
     WF_STAMP(0);
     __shared__ float sm_m[NG][G], sm_l[NG][G];
@@ -452,8 +452,8 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
             const float4 ov = *reinterpret_cast<const float4*>(&sm_o[w][h][d]);
             os[0] += ov.x * a; os[1] += ov.y * a; os[2] += ov.z * a; os[3] += ov.w * a;
         }
-        const int64_t rec = (int64_t)(b * Hq + hq0 + h) * kAttnPartSplits + s;
-        *reinterpret_cast<float4*>(o_out + part_o_off(rec / kAttnPartSplits, (int)(rec % kAttnPartSplits), d)) =
+        const int64_t rec = (int64_t)(b * Hq + hq0 + h) * NS + s;
+        *reinterpret_cast<float4*>(o_out + part_o_off<NS>(rec / NS, (int)(rec % NS), d)) =
             make_float4(os[0], os[1], os[2], os[3]);
         if (d == 0) ml_out[rec] = make_float2(mx, ls);
     }
@@ -1034,8 +1034,8 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_lds(const uint16_t* __r
 //   online softmax in log2 units: lane (c, h) holds keys j % 4 + 8 (j / 4) + 4 h of column c, so a
 //       column's max / sum needs one v_permlane32_swap, and the rescale factor is the lane's own;
 //   O^T (128 dims x 32 queries) += V^T . P^T: 8 MFMAs; P^T's fragments are the score lanes as they
-//       stand (keys permuted: k-slot i of lane half h = key 16 s + i % 4 + 8 (i / 4) + 4 h), V^T's
-//       fragments two 8-byte ds_reads of the V tile layout (keys contiguous per dim).
+//       stand (the QK MFMA takes the keys permuted so that k-slot i of lane half h is key
+//       16 s + 8 h + i), V^T's fragments one 16-byte ds_read of the V tile layout each.
 // Per-column causal limit (masking only on diagonal tiles), P rounded to bf16 for the P.V MFMA (a
 // bf16 flash SDPA), V rows past the block's last position zeroed (stale pages). Heavy row groups
 // (late positions) are launched first. A column's result depends only on its own key range (tiles
@@ -1061,7 +1061,8 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
                                                             int npages, int64_t kv_pgs, uint16_t* __restrict__ out,
                                                             int64_t o_rs) {
     constexpr int D = 128, P = kFaStages;
-    __shared__ __attribute__((aligned(16))) uint8_t ring[P * 16384];
+    constexpr int kSlot = 16384;  // K 8 KiB + V 8 KiB of one 32-key tile, as in the cache
+    __shared__ __attribute__((aligned(16))) uint8_t ring[P * kSlot];
     __shared__ int s_page[kPfMaxTiles];
     const int g = blockIdx.y, hq0 = g * 4;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
@@ -1093,7 +1094,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
     }
     auto issue = [&](int t) {  // wave w DMAs pieces 4w .. 4w + 3 of tile t (K 0..7, V 8..15)
         const int64_t blk = pt ? (int64_t)s_page[t] * kv_pgs : (int64_t)t * 4096;
-        uint8_t* st = ring + (t % P) * 16384;
+        uint8_t* st = ring + (t % P) * kSlot;
         if (STUDY == 2 && t >= P) return;  // study: no DMA after the first ring fill
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
@@ -1107,51 +1108,41 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int e = 0; e < 16; ++e) oacc[mt][e] = 0.f;
-    // K fragment offset of key c, dims 16 s + 8 h (k_tile_off * 2): (tau 16 + dg) 16 + row, x 16 bytes
-    const int koff = ((((c >> 2) & 1) * 16 + h) * 16 + 4 * (c >> 3) + (c & 3)) * 16;
-#pragma unroll
-    for (int t = 0; t < P - 1; ++t)
-        if (t < ntiles) issue(t);
-    for (int t = 0; t < ntiles; ++t) {
-        if (STUDY == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if (t + P - 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (P - 2)) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (t + P - 1 < ntiles) issue(t + P - 1);  // the slot of tile t - 1, read before this barrier
-        const int bs = 32 * t;
-        if (bs >= lim_w || STUDY == 1) continue;  // every column of this wave is done (wave-uniform)
-        const uint8_t* st = ring + (t % P) * 16384;
-        // all of the tile's K fragments in flight at once (hipcc otherwise issues two ds_reads per
-        // MFMA pair and waits for each), then the V fragments behind them: their LDS latency
-        // overlaps the QK MFMAs and the softmax
+    // Keys enter the QK MFMA permuted: row r of S^T is key o = r with bits 2 and 3 swapped. Lane
+    // (c, h) then holds, for j < 16, the score of key (j & 7) + 8 h + 16 (j >> 3), so the eight
+    // P^T k-slots of k-step s are keys 16 s + 8 h + 0..7: one 16-byte piece of the V tile layout
+    // (keys contiguous per dim). K fragment of row c, dims 16 s + 8 h (k_tile_off * 2):
+    // ((tau 16 + dg) 16 + row) x 16 bytes; K and V reads are bank-conflict-free.
+    const int o = (c & ~12) | ((c & 4) << 1) | ((c & 8) >> 1);
+    const int koff = ((((o >> 2) & 1) * 16 + h) * 16 + 4 * (o >> 3) + (o & 3)) * 16;
+    // S^T of one tile: all 8 K fragments in flight, then the 8 MFMAs (their results are read one
+    // iteration later: the QK of tile t + 1 runs on the matrix pipe during tile t's softmax)
+    auto qk = [&](const uint8_t* st, v16f_t& sacc) {
         uint4 kf[8];
-        uint2 va[4][2], vb[4][2];
 #pragma unroll
         for (int s2 = 0; s2 < 8; ++s2) kf[s2] = *reinterpret_cast<const uint4*>(st + koff + s2 * 512);
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-            const int d = 32 * mt + c, n = d >> 4, l = d & 15;
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                const uint8_t* vp = st + 8192 + ((n * 4 + 2 * s2) * 16 + l) * 16 + 8 * h;
-                va[mt][s2] = *reinterpret_cast<const uint2*>(vp);
-                vb[mt][s2] = *reinterpret_cast<const uint2*>(vp + 256);
-            }
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 8; ++s2) reg_fence(kf[s2]);
-        v16f_t sacc;
 #pragma unroll
         for (int e = 0; e < 16; ++e) sacc[e] = 0.f;
 #pragma unroll
         for (int s2 = 0; s2 < 8; ++s2)
             sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf_t, kf[s2]), qf[s2], sacc, 0, 0, 0);
+    };
+    // online softmax of tile t's scores, then O^T += V^T . P^T
+    auto softmax_pv = [&](const uint8_t* st, const v16f_t& sacc, int bs) {
+        uint4 vv[4][2];  // V^T fragments (dim 32 mt + c, keys 16 s + 8 h + 0..7): issued first
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+            const int d = 32 * mt + c, n = d >> 4, l = d & 15;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+                vv[mt][s2] = *reinterpret_cast<const uint4*>(st + 8192 + ((n * 4 + 2 * s2 + h) * 16 + l) * 16);
+        }
         float x[16], mx = -INFINITY;
         if (bs + 32 > lim_min) {  // diagonal tile: per-column limit
-            const int lim = lim_q - bs - 4 * h;
+            const int lim = lim_q - bs - 8 * h;
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
-                x[j] = (j & 3) + 8 * (j >> 2) < lim ? sacc[j] * sl2 : -INFINITY;
+                x[j] = (j & 7) + 16 * (j >> 3) < lim ? sacc[j] * sl2 : -INFINITY;
                 mx = fmaxf(mx, x[j]);
             }
         } else {
@@ -1162,8 +1153,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
             }
         }
         mx = swap32_max(mx);
-        float mnew = fmaxf(m_run, mx);  // finite: key 0 is valid for every column
-        if (STUDY == 3 && m_run != -INFINITY && mx <= m_run + 8.0f) mnew = m_run;  // lazy rescale (study)
+        const float mnew = fmaxf(m_run, mx);  // finite: key 0 is valid for every column
         const float alpha = __builtin_amdgcn_exp2f(m_run - mnew);
         m_run = mnew;
         float ps = 0.f;
@@ -1184,24 +1174,55 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
         }
         const v8bf_t pb0 = __builtin_bit_cast(v8bf_t, make_uint4(pk[0], pk[1], pk[2], pk[3]));
         const v8bf_t pb1 = __builtin_bit_cast(v8bf_t, make_uint4(pk[4], pk[5], pk[6], pk[7]));
-        const int limv = lim_b - bs - 4 * h;  // V keys past the block's last position: zero (stale)
+        const int limv = lim_b - bs - 8 * h;  // V keys past the block's last position: zero (stale)
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
-                uint2 a = va[mt][s2], b = vb[mt][s2];
-                if (limv < 32) {  // keys 16 s2 + {0..3} and 16 s2 + 8 + {0..3} (+ 4 h)
-                    const int k0 = 16 * s2, k1 = 16 * s2 + 8;
+                uint4 a = vv[mt][s2];
+                if (limv < 32) {  // keys 16 s2 + 8 h + 0..7
+                    const int k0 = 16 * s2;
                     a.x &= (k0 < limv ? 0xffffu : 0u) | (k0 + 1 < limv ? 0xffff0000u : 0u);
                     a.y &= (k0 + 2 < limv ? 0xffffu : 0u) | (k0 + 3 < limv ? 0xffff0000u : 0u);
-                    b.x &= (k1 < limv ? 0xffffu : 0u) | (k1 + 1 < limv ? 0xffff0000u : 0u);
-                    b.y &= (k1 + 2 < limv ? 0xffffu : 0u) | (k1 + 3 < limv ? 0xffff0000u : 0u);
+                    a.z &= (k0 + 4 < limv ? 0xffffu : 0u) | (k0 + 5 < limv ? 0xffff0000u : 0u);
+                    a.w &= (k0 + 6 < limv ? 0xffffu : 0u) | (k0 + 7 < limv ? 0xffff0000u : 0u);
                 }
-                const v8bf_t vf = __builtin_bit_cast(v8bf_t, make_uint4(a.x, a.y, b.x, b.y));
+                const v8bf_t vf = __builtin_bit_cast(v8bf_t, a);
                 oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, s2 ? pb1 : pb0, oacc[mt], 0, 0, 0);
             }
         }
+    };
+    // ring: tiles 0 .. P - 2 issued up front, tile t + P - 1 at iteration t (into tile t - 1's slot)
+#pragma unroll
+    for (int t = 0; t < P - 1; ++t)
+        if (t < ntiles) issue(t);
+    // tiles <= t landed, tiles t + 1 .. last_issued may stay in flight (4 DMAs per tile and wave)
+    auto wait_through = [&](int t, int last_issued) {
+        const int pending = min(ntiles - 1, last_issued) - t;
+        if (STUDY == 2 || pending <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (pending == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if (pending == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    };
+    v16f_t sa, sb;
+    wait_through(0, P - 2);
+    if (STUDY != 1) qk(ring, sa);
+    auto iter = [&](int t, v16f_t& cur, v16f_t& nxt) {
+        // tile t + 1 landed (one more in flight); everyone is done with tile t - 1's slot
+        if (t + 1 < ntiles) wait_through(t + 1, t + P - 2);
+        else __builtin_amdgcn_s_barrier();
+        if (t + P - 1 < ntiles) issue(t + P - 1);
+        if (STUDY == 1) return;
+        if (t + 1 < ntiles && 32 * (t + 1) < lim_w) qk(ring + ((t + 1) % P) * kSlot, nxt);
+        if (32 * t < lim_w) softmax_pv(ring + (t % P) * kSlot, cur, 32 * t);
+    };
+    int t = 0;
+    for (; t + 1 < ntiles; t += 2) {
+        iter(t, sa, sb);
+        iter(t + 1, sb, sa);
     }
+    if (t < ntiles) iter(t, sa, sb);
     const float inv = 1.0f / swap32_sum(l_run);
     if (qrow < M) {
         uint16_t* orow = out + (int64_t)qrow * o_rs + (int64_t)(hq0 + (c & 3)) * D;
@@ -1459,7 +1480,6 @@ int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const 
                                     row_slot, M, sl2, pt, pps, npages, kv_pgs, out, o_rs)
         if (var == 11) WF_FA(1);       // study: DMA + barriers only
         else if (var == 12) WF_FA(2);  // study: compute on the first ring fill only
-        else if (var == 13) WF_FA(3);  // study: lazy rescale
         else WF_FA(0);
 #undef WF_FA
     } else if (var == 3) {
@@ -1496,7 +1516,7 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
         // one block per query head (G = 1): 4x the blocks of one per kv head at Hq/Hkv = 4, a quarter
         // of the per-lane arithmetic (at batch 1 the kernel is latency-bound on its score/softmax
         // chain; the K/V re-reads of the group's heads hit L2)
-        hipLaunchKernelGGL((k_attn_part<1>), dim3(kAttnPartSplits, Hq, B), dim3(kAttnPartThreads), 0, st, q, q_sb, k, v,
+        hipLaunchKernelGGL((k_attn_part<1>), dim3(kAttnPartSplits1, Hq, B), dim3(kAttnPartThreads), 0, st, q, q_sb, k, v,
                            kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, ml, o);
         return check_launch("decode_attention_partials");
     }

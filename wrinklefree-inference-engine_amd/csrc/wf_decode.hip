@@ -126,7 +126,7 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
     // 1) the input row (issued first: vmcnt retires in order), 2) the weight stream, 3) residual
     NormRow<PPT == 0 ? 1 : PPT, kNT> nr;
     constexpr bool kAttnIn = (MODE == MODE_O && PPT > 0);
-    AttnRow<kAttnIn ? PPT : 1, kNT> ar;
+    AttnRow<kAttnIn ? PPT : 1, kNT, kAttnPartSplits1> ar;  // batch < 16: the k_attn_part records
     constexpr int kMaxPiecesPerThread = 8192 / 16 / kNT;  // staged int8: K_pad <= 8192
     uint4 apre[MB][kMaxPiecesPerThread];
     const int pieces16 = F::k_pad(K) / 16;
@@ -1233,14 +1233,14 @@ __global__ __launch_bounds__(512) void k_rownorm_tile8(const uint16_t* __restric
 }
 
 // Batch > 1 O-projection input: attention row from the partials -> rms_norm -> int8 codes.
-template <int PPT, bool TL = false>
+template <int PPT, bool TL = false, int NS = kAttnPartSplits>
 __global__ __launch_bounds__(kNT) void k_rownorm_attn(const float2* __restrict__ ml, const float* __restrict__ o, int Hq,
                                                       const uint16_t* __restrict__ nw, float eps, int8_t* __restrict__ q8,
                                                       int64_t q8s, float* __restrict__ sf, int* __restrict__ asum) {
     __shared__ float red[2 * kNT / 64];
     __shared__ int red_i[kNT / 64];
     const int b = blockIdx.x, K = Hq * 128;
-    AttnRow<PPT, kNT> ar;
+    AttnRow<PPT, kNT, NS> ar;
     ar.issue(ml, o, b, Hq, 128);
     NormRow<PPT, kNT> nr;
     nr.issue_w(nw, K);
@@ -1408,8 +1408,8 @@ struct wf_model {
     uint16_t *h_a = nullptr, *h_b = nullptr, *qbuf = nullptr, *act = nullptr, *hn = nullptr;
     int* dec_ws = nullptr;      // batched decode split-K partials
     size_t dec_ws_ints = 0;
-    float2* part_ml = nullptr;  // attention partials [B, Hq, kAttnPartSplits] (m, l)
-    float* part_o = nullptr;    // [B, Hq, kAttnPartSplits, head_dim] unnormalised o
+    float2* part_ml = nullptr;  // attention partials [B, Hq, splits] (m, l); splits 16 below B 16, else 8
+    float* part_o = nullptr;    // [B, Hq, splits, head_dim] unnormalised o
     int8_t* q8 = nullptr;   // batch > 1: activation codes of the next GEMV [B, q8_stride]
     float* act_sf = nullptr;
     int* act_sum = nullptr;
@@ -1628,16 +1628,17 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             a.part_ml = m->part_ml;
             a.part_o = m->part_o;
             if (B > 1) {
-#define WF_RA(PPTV, TL)                                                                                                 \
-    hipLaunchKernelGGL((k_rownorm_attn<PPTV, TL>), dim3(B), dim3(kNT), 0, st, m->part_ml, m->part_o, d.n_heads, a.nw, \
+// the records of decode_attention_partials: kAttnPartSplits1 per head below batch 16, else kAttnPartSplits
+#define WF_RA(PPTV, TL, NS)                                                                                                 \
+    hipLaunchKernelGGL((k_rownorm_attn<PPTV, TL, NS>), dim3(B), dim3(kNT), 0, st, m->part_ml, m->part_o, d.n_heads, a.nw, \
                        d.eps, m->q8, m->q8_stride, m->act_sf, m->act_sum)
-                const bool tl = d.wfmt == WF_FMT_I2S_MFMA;
+                const bool tl = d.wfmt == WF_FMT_I2S_MFMA, few = B < 16;
                 if (norm_ppt(H) == 1) {
-                    if (tl) WF_RA(1, true);
-                    else WF_RA(1, false);
+                    if (tl) { if (few) WF_RA(1, true, kAttnPartSplits1); else WF_RA(1, true, kAttnPartSplits); }
+                    else { if (few) WF_RA(1, false, kAttnPartSplits1); else WF_RA(1, false, kAttnPartSplits); }
                 } else {
-                    if (tl) WF_RA(2, true);
-                    else WF_RA(2, false);
+                    if (tl) { if (few) WF_RA(2, true, kAttnPartSplits1); else WF_RA(2, true, kAttnPartSplits); }
+                    else { if (few) WF_RA(2, false, kAttnPartSplits1); else WF_RA(2, false, kAttnPartSplits); }
                 }
 #undef WF_RA
                 if ((rc = check_launch("rownorm_attn"))) return rc;
@@ -1765,8 +1766,8 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
             m->dec_ws_ints = std::max(m->dec_ws_ints, (size_t)dec_split(sh[0], sh[1], nullptr) * B * sh[0]);
         WF_ALLOC(m->dec_ws, sizeof(int) * m->dec_ws_ints);
     }
-    WF_ALLOC(m->part_ml, sizeof(float2) * (size_t)B * d.n_heads * kAttnPartSplits);
-    WF_ALLOC(m->part_o, sizeof(float) * (size_t)B * d.n_heads * kAttnPartSplits * d.head_dim);
+    WF_ALLOC(m->part_ml, sizeof(float2) * (size_t)B * d.n_heads * kAttnPartSplitsMax);
+    WF_ALLOC(m->part_o, sizeof(float) * (size_t)B * d.n_heads * kAttnPartSplitsMax * d.head_dim);
     WF_ALLOC(m->hn, 2 * (size_t)((B + 15) / 16 * 16) * d.hidden);  // fragment layout: whole row tiles
     if ((d.wfmt == WF_FMT_I2S || d.wfmt == WF_FMT_I2S_MFMA) && B >= kDecMfmaMinB && d.vocab % 16 == 0 &&
         d.hidden % 32 == 0) {

@@ -318,15 +318,18 @@ __device__ __forceinline__ int64_t bf_tile_off(int r, int p, int H) {
     return ((((int64_t)(r >> 4) * (H >> 5) + (p >> 2)) << 6) + (r & 15) + 16 * (p & 3)) << 3;
 }
 
-constexpr int kAttnPartSplits = 8;
+constexpr int kAttnPartSplits = 8;    // records per (sequence, query head): batched decode (B >= 16)
+constexpr int kAttnPartSplits1 = 8;   // batch < 16 (16 measured: attention 5.70 -> 5.63 us, O input 6.01 -> 7.27 us)
+constexpr int kAttnPartSplitsMax = 16;
 // Float offset of element d of split s's unnormalised o in the decode-attention partials of (b, h)
 // (bh = b * Hq + h; head_dim 128): [bh][split][half = (d >> 2) & 1][d >> 3][4]. The merging reader
 // (AttnRow) gives each thread the 8-wide piece d0 = 8 t of every split and loads it as two halves:
 // for one (split, half) the threads of a wave read consecutive 16-byte slots -- one contiguous KiB
 // per wave-instruction (the plain [bh][split][d] order left every other 16-byte slot of each line
 // to the next instruction). (m, l) records stay [bh][split].
+template <int NS = kAttnPartSplits>
 __device__ __forceinline__ int64_t part_o_off(int64_t bh, int s, int d) {
-    return ((bh * kAttnPartSplits + s) * 2 + ((d >> 2) & 1)) * 64 + (d >> 3) * 4 + (d & 3);
+    return ((bh * NS + s) * 2 + ((d >> 2) & 1)) * 64 + (d >> 3) * 4 + (d & 3);
 }
 constexpr int kPrefillRowGroup = WF_PREFILL_ROW_GROUP;  // prefill rows per slot-uniform group (include/wf_bitnet.h)
 
@@ -346,10 +349,10 @@ __device__ __forceinline__ int64_t v_tile_off(int t, int d) {
     return ((((int64_t)blk * 8 + (d >> 4)) * 4 + (o >> 3)) * 16 + (d & 15)) * 8 + (o & 7);
 }
 
-template <int PPT, int NT>
+template <int PPT, int NT, int NS = kAttnPartSplits>
 struct AttnRow {
-    float4 ml[PPT][kAttnPartSplits / 2];  // (m0, l0, m1, l1) pairs
-    float4 oa[PPT][kAttnPartSplits], ob[PPT][kAttnPartSplits];
+    float4 ml[PPT][NS / 2];  // (m0, l0, m1, l1) pairs
+    float4 oa[PPT][NS], ob[PPT][NS];
     __device__ __forceinline__ void issue(const float2* __restrict__ ml_in, const float* __restrict__ o_in, int b, int Hq,
                                           int D) {
         const int npk = Hq * D / 8;
@@ -357,13 +360,13 @@ struct AttnRow {
         for (int i = 0; i < PPT; ++i) {
             const int pc = min((int)threadIdx.x + NT * i, npk - 1);
             const int h = (8 * pc) / D, d0 = 8 * pc - h * D;
-            const int64_t rec = (int64_t)(b * Hq + h) * kAttnPartSplits;
+            const int64_t rec = (int64_t)(b * Hq + h) * NS;
 #pragma unroll
-            for (int u = 0; u < kAttnPartSplits / 2; ++u) ml[i][u] = reinterpret_cast<const float4*>(ml_in + rec)[u];
+            for (int u = 0; u < NS / 2; ++u) ml[i][u] = reinterpret_cast<const float4*>(ml_in + rec)[u];
 #pragma unroll
-            for (int u = 0; u < kAttnPartSplits; ++u) {
-                oa[i][u] = *reinterpret_cast<const float4*>(o_in + part_o_off(b * Hq + h, u, d0));
-                ob[i][u] = *reinterpret_cast<const float4*>(o_in + part_o_off(b * Hq + h, u, d0 + 4));
+            for (int u = 0; u < NS; ++u) {
+                oa[i][u] = *reinterpret_cast<const float4*>(o_in + part_o_off<NS>(b * Hq + h, u, d0));
+                ob[i][u] = *reinterpret_cast<const float4*>(o_in + part_o_off<NS>(b * Hq + h, u, d0 + 4));
             }
         }
     }
@@ -371,9 +374,9 @@ struct AttnRow {
 #pragma unroll
         for (int i = 0; i < PPT; ++i) {
 #pragma unroll
-            for (int u = 0; u < kAttnPartSplits / 2; ++u) reg_fence(ml[i][u]);
+            for (int u = 0; u < NS / 2; ++u) reg_fence(ml[i][u]);
 #pragma unroll
-            for (int u = 0; u < kAttnPartSplits; ++u) {
+            for (int u = 0; u < NS; ++u) {
                 reg_fence(oa[i][u]);
                 reg_fence(ob[i][u]);
             }
@@ -383,18 +386,18 @@ struct AttnRow {
         const int npk = Hq * D / 8;
 #pragma unroll
         for (int i = 0; i < PPT; ++i) {
-            float mm[kAttnPartSplits], ll[kAttnPartSplits];
+            float mm[NS], ll[NS];
 #pragma unroll
-            for (int u = 0; u < kAttnPartSplits / 2; ++u) {
+            for (int u = 0; u < NS / 2; ++u) {
                 mm[2 * u] = ml[i][u].x; ll[2 * u] = ml[i][u].y;
                 mm[2 * u + 1] = ml[i][u].z; ll[2 * u + 1] = ml[i][u].w;
             }
             float M = mm[0];
 #pragma unroll
-            for (int u = 1; u < kAttnPartSplits; ++u) M = fmaxf(M, mm[u]);
+            for (int u = 1; u < NS; ++u) M = fmaxf(M, mm[u]);
             float L = 0.f, O[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int u = 0; u < kAttnPartSplits; ++u) {
+            for (int u = 0; u < NS; ++u) {
                 const float w = (mm[u] == -INFINITY) ? 0.f : __expf(mm[u] - M);
                 L = fmaf(w, ll[u], L);
                 const float ov[8] = {oa[i][u].x, oa[i][u].y, oa[i][u].z, oa[i][u].w,
