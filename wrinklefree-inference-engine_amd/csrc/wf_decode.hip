@@ -846,33 +846,33 @@ __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int b
 // Prefill GEMM (rows = prompt tokens) on the tile layouts with the decode step's fused epilogues:
 // the wf_mfma.h 128 x 256 tile main loop (pgemm_tile), then EpiDec<MODE> per 16 x 16 fragment
 // (correction, RoPE + K/V cache write through row_slot, residual, ReLU^2 * up).
-template <int MODE>
+template <int MODE, int TNW = 4>
 __global__ __launch_bounds__(512) void k_pgemm_fused(GemvArgs a, int nbm, int nbn) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kPgStages * kPgStage];
+    static_assert(MODE != MODE_QKV || TNW == 4, "the q|k|v epilogue stages 256 columns (two heads)");
+    constexpr int P = pg_stages<TNW>(), BC = pg_block_cols<TNW>();
+    __shared__ __attribute__((aligned(16))) uint8_t lds[P * pg_stage_bytes<TNW>()];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
     const int wr = wave >> 2, wc = wave & 3;
     int bm, bn;
     pg_tile_of(blockIdx.x, nbm, nbn, bm, bn);
-    v4i_t acc[4][4];
-    pgemm_tile<kPgStages>(a.w, a.q8, a.B, a.N, a.K, bm, bn, lds, acc);
-    // epilogue per row tile: the four column tiles' per-row inputs (scale, code sum, residual) are
-    // all issued before the first store -- one round trip per row tile instead of per fragment
-    // (stores in between would pin the loads behind them): o 159 -> 141, down 291 -> 274 us
+    v4i_t acc[4][TNW];
+    pgemm_tile<P, TNW>(a.w, a.q8, a.B, a.N, a.K, bm, bn, lds, acc);
     if constexpr (MODE == MODE_QKV) {
         pf_qkv_epilogue(a, bm, bn, acc, lds);
-        return;
-    }
+    } else {
+    // epilogue per row tile: the column tiles' per-row inputs (scale, code sum, residual) are all
+    // issued before the first store -- one round trip per row tile instead of per fragment (stores
+    // in between would pin the loads behind them): o 159 -> 141, down 291 -> 274 us
     EpiDec<MODE> e{&a};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int r0 = bm * 128 + (4 * wr + i) * 16;
-        EpiIn in[4];
+        EpiIn in[TNW];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) e.load(r0, bn * 256 + (4 * wc + j) * 16, l16, q, in[j]);
+        for (int j = 0; j < TNW; ++j) e.load(r0, bn * BC + (TNW * wc + j) * 16, l16, q, in[j]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) e.load_rope(bn * 256 + (4 * wc + j) * 16, l16, in[j]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) e.apply(r0, bn * 256 + (4 * wc + j) * 16, acc[i][j], l16, q, in[j]);
+        for (int j = 0; j < TNW; ++j) e.apply(r0, bn * BC + (TNW * wc + j) * 16, acc[i][j], l16, q, in[j]);
+    }
     }
 }
 
@@ -1884,8 +1884,16 @@ static void prefill_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, co
 
 template <int MODE>
 static void prefill_gemm(const GemvArgs& a, hipStream_t st) {
-    const int nbm = (a.B + 127) / 128, nbn = (a.N + 255) / 256;
-    hipLaunchKernelGGL((k_pgemm_fused<MODE>), dim3(nbm * nbn), dim3(512), 0, st, a, nbm, nbn);
+    const int nbm = (a.B + 127) / 128;
+    if constexpr (MODE != MODE_QKV) {
+        if (pg_wide(a.N)) {  // gate|up: 128 x 512 tiles
+            const int nbn = (a.N + 511) / 512;
+            hipLaunchKernelGGL((k_pgemm_fused<MODE, 8>), dim3(nbm * nbn), dim3(512), 0, st, a, nbm, nbn);
+            return;
+        }
+    }
+    const int nbn = (a.N + 255) / 256;
+    hipLaunchKernelGGL((k_pgemm_fused<MODE, 4>), dim3(nbm * nbn), dim3(512), 0, st, a, nbm, nbn);
 }
 }  // extern "C++"
 

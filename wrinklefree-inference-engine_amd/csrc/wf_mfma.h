@@ -136,9 +136,19 @@ __device__ __forceinline__ void tgemm_tile(const uint8_t* __restrict__ W, const 
 // range of logical tiles, walked in groups of 4 row blocks x all column blocks, so the A slabs and
 // weight columns a XCD's 32 resident blocks share stay in its L2.
 // ---------------------------------------------------------------------------------------------
-constexpr int kPgStage = 8 * 2048 + 16 * 512;  // 24 KiB
+constexpr int kPgStage = 8 * 2048 + 16 * 512;  // 24 KiB (TNW = 4)
 constexpr int kPgStages = 6;                    // 144 KiB: one block per CU, 4 stages in flight
 constexpr int kPgGroupRows = 4;
+// TNW column tiles per wave: 4 -> 128 x 256 block tiles (kPgStage, kPgStages), 8 -> 128 x 512 (a
+// third fewer L2 -> LDS bytes per MAC: 1/512 + 1/512 instead of 1/256 + 1/512; 32 KiB stages)
+template <int TNW>
+constexpr int pg_stage_bytes() { return 8 * 2048 + TNW * 4 * 512; }
+template <int TNW>
+constexpr int pg_stages() { return TNW == 4 ? kPgStages : 4; }
+template <int TNW>
+constexpr int pg_block_cols() { return TNW * 64; }
+// 512-column tiles where N fills them and there are enough of them for the chip
+inline bool pg_wide(int N) { return N % 512 == 0 && N >= 8192; }
 
 // XCD-aware grouped tile order (measured: 4 % less time than plain row-major order)
 __device__ __forceinline__ void pg_tile_of(int bid, int nbm, int nbn, int& bm, int& bn) {
@@ -150,10 +160,13 @@ __device__ __forceinline__ void pg_tile_of(int bid, int nbm, int nbn, int& bm, i
     bn = t / rows;
 }
 
-// Fragments of one stage for one wave: A row tiles 4 wr + i (both halves), W column tiles 4 wc + j.
+// Fragments of one stage for one wave: A row tiles 4 wr + i (both halves), W column tiles TNW wc + j.
+// At TNW = 8 the 128 accumulators leave no room for a second fragment set: each stage reads its
+// own fragments after its barrier (at TNW = 4 they are read one stage ahead).
+template <int TNW>
 struct PgFrag {
     v4i_t a[2][4];
-    uint2 w[4];
+    uint2 w[TNW == 4 ? TNW : 1];
 };
 
 // The fragments of stage c are read from LDS one iteration ahead (while the MFMAs of stage c - 1
@@ -161,30 +174,42 @@ struct PgFrag {
 // for stage c + 1 (vmcnt: stages c + 2 .. c + P - 2 may stay in flight), barrier, refill the slot
 // of stage c - 1 (its fragments were consumed by the MFMAs of iteration c - 1, before the
 // barrier), read stage c + 1's fragments, run stage c's MFMAs.
-// Main loop of one 128 x 256 tile (bm, bn): int32 sums of wave (wr, wc) = (wave >> 2, wave & 3) in
-// acc[i][j] = rows (4 wr + i) * 16 .., columns (4 wc + j) * 16 .. of the tile (C/D fragment layout).
-template <int P>
+// Main loop of one 128 x (64 TNW) tile (bm, bn): int32 sums of wave (wr, wc) = (wave >> 2, wave & 3)
+// in acc[i][j] = rows (4 wr + i) * 16 .., columns (TNW wc + j) * 16 .. of the tile (C/D layout).
+template <int P, int TNW = 4>
 __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const int8_t* __restrict__ A, int M, int N,
-                                           int K, int bm, int bn, uint8_t* lds, v4i_t (&acc)[4][4]) {
+                                           int K, int bm, int bn, uint8_t* lds, v4i_t (&acc)[4][TNW]) {
     static_assert(P >= 4, "two stages in flight beyond the one being read");
+    static_assert(TNW == 4 || TNW == 8, "256- or 512-column block tiles");
+    constexpr int SB = pg_stage_bytes<TNW>(), NDMA = 2 + TNW / 4;  // DMAs per wave per stage
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wr = wave >> 2, wc = wave & 3;
     const int nkb = K >> 7, nrt = (M + 15) >> 4, nct = N >> 4;
-    // DMA sources: A row tile 8 bm + wave (both halves), W column tiles 16 bn + 2 wave + (lane >= 32)
+    // DMA sources: A row tile 8 bm + wave (both halves); W column tiles 4 TNW bn + (TNW / 2) wave
+    // + 2 u + (lane >= 32), u < TNW / 4 (two 512-byte column tiles per KiB piece)
     const int rt = min(bm * 8 + wave, nrt - 1);
     const int8_t* asrc = A + ((int64_t)rt * nkb << 11) + lane * 16;
-    const int ct = min(bn * 16 + 2 * wave + (lane >> 5), nct - 1);
-    const uint8_t* wsrc = W + ((int64_t)ct * nkb << 9) + (lane & 31) * 16;
+    const uint8_t* wsrc[TNW / 4];
+#pragma unroll
+    for (int u = 0; u < TNW / 4; ++u) {
+        const int ct = min(bn * 4 * TNW + (TNW / 2) * wave + 2 * u + (lane >> 5), nct - 1);
+        wsrc[u] = W + ((int64_t)ct * nkb << 9) + (lane & 31) * 16;
+    }
     auto issue = [&](int kb) {
-        uint8_t* st = lds + (kb % P) * kPgStage;
+        uint8_t* st = lds + (kb % P) * SB;
         glds16_asm(asrc + ((int64_t)kb << 11), st + wave * 2048);
         glds16_asm(asrc + ((int64_t)kb << 11) + 1024, st + wave * 2048 + 1024);
-        glds16_asm(wsrc + ((int64_t)kb << 9), st + 16384 + wave * 1024);
-    };
-    auto read = [&](PgFrag& f, int kb) {
-        const uint8_t* st = lds + (kb % P) * kPgStage;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) f.w[j] = *reinterpret_cast<const uint2*>(st + 16384 + (4 * wc + j) * 512 + lane * 8);
+        for (int u = 0; u < TNW / 4; ++u) glds16_asm(wsrc[u] + ((int64_t)kb << 9), st + 16384 + ((TNW / 4) * wave + u) * 1024);
+    };
+    auto read_w = [&](uint2 (&w)[TNW], int kb) {
+        const uint8_t* st = lds + (kb % P) * SB;
+#pragma unroll
+        for (int j = 0; j < TNW; ++j) w[j] = *reinterpret_cast<const uint2*>(st + 16384 + (TNW * wc + j) * 512 + lane * 8);
+    };
+    auto read = [&](PgFrag<TNW>& f, int kb) {
+        const uint8_t* st = lds + (kb % P) * SB;
+        if constexpr (TNW == 4) read_w(f.w, kb);
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -194,43 +219,65 @@ __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const 
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = v4i_t{0, 0, 0, 0};
-    auto mma = [&](const PgFrag& f) {
+        for (int j = 0; j < TNW; ++j) acc[i][j] = v4i_t{0, 0, 0, 0};
+    auto mma = [&](const PgFrag<TNW>& fc, int kb) {
+        uint2 wl[TNW];
+        PgFrag<TNW> fl;  // TNW = 8: this stage's A fragments, read here (no second set in registers)
+        if constexpr (TNW == 4) {
+#pragma unroll
+            for (int j = 0; j < TNW; ++j) wl[j] = fc.w[j];
+        } else {
+            read_w(wl, kb);
+            read(fl, kb);
+        }
+        const PgFrag<TNW>& f = TNW == 4 ? fc : fl;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            v4i_t bf[4];
+            if constexpr (TNW == 4) {
+                v4i_t bf[TNW];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t w = h ? f.w[j].y : f.w[j].x;
-                bf[j] = v4i_t{(int)((w >> 6) & 0x03030303u), (int)((w >> 4) & 0x03030303u),
-                              (int)((w >> 2) & 0x03030303u), (int)(w & 0x03030303u)};
+                for (int j = 0; j < TNW; ++j) {
+                    const uint32_t w = h ? wl[j].y : wl[j].x;
+                    bf[j] = v4i_t{(int)((w >> 6) & 0x03030303u), (int)((w >> 4) & 0x03030303u),
+                                  (int)((w >> 2) & 0x03030303u), (int)(w & 0x03030303u)};
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < TNW; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[h][i], bf[j], acc[i][j], 0, 0, 0);
+            } else {  // one column tile's decoded B fragment live at a time (register budget)
+#pragma unroll
+                for (int j = 0; j < TNW; ++j) {
+                    const uint32_t w = h ? wl[j].y : wl[j].x;
+                    const v4i_t bf = v4i_t{(int)((w >> 6) & 0x03030303u), (int)((w >> 4) & 0x03030303u),
+                                           (int)((w >> 2) & 0x03030303u), (int)(w & 0x03030303u)};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[h][i], bf, acc[i][j], 0, 0, 0);
+                }
             }
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[h][i], bf[j], acc[i][j], 0, 0, 0);
         }
     };
     // one iteration: stage c + 1 published and read into `nxt`, stage c computed from `cur`
-    auto step = [&](int c, PgFrag& cur, PgFrag& nxt) {
+    auto step = [&](int c, PgFrag<TNW>& cur, PgFrag<TNW>& nxt) {
         if (c + 1 < nkb) {
-            if (c + P - 2 < nkb) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (P - 3)) : "memory");
+            if (c + P - 2 < nkb) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA * (P - 3)) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             if (c + P - 1 < nkb) issue(c + P - 1);
-            read(nxt, c + 1);
+            if constexpr (TNW == 4) read(nxt, c + 1);
         }
-        mma(cur);
+        mma(cur, c);
     };
 #pragma unroll
     for (int c = 0; c < P - 1; ++c)
         if (c < nkb) issue(c);
-    PgFrag f0, f1;
-    if (P - 2 < nkb) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (P - 2)) : "memory");
+    PgFrag<TNW> f0, f1;
+    if (P - 2 < nkb) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA * (P - 2)) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    read(f0, 0);
+    if constexpr (TNW == 4) read(f0, 0);
     int c = 0;
     for (; c + 1 < nkb; c += 2) {
         step(c, f0, f1);

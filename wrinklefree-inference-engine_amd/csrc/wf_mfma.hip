@@ -50,37 +50,48 @@ __global__ __launch_bounds__(256) void k_tgemm_lds(const uint8_t* __restrict__ W
     tgemm_tile<WR, P>(W, A, lda, M, N, K, blockIdx.y * 128, blockIdx.x * 64 * (4 / WR), lds, e);
 }
 
-template <int P>
+template <int TNW>
 __global__ __launch_bounds__(512) void k_pgemm_t(const uint8_t* __restrict__ W, const int8_t* __restrict__ A,
                                                  float scale, int M, int N, int K, float* __restrict__ Y, int64_t ldy,
                                                  int nbm, int nbn) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[P * kPgStage];
+    constexpr int P = pg_stages<TNW>();
+    __shared__ __attribute__((aligned(16))) uint8_t lds[P * pg_stage_bytes<TNW>()];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
     const int wr = wave >> 2, wc = wave & 3;
     int bm, bn;
     pg_tile_of(blockIdx.x, nbm, nbn, bm, bn);
-    v4i_t acc[4][4];
-    pgemm_tile<P>(W, A, M, N, K, bm, bn, lds, acc);
-    // Epilogue through LDS: the 128 x 256 fp32 tile (row stride 272 floats: the four lane quarters,
-    // 4 rows apart, land 16 banks apart) is written by fragment, then stored as whole rows, one KiB
-    // per wave-instruction (the fragment layout would store 64-byte pieces of 4 rows each).
+    v4i_t acc[4][TNW];
+    pgemm_tile<P, TNW>(W, A, M, N, K, bm, bn, lds, acc);
+    // Epilogue through LDS, 64 rows x 256 columns at a time: the fp32 tile (row stride 272 floats:
+    // the four lane quarters, 4 rows apart, land 16 banks apart) is written by fragment, then stored
+    // as whole rows, one KiB per wave-instruction (the fragment layout would store 64-byte pieces).
     constexpr int kRs = 272;
-    static_assert(128 * kRs * 4 <= P * kPgStage, "epilogue tile fits the ring");
+    static_assert(64 * kRs * 4 <= P * pg_stage_bytes<TNW>(), "epilogue tile fits the ring");
     float* tile = reinterpret_cast<float*>(lds);
-    __syncthreads();  // every wave is done reading the ring
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int hh = 0; hh < TNW / 4; ++hh) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int pr = 0; pr < 2; ++pr) {
+            __syncthreads();  // every wave is done reading the ring / the previous piece
+            if (wr == pr) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                tile[((4 * wr + i) * 16 + 4 * q + r) * kRs + (4 * wc + j) * 16 + l16] = (float)acc[i][j][r] * scale;
-    __syncthreads();
-    const int col = bn * 256 + lane * 4;
-    for (int rr = wave; rr < 128; rr += 8) {
-        const int row = bm * 128 + rr;
-        const float4 v = *reinterpret_cast<const float4*>(tile + rr * kRs + lane * 4);
-        if (row < M && col < N) *reinterpret_cast<float4*>(Y + (int64_t)row * ldy + col) = v;
+                for (int j = 0; j < TNW; ++j) {
+                    const int ct = TNW * wc + j - 16 * hh;  // column tile inside this 256-column half
+                    if (ct < 0 || ct >= 16) continue;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) tile[(i * 16 + 4 * q + r) * kRs + ct * 16 + l16] = (float)acc[i][j][r] * scale;
+                }
+            }
+            __syncthreads();
+            const int col = bn * pg_block_cols<TNW>() + hh * 256 + lane * 4;
+            for (int rr = wave; rr < 64; rr += 8) {
+                const int row = bm * 128 + 64 * pr + rr;
+                const float4 v = *reinterpret_cast<const float4*>(tile + rr * kRs + lane * 4);
+                if (row < M && col < N) *reinterpret_cast<float4*>(Y + (int64_t)row * ldy + col) = v;
+            }
+        }
     }
 }
 
@@ -136,8 +147,15 @@ extern "C" int wf_bitnet_gemm_tiled(const uint8_t* w, const int8_t* a, float sca
     WF_REQUIRE(K % 128 == 0 && N % 16 == 0, "gemm_tiled: K %% 128 == 0 and N %% 16 == 0 required (K=%d N=%d)", K, N);
     WF_REQUIRE(ldy >= N && ldy % 4 == 0 && aligned16(a) && aligned16(w) && aligned16(y),
                "gemm_tiled: bad ldy or unaligned operands (ldy %% 4 == 0, 16-byte aligned pointers)");
-    const int nbm = (M + 127) / 128, nbn = (N + 255) / 256;
-    hipLaunchKernelGGL((k_pgemm_t<kPgStages>), dim3(nbm * nbn), dim3(512), 0, as_stream(stream), w, a, scale, M, N, K,
-                       y, ldy, nbm, nbn);
+    const int nbm = (M + 127) / 128;
+    if (pg_wide(N)) {
+        const int nbn = (N + 511) / 512;
+        hipLaunchKernelGGL((k_pgemm_t<8>), dim3(nbm * nbn), dim3(512), 0, as_stream(stream), w, a, scale, M, N, K, y,
+                           ldy, nbm, nbn);
+    } else {
+        const int nbn = (N + 255) / 256;
+        hipLaunchKernelGGL((k_pgemm_t<4>), dim3(nbm * nbn), dim3(512), 0, as_stream(stream), w, a, scale, M, N, K, y,
+                           ldy, nbm, nbn);
+    }
     return check_launch("gemm_tiled");
 }
