@@ -148,7 +148,11 @@ constexpr int pg_stages() { return TNW == 4 ? kPgStages : 4; }
 template <int TNW>
 constexpr int pg_block_cols() { return TNW * 64; }
 // 512-column tiles where N fills them and there are enough of them for the chip
-inline bool pg_wide(int N) { return N % 512 == 0 && N >= 8192; }
+// (WF_PG_WIDE_MIN_N: study override of the 8192 threshold)
+inline bool pg_wide(int N) {
+    static const int min_n = getenv("WF_PG_WIDE_MIN_N") ? atoi(getenv("WF_PG_WIDE_MIN_N")) : 8192;
+    return N % 512 == 0 && N >= min_n;
+}
 
 // XCD-aware grouped tile order (measured: 4 % less time than plain row-major order)
 __device__ __forceinline__ void pg_tile_of(int bid, int nbm, int nbn, int& bm, int& bn) {
