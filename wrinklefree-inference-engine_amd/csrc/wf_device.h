@@ -156,7 +156,9 @@ __device__ __forceinline__ int8_t quant_one(float x, float sf) {
 }
 // Eight codes at once, bit-identical to quant_one. The exact product x * inv (inv = 1/s rounded)
 // is within 2^-17 of x/s for |x/s| <= 128, so rne(x/s) = rne(x * inv) unless x * inv lies within
-// 2^-13 of a half-integer; only then (p ~ 2.4e-4 per element) the lane redoes the IEEE divide.
+// 2^-13 of a half-integer; only then (p ~ 2.4e-4 per element) that element is redone with the
+// IEEE divide (per element: a wave pays one divide sequence when any of its lanes needs it for that
+// element, not eight -- with eight waves per block nearly every block had a wave on the slow path).
 // rne comes from the fma's own rounding: fma(x, inv, 1.5 * 2^23) keeps rne(x * inv) in the low
 // mantissa bits (low byte = the int8 code), fma(x, inv, -q) is the exact remainder. No clamp is
 // needed: s = max|x| / 127 bounds |x * inv| by 127 (1 + 2^-23). Returns the 8 codes packed
@@ -164,17 +166,13 @@ __device__ __forceinline__ int8_t quant_one(float x, float sf) {
 __device__ __forceinline__ uint2 quant8(const float (&x)[8], float sf, float inv, int& asum) {
     constexpr float kMagic = 12582912.0f;  // 1.5 * 2^23
     uint32_t b[8];
-    bool risky = false;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const float sm = fmaf(x[j], inv, kMagic);
         const float q = sm - kMagic;
-        risky |= fabsf(fmaf(x[j], inv, -q)) > 0.4998779296875f;  // 0.5 - 2^-13
         b[j] = __float_as_uint(sm);
-    }
-    if (risky) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) b[j] = __float_as_uint(fminf(fmaxf(rintf(x[j] / sf), -128.f), 127.f) + kMagic);
+        if (fabsf(fmaf(x[j], inv, -q)) > 0.4998779296875f)  // within 2^-13 of a half-integer
+            b[j] = __float_as_uint(fminf(fmaxf(rintf(x[j] / sf), -128.f), 127.f) + kMagic);
     }
     const uint32_t lo = __builtin_amdgcn_perm(b[1], b[0], 0x0c0c0400u) | __builtin_amdgcn_perm(b[3], b[2], 0x04000c0cu);
     const uint32_t hi = __builtin_amdgcn_perm(b[5], b[4], 0x0c0c0400u) | __builtin_amdgcn_perm(b[7], b[6], 0x04000c0cu);
