@@ -709,10 +709,10 @@ __global__ __launch_bounds__(NW * 64) void k_dec_gemm_t(GemvArgs a) {
 // are positions 8a .. 8a + 7 of one slot, else per element). The per-fragment form (scattered
 // 2-byte stores, two dependent loads per fragment) spilled its accumulators (272 B per lane).
 constexpr int kPfEpiRS = 256 * 2 + 16;  // LDS row stride of the staged tile (bytes)
+template <bool CW>
 __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int bn, const v4i_t (&acc)[4][4],
                                                 uint8_t* lds) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
-    const int wr = wave >> 2, wc = wave & 3;
     uint8_t* tile = lds;                                              // [128][kPfEpiRS]
     float* s_sf = reinterpret_cast<float*>(lds + 128 * kPfEpiRS);     // [128]
     int* s_as = reinterpret_cast<int*>(s_sf + 128);                    // [128]
@@ -734,13 +734,13 @@ __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int b
     const int head0 = bn * 2, nheads = g.Hq + 2 * g.Hkv;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int ct = 4 * wc + j, head = head0 + (ct >> 3);
-        const float ws = head < g.Hq ? g.ws0 : (head < g.Hq + g.Hkv ? g.ws1 : g.ws2);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+            const int ct = pg_frag_ct<4, CW>(wave, i, j), head = head0 + (ct >> 3);
+            const float ws = head < g.Hq ? g.ws0 : (head < g.Hq + g.Hkv ? g.ws1 : g.ws2);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int rl = (4 * wr + i) * 16 + 4 * q + r;
+                const int rl = pg_frag_rt<4, CW>(wave, i, j) * 16 + 4 * q + r;
                 const float v = rbf(corrected(acc[i][j][r], ws, s_as[rl], s_sf[rl]));
                 const float nv = dpp_f<DPP_QP_1032>(v);  // column l16 ^ 1
                 if (!(l16 & 1)) *reinterpret_cast<uint32_t*>(tile + rl * kPfEpiRS + (16 * ct + l16) * 2) = pk_bf16(v, nv);
@@ -843,22 +843,108 @@ __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int b
     }
 }
 
+// Prefill GU / O / DN epilogue, staged through the (idle) LDS ring: EpiDec's float sequence, but the
+// per-row inputs are loaded once per row into LDS, every wave writes its fragments' bf16 results
+// (GU: the act = bf16(bf16(relu(g)^2) * u) values) into a 128-row LDS tile, and the block then
+// stores whole 16-byte pieces of rows (O / DN: + the residual, read as 16-byte pieces). The
+// per-fragment form stored 2-byte elements, 32 or 64 per wave-instruction: measured with the main
+// loop removed, the GU epilogue alone took 103 us per layer at 16384 rows (store-issue bound;
+// ~28 us of HBM writes), O / DN 64 us, and with one block per CU it is not overlapped by MFMAs.
+// Needs out_stride % 8 == 0 and a 16-byte aligned out / resid (checked by the host).
+template <int MODE, int TNW, bool CW>
+__device__ __forceinline__ void pf_tile_epilogue(const GemvArgs& g, int bm, int bn, const v4i_t (&acc)[4][TNW],
+                                                 uint8_t* lds) {
+    static_assert(MODE == MODE_GU || MODE == MODE_O || MODE == MODE_DN, "row-tile epilogues");
+    constexpr int BC = pg_block_cols<TNW>();
+    constexpr int OC = MODE == MODE_GU ? BC / 2 : BC;  // output columns of the block
+    constexpr int RS = OC * 2 + 32;                     // LDS row stride: 4 rows of a fragment 8 banks apart
+    constexpr int PPR = OC / 8;                         // 16-byte pieces per row
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+    constexpr int IT = 128 * PPR / 512;                 // store items per thread
+    static_assert(IT * 512 == 128 * PPR, "whole items per thread");
+    uint8_t* tile = lds;
+    float* s_sf = reinterpret_cast<float*>(lds + 128 * RS);
+    int* s_as = reinterpret_cast<int*>(s_sf + 128);
+    const int limit = MODE == MODE_GU ? g.N / 2 : g.N;
+    // O / DN: every residual piece of this thread in flight before the LDS phase (a load inside the
+    // store loop would wait one HBM round trip per item: stores may alias it)
+    uint4 rsv[MODE == MODE_GU ? 1 : IT];
+    if constexpr (MODE != MODE_GU) {
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const int it = threadIdx.x + 512 * k, rl = it / PPR, pc = it % PPR;
+            const int m = min(bm * 128 + rl, g.B - 1), n = min(bn * OC + pc * 8, limit - 8);
+            rsv[k] = *reinterpret_cast<const uint4*>(g.resid + (int64_t)m * g.out_stride + n);
+        }
+    }
+    __syncthreads();  // every wave is done with the ring
+    if (threadIdx.x < 128) {
+        const int mc = min(bm * 128 + (int)threadIdx.x, g.B - 1);
+        s_sf[threadIdx.x] = g.act_sf[mc];
+        s_as[threadIdx.x] = g.act_sum[mc];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TNW; ++j) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int rt = pg_frag_rt<TNW, CW>(wave, i, j), ct = pg_frag_ct<TNW, CW>(wave, i, j);
+            const float ws = (MODE == MODE_GU && l16 >= 8) ? g.ws1 : g.ws0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int rl = rt * 16 + 4 * q + r;
+                const float v = rbf(corrected(acc[i][j][r], ws, s_as[rl], s_sf[rl]));
+                if constexpr (MODE == MODE_GU) {
+                    const float pv = __shfl_xor(v, 8, 64);  // up column l16 + 8 of the same row
+                    const float gt = fmaxf(v, 0.f);
+                    const float y = rbf(rbf(gt * gt) * pv);
+                    const float ny = dpp_f<DPP_QP_1032>(y);  // column l16 ^ 1
+                    if (l16 < 8 && !(l16 & 1)) *reinterpret_cast<uint32_t*>(tile + rl * RS + (ct * 8 + l16) * 2) = pk_bf16(y, ny);
+                } else {
+                    const float nv = dpp_f<DPP_QP_1032>(v);
+                    if (!(l16 & 1)) *reinterpret_cast<uint32_t*>(tile + rl * RS + (ct * 16 + l16) * 2) = pk_bf16(v, nv);
+                }
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const int it = threadIdx.x + 512 * k, rl = it / PPR, pc = it % PPR;
+        const int m = bm * 128 + rl, n = bn * OC + pc * 8;
+        if (m >= g.B || n >= limit) continue;
+        uint4 v = *reinterpret_cast<const uint4*>(tile + rl * RS + pc * 16);
+        if constexpr (MODE != MODE_GU) {  // out = bf16(resid + bf16(o))
+            const uint4 rs = rsv[k];
+            uint32_t ov[4] = {v.x, v.y, v.z, v.w};
+            const uint32_t rv[4] = {rs.x, rs.y, rs.z, rs.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                ov[e] = pk_bf16(rbf(bf_lo(rv[e]) + bf_lo(ov[e])), rbf(bf_hi(rv[e]) + bf_hi(ov[e])));
+            v = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+        }
+        *reinterpret_cast<uint4*>(g.out + (int64_t)m * g.out_stride + n) = v;
+    }
+}
+
 // Prefill GEMM (rows = prompt tokens) on the tile layouts with the decode step's fused epilogues:
 // the wf_mfma.h 128 x 256 tile main loop (pgemm_tile), then EpiDec<MODE> per 16 x 16 fragment
 // (correction, RoPE + K/V cache write through row_slot, residual, ReLU^2 * up).
-template <int MODE, int TNW = 4>
+template <int MODE, int TNW = 4, int ALG = 0, bool STAGED = false>
 __global__ __launch_bounds__(512) void k_pgemm_fused(GemvArgs a, int nbm, int nbn) {
     static_assert(MODE != MODE_QKV || TNW == 4, "the q|k|v epilogue stages 256 columns (two heads)");
-    constexpr int P = pg_stages<TNW>(), BC = pg_block_cols<TNW>();
-    __shared__ __attribute__((aligned(16))) uint8_t lds[P * pg_stage_bytes<TNW>()];
+    constexpr int BC = pg_block_cols<TNW>();
+    __shared__ __attribute__((aligned(16))) uint8_t lds[PgCfg<TNW, ALG>::LDS];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
-    const int wr = wave >> 2, wc = wave & 3;
+    constexpr bool CW = PgCfg<TNW, ALG>::CW;
     int bm, bn;
     pg_tile_of(blockIdx.x, nbm, nbn, bm, bn);
     v4i_t acc[4][TNW];
-    pgemm_tile<P, TNW>(a.w, a.q8, a.B, a.N, a.K, bm, bn, lds, acc);
+    pg_main<TNW, ALG>(a.w, a.q8, a.B, a.N, a.K, bm, bn, lds, acc);
     if constexpr (MODE == MODE_QKV) {
-        pf_qkv_epilogue(a, bm, bn, acc, lds);
+        pf_qkv_epilogue<CW>(a, bm, bn, acc, lds);
+    } else if constexpr (STAGED) {
+        pf_tile_epilogue<MODE, TNW, CW>(a, bm, bn, acc, lds);
     } else {
     // epilogue per row tile: the column tiles' per-row inputs (scale, code sum, residual) are all
     // issued before the first store -- one round trip per row tile instead of per fragment (stores
@@ -866,12 +952,14 @@ __global__ __launch_bounds__(512) void k_pgemm_fused(GemvArgs a, int nbm, int nb
     EpiDec<MODE> e{&a};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int r0 = bm * 128 + (4 * wr + i) * 16;
         EpiIn in[TNW];
 #pragma unroll
-        for (int j = 0; j < TNW; ++j) e.load(r0, bn * BC + (TNW * wc + j) * 16, l16, q, in[j]);
+        for (int j = 0; j < TNW; ++j)
+            e.load(bm * 128 + pg_frag_rt<TNW, CW>(wave, i, j) * 16, bn * BC + pg_frag_ct<TNW, CW>(wave, i, j) * 16, l16, q, in[j]);
 #pragma unroll
-        for (int j = 0; j < TNW; ++j) e.apply(r0, bn * BC + (TNW * wc + j) * 16, acc[i][j], l16, q, in[j]);
+        for (int j = 0; j < TNW; ++j)
+            e.apply(bm * 128 + pg_frag_rt<TNW, CW>(wave, i, j) * 16, bn * BC + pg_frag_ct<TNW, CW>(wave, i, j) * 16, acc[i][j], l16,
+                    q, in[j]);
     }
     }
 }
@@ -1882,18 +1970,39 @@ static void prefill_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, co
 #undef WF_RN8
 }
 
+// LDS-staged row-tile epilogue (pf_tile_epilogue) where the output rows are 16-byte pieces
+// (WF_PF_EPI=0: per-fragment EpiDec, for A/B studies)
+static bool pf_staged_ok(const GemvArgs& a, bool wide) {
+    // default: O / DN (256-column tiles; measured o 141 -> 131, down 275 -> 262 us per layer at 16384
+    // rows); the 512-column gate|up tile stays per fragment (staged: 570 -> 614 us)
+    static const int mode = getenv("WF_PF_EPI") ? atoi(getenv("WF_PF_EPI")) : 1;
+    const bool on = mode == 2 || (mode == 1 && !wide);
+    const bool al = a.out_stride % 8 == 0 && reinterpret_cast<uintptr_t>(a.out) % 16 == 0 &&
+                    (!a.resid || reinterpret_cast<uintptr_t>(a.resid) % 16 == 0);
+    return on && al;
+}
+template <int MODE, int TNW, int ALG>
+static void pg_launch(const GemvArgs& a, int nbm, int nbn, hipStream_t st) {
+    if (MODE != MODE_QKV && pf_staged_ok(a, TNW == 8))
+        hipLaunchKernelGGL((k_pgemm_fused<MODE, TNW, ALG, MODE != MODE_QKV>), dim3(nbm * nbn), dim3(512), 0, st, a, nbm, nbn);
+    else
+        hipLaunchKernelGGL((k_pgemm_fused<MODE, TNW, ALG, false>), dim3(nbm * nbn), dim3(512), 0, st, a, nbm, nbn);
+}
+template <int MODE, int TNW>
+static void pg_launch_alg(int alg, const GemvArgs& a, int nbm, int nbn, hipStream_t st) {
+    if (alg == 3) pg_launch<MODE, TNW, 3>(a, nbm, nbn, st);
+    else pg_launch<MODE, TNW, 0>(a, nbm, nbn, st);
+}
 template <int MODE>
 static void prefill_gemm(const GemvArgs& a, hipStream_t st) {
     const int nbm = (a.B + 127) / 128;
     if constexpr (MODE != MODE_QKV) {
         if (pg_wide(a.N)) {  // gate|up: 128 x 512 tiles
-            const int nbn = (a.N + 511) / 512;
-            hipLaunchKernelGGL((k_pgemm_fused<MODE, 8>), dim3(nbm * nbn), dim3(512), 0, st, a, nbm, nbn);
+            pg_launch_alg<MODE, 8>(pg_alg(true, 0), a, nbm, (a.N + 511) / 512, st);
             return;
         }
     }
-    const int nbn = (a.N + 255) / 256;
-    hipLaunchKernelGGL((k_pgemm_fused<MODE, 4>), dim3(nbm * nbn), dim3(512), 0, st, a, nbm, nbn);
+    pg_launch_alg<MODE, 4>(pg_alg(false, 0), a, nbm, (a.N + 255) / 256, st);
 }
 }  // extern "C++"
 

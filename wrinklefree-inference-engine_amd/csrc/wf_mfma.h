@@ -180,7 +180,23 @@ struct PgFrag {
 // barrier), read stage c + 1's fragments, run stage c's MFMAs.
 // Main loop of one 128 x (64 TNW) tile (bm, bn): int32 sums of wave (wr, wc) = (wave >> 2, wave & 3)
 // in acc[i][j] = rows (4 wr + i) * 16 .., columns (TNW wc + j) * 16 .. of the tile (C/D layout).
-template <int P, int TNW = 4>
+// CW (column waves, ALG 3): the same stages and DMAs, but wave w owns every row tile (0..7) of the
+// column tiles (TNW / 2) w + c, c < TNW / 2: each decoded weight fragment (7 VALU per 32-bit code
+// word) feeds 8 MFMAs instead of 4. Two waves per SIMD issue into one matrix pipe and share its
+// vector issue slots; an MFMA holds the issue for 8 of its 16 cycles, so at 4 MFMAs per decode the
+// pair needs ~1900 issue cycles per 2048 MFMA cycles (measured ~55 % MFMA busy); at 8 per decode
+// ~1500. acc[i][j] then holds row tile i + 4 (j / (TNW / 2)), column tile (TNW / 2) w + j % (TNW / 2)
+// (pg_frag_rt / pg_frag_ct).
+template <int TNW, bool CW>
+__device__ __forceinline__ int pg_frag_rt(int wave, int i, int j) {
+    return CW ? i + 4 * (j / (TNW / 2)) : 4 * (wave >> 2) + i;
+}
+template <int TNW, bool CW>
+__device__ __forceinline__ int pg_frag_ct(int wave, int i, int j) {
+    return CW ? (TNW / 2) * wave + j % (TNW / 2) : TNW * (wave & 3) + j;
+}
+
+template <int P, int TNW = 4, bool CW = false>
 __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const int8_t* __restrict__ A, int M, int N,
                                            int K, int bm, int bn, uint8_t* lds, v4i_t (&acc)[4][TNW]) {
     static_assert(P >= 4, "two stages in flight beyond the one being read");
@@ -224,7 +240,33 @@ __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const 
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < TNW; ++j) acc[i][j] = v4i_t{0, 0, 0, 0};
+    auto mma_cw = [&](int kb) {  // CW: fragments read here, each decoded B feeds 8 MFMAs
+        constexpr int CT = TNW / 2;
+        const uint8_t* st = lds + (kb % P) * SB;
+        uint2 wl[CT];
+#pragma unroll
+        for (int j = 0; j < CT; ++j) wl[j] = *reinterpret_cast<const uint2*>(st + 16384 + (CT * wave + j) * 512 + lane * 8);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            v4i_t fa[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) fa[r] = *reinterpret_cast<const v4i_t*>(st + r * 2048 + h * 1024 + lane * 16);
+#pragma unroll
+            for (int j = 0; j < CT; ++j) {
+                const uint32_t w = h ? wl[j].y : wl[j].x;
+                const v4i_t bf = v4i_t{(int)((w >> 6) & 0x03030303u), (int)((w >> 4) & 0x03030303u),
+                                       (int)((w >> 2) & 0x03030303u), (int)(w & 0x03030303u)};
+#pragma unroll
+                for (int r = 0; r < 8; ++r)
+                    acc[r & 3][(r >> 2) * CT + j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[r], bf, acc[r & 3][(r >> 2) * CT + j], 0, 0, 0);
+            }
+        }
+    };
     auto mma = [&](const PgFrag<TNW>& fc, int kb) {
+        if constexpr (CW) {
+            mma_cw(kb);
+            return;
+        }
         uint2 wl[TNW];
         PgFrag<TNW> fl;  // TNW = 8: this stage's A fragments, read here (no second set in registers)
         if constexpr (TNW == 4) {
@@ -264,15 +306,26 @@ __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const 
         }
     };
     // one iteration: stage c + 1 published and read into `nxt`, stage c computed from `cur`
+#ifdef WF_STAMPS
+#define WF_PG_STAMP(i) \
+    if (c == 8 || c == 9) WF_STAMP((i) + 5 * (c - 8))
+#else
+#define WF_PG_STAMP(i)
+#endif
     auto step = [&](int c, PgFrag<TNW>& cur, PgFrag<TNW>& nxt) {
+        WF_PG_STAMP(1);
         if (c + 1 < nkb) {
             if (c + P - 2 < nkb) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA * (P - 3)) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            WF_PG_STAMP(2);
             __builtin_amdgcn_s_barrier();
+            WF_PG_STAMP(3);
             if (c + P - 1 < nkb) issue(c + P - 1);
-            if constexpr (TNW == 4) read(nxt, c + 1);
+            if constexpr (TNW == 4 && !CW) read(nxt, c + 1);
         }
+        WF_PG_STAMP(4);
         mma(cur, c);
+        WF_PG_STAMP(5);
     };
 #pragma unroll
     for (int c = 0; c < P - 1; ++c)
@@ -281,13 +334,44 @@ __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const 
     if (P - 2 < nkb) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA * (P - 2)) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if constexpr (TNW == 4) read(f0, 0);
+    if constexpr (TNW == 4 && !CW) read(f0, 0);
     int c = 0;
     for (; c + 1 < nkb; c += 2) {
         step(c, f0, f1);
         step(c + 1, f1, f0);
     }
     if (c < nkb) step(c, f0, f1);
+#undef WF_PG_STAMP
+}
+
+// Main-loop choice of the prefill GEMM kernels: ALG 0 = pgemm_tile with waves 2 (rows) x 4
+// (columns), ALG 3 = the CW form (waves own column strips; each decoded weight fragment feeds 8
+// MFMAs). Measured at 16384 x 13824 x 2560: the standalone fp32-output GEMM (k_pgemm_t) 565 -> 527 us
+// with CW; the fused gate|up (k_pgemm_fused) 570 -> 580 us, and CW at 256-column tiles is slower
+// (every wave reads all 8 A row tiles: LDS-read bound), so CW is the default only for k_pgemm_t's
+// 512-column tiles. (Also measured and removed: two I2_S blocks per stage, a ping-pong form with
+// the two waves of a SIMD alternating compute / load half-steps, and a software-pipelined CW form
+// with the DMA pieces spread between the MFMAs -- none faster end to end; DESIGN.md.)
+template <int TNW, int ALG>
+struct PgCfg {
+    static_assert(ALG == 0 || ALG == 3, "main-loop forms");
+    static constexpr int P = pg_stages<TNW>();
+    static constexpr int SB = pg_stage_bytes<TNW>();
+    static constexpr int LDS = P * SB;
+    static constexpr bool CW = ALG == 3;  // fragment -> tile mapping: pg_frag_rt / pg_frag_ct
+};
+template <int TNW, int ALG>
+__device__ __forceinline__ void pg_main(const uint8_t* __restrict__ W, const int8_t* __restrict__ A, int M, int N,
+                                        int K, int bm, int bn, uint8_t* lds, v4i_t (&acc)[4][TNW]) {
+    pgemm_tile<PgCfg<TNW, ALG>::P, TNW, PgCfg<TNW, ALG>::CW>(W, A, M, N, K, bm, bn, lds, acc);
+}
+// study switches (read once): WF_PG_ALG for the 256-column tiles, WF_PG_ALG8 for the 512-column
+// ones (def: the default of the caller)
+inline int pg_alg(bool wide, int def) {
+    static const int alg = getenv("WF_PG_ALG") ? atoi(getenv("WF_PG_ALG")) : -1;
+    static const int alg8 = getenv("WF_PG_ALG8") ? atoi(getenv("WF_PG_ALG8")) : -1;
+    const int a = wide ? alg8 : alg;
+    return (a == 0 || a == 3) ? a : def;
 }
 
 }  // namespace wf

@@ -19,6 +19,7 @@
 
 #include "wf_common.h"
 #include "wf_device.h"
+#include "wf_norm.h"
 #include "wf_mfma.h"
 
 namespace wf {
@@ -50,40 +51,41 @@ __global__ __launch_bounds__(256) void k_tgemm_lds(const uint8_t* __restrict__ W
     tgemm_tile<WR, P>(W, A, lda, M, N, K, blockIdx.y * 128, blockIdx.x * 64 * (4 / WR), lds, e);
 }
 
-template <int TNW>
+template <int TNW, int ALG = 0>
 __global__ __launch_bounds__(512) void k_pgemm_t(const uint8_t* __restrict__ W, const int8_t* __restrict__ A,
                                                  float scale, int M, int N, int K, float* __restrict__ Y, int64_t ldy,
                                                  int nbm, int nbn) {
-    constexpr int P = pg_stages<TNW>();
-    __shared__ __attribute__((aligned(16))) uint8_t lds[P * pg_stage_bytes<TNW>()];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[PgCfg<TNW, ALG>::LDS];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
-    const int wr = wave >> 2, wc = wave & 3;
     int bm, bn;
+    WF_STAMP(0);
     pg_tile_of(blockIdx.x, nbm, nbn, bm, bn);
     v4i_t acc[4][TNW];
-    pgemm_tile<P, TNW>(W, A, M, N, K, bm, bn, lds, acc);
+    pg_main<TNW, ALG>(W, A, M, N, K, bm, bn, lds, acc);
+    WF_STAMP(11);
     // Epilogue through LDS, 64 rows x 256 columns at a time: the fp32 tile (row stride 272 floats:
     // the four lane quarters, 4 rows apart, land 16 banks apart) is written by fragment, then stored
     // as whole rows, one KiB per wave-instruction (the fragment layout would store 64-byte pieces).
     constexpr int kRs = 272;
-    static_assert(64 * kRs * 4 <= P * pg_stage_bytes<TNW>(), "epilogue tile fits the ring");
+    static_assert(64 * kRs * 4 <= PgCfg<TNW, ALG>::LDS, "epilogue tile fits the ring");
     float* tile = reinterpret_cast<float*>(lds);
 #pragma unroll
     for (int hh = 0; hh < TNW / 4; ++hh) {
 #pragma unroll
         for (int pr = 0; pr < 2; ++pr) {
             __syncthreads();  // every wave is done reading the ring / the previous piece
-            if (wr == pr) {
 #pragma unroll
-                for (int j = 0; j < TNW; ++j) {
-                    const int ct = TNW * wc + j - 16 * hh;  // column tile inside this 256-column half
-                    if (ct < 0 || ct >= 16) continue;
+            for (int j = 0; j < TNW; ++j)
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < 4; ++i) {
+                    constexpr bool CW = PgCfg<TNW, ALG>::CW;
+                    const int rt = pg_frag_rt<TNW, CW>(wave, i, j);
+                    const int ct = pg_frag_ct<TNW, CW>(wave, i, j) - 16 * hh;  // inside this 256-column half
+                    if ((rt >> 2) != pr || ct < 0 || ct >= 16) continue;
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) tile[(i * 16 + 4 * q + r) * kRs + ct * 16 + l16] = (float)acc[i][j][r] * scale;
+                    for (int r = 0; r < 4; ++r)
+                        tile[((rt & 3) * 16 + 4 * q + r) * kRs + ct * 16 + l16] = (float)acc[i][j][r] * scale;
                 }
-            }
             __syncthreads();
             const int col = bn * pg_block_cols<TNW>() + hh * 256 + lane * 4;
             for (int rr = wave; rr < 64; rr += 8) {
@@ -131,6 +133,8 @@ int launch_tgemm_mfma(const uint8_t* w, const int8_t* a, int64_t lda, float scal
 
 using namespace wf;
 
+WF_STAMP_READER(wf_debug_stamps_mfma)
+
 extern "C" int wf_codes_to_tiles(const int8_t* a, int64_t lda, int M, int K, int8_t* out, void* stream) {
     WF_REQUIRE(a && out && M > 0 && K > 0 && K % 128 == 0 && lda >= K && lda % 4 == 0 && ((uintptr_t)a & 3u) == 0,
                "codes_to_tiles: bad arguments (K %% 128 == 0, 4-byte aligned rows)");
@@ -148,14 +152,18 @@ extern "C" int wf_bitnet_gemm_tiled(const uint8_t* w, const int8_t* a, float sca
     WF_REQUIRE(ldy >= N && ldy % 4 == 0 && aligned16(a) && aligned16(w) && aligned16(y),
                "gemm_tiled: bad ldy or unaligned operands (ldy %% 4 == 0, 16-byte aligned pointers)");
     const int nbm = (M + 127) / 128;
-    if (pg_wide(N)) {
+#define WF_PGT(TNWV, ALGV, NBN) \
+    hipLaunchKernelGGL((k_pgemm_t<TNWV, ALGV>), dim3(nbm * (NBN)), dim3(512), 0, as_stream(stream), w, a, scale, M, N, K, y, \
+                       ldy, nbm, NBN)
+    if (pg_wide(N)) {  // 512-column tiles: CW main loop by default
         const int nbn = (N + 511) / 512;
-        hipLaunchKernelGGL((k_pgemm_t<8>), dim3(nbm * nbn), dim3(512), 0, as_stream(stream), w, a, scale, M, N, K, y,
-                           ldy, nbm, nbn);
+        if (pg_alg(true, 3) == 3) WF_PGT(8, 3, nbn);
+        else WF_PGT(8, 0, nbn);
     } else {
         const int nbn = (N + 255) / 256;
-        hipLaunchKernelGGL((k_pgemm_t<4>), dim3(nbm * nbn), dim3(512), 0, as_stream(stream), w, a, scale, M, N, K, y,
-                           ldy, nbm, nbn);
+        if (pg_alg(false, 0) == 3) WF_PGT(4, 3, nbn);
+        else WF_PGT(4, 0, nbn);
     }
+#undef WF_PGT
     return check_launch("gemm_tiled");
 }

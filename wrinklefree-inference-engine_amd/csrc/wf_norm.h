@@ -80,14 +80,22 @@ constexpr int kStampBlocks = 16384;
 __attribute__((visibility("hidden"))) static __device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
 // slot i of wave w lives at column 16 w + i; wave 0 also records the shader clock (s_memtime) of
 // slot i in column 64 + i (clock rate = d(memtime) / d(memrealtime) * 100 MHz)
+// WF_STAMPS_EVEN: record the even waves 0, 2, 4, 6 (columns 0, 16, 32, 48) instead of waves 0..3
+#ifdef WF_STAMPS_EVEN
+#define WF_STAMP_WAVE_OK ((threadIdx.x >> 6) % 2 == 0 && threadIdx.x < 512)
+#define WF_STAMP_COL (16 * ((threadIdx.x >> 6) >> 1))
+#else
+#define WF_STAMP_WAVE_OK (threadIdx.x < 256)
+#define WF_STAMP_COL (16 * (threadIdx.x >> 6))
+#endif
 #define WF_STAMP(i)                                                                                 \
     do {                                                                                            \
         __builtin_amdgcn_sched_barrier(0);                                                          \
-        if ((threadIdx.x & 63) == 0 && threadIdx.x < 256) {                                         \
+        if ((threadIdx.x & 63) == 0 && WF_STAMP_WAVE_OK) {                                          \
             const unsigned sb_ = blockIdx.x + 2048u * blockIdx.y + 8192u * blockIdx.z;               \
             if (sb_ < (unsigned)::wf::kStampBlocks) {                                                \
                 unsigned long long* row_ = ::wf::g_stamps + (size_t)sb_ * ::wf::kStampSlots;          \
-                row_[16 * (threadIdx.x >> 6) + (i)] = __builtin_amdgcn_s_memrealtime();              \
+                row_[WF_STAMP_COL + (i)] = __builtin_amdgcn_s_memrealtime();                         \
                 if (threadIdx.x == 0) row_[64 + (i)] = __builtin_amdgcn_s_memtime();                  \
             }                                                                                       \
         }                                                                                           \
