@@ -1059,15 +1059,29 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
                                                             const int32_t* __restrict__ row_slot, int M,
                                                             float sl2, const int32_t* __restrict__ pt, int pps,
                                                             int npages, int64_t kv_pgs, uint16_t* __restrict__ out,
-                                                            int64_t o_rs) {
+                                                            int64_t o_rs, int xchunk) {
     constexpr int D = 128, P = kFaStages;
     constexpr int kSlot = 16384;  // K 8 KiB + V 8 KiB of one 32-key tile, as in the cache
     __shared__ __attribute__((aligned(16))) uint8_t ring[P * kSlot];
     __shared__ int s_page[kPfMaxTiles];
-    const int g = blockIdx.y, hq0 = g * 4;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
     const int nrb = M / 32;
-    const int rb = (nrb - 1 - (int)blockIdx.x) * 32;  // late (heavy) row groups first
+    // Work item = (kv head g, row group rbi), g-major, so consecutive items share a sequence's K/V.
+    // xchunk > 0 (1-D grid of 8 xchunk blocks): the blocks one XCD receives (b % 8, dealt round-robin)
+    // take one contiguous chunk of xchunk items, last first -- an XCD streams one (sequence, kv head)
+    // K/V at a time out of its own L2, heavy (late) row groups of it first. Else: grid (nrb, Hkv),
+    // late row groups first.
+    int g, rbi;
+    if (xchunk > 0) {
+        const int b = blockIdx.x, item = (b & 7) * xchunk + (xchunk - 1 - (b >> 3));
+        g = item / nrb;
+        rbi = item - g * nrb;
+    } else {
+        g = blockIdx.y;
+        rbi = nrb - 1 - (int)blockIdx.x;
+    }
+    const int hq0 = g * 4;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
+    const int rb = rbi * 32;
     const int slot = __builtin_amdgcn_readfirstlane(row_slot[rb]);
     const int qrow = rb + 8 * wave + (c >> 2);
     const int lim_q = row_pos[qrow] + 1;  // keys [0, lim_q) of column c
@@ -1154,13 +1168,15 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
         }
         mx = swap32_max(mx);
         const float mnew = fmaxf(m_run, mx);  // finite: key 0 is valid for every column
-        const float alpha = __builtin_amdgcn_exp2f(m_run - mnew);
+        const float alpha = STUDY == 3 ? 1.0f : __builtin_amdgcn_exp2f(m_run - mnew);
         m_run = mnew;
         float ps = 0.f;
         uint32_t pk[8];
 #pragma unroll
         for (int j = 0; j < 16; j += 2) {
-            const float p0 = __builtin_amdgcn_exp2f(x[j] - mnew), p1 = __builtin_amdgcn_exp2f(x[j + 1] - mnew);
+            // (study 3: no exponentials -- the softmax's transcendental cost)
+            const float p0 = STUDY == 3 ? x[j] - mnew : __builtin_amdgcn_exp2f(x[j] - mnew);
+            const float p1 = STUDY == 3 ? x[j + 1] - mnew : __builtin_amdgcn_exp2f(x[j + 1] - mnew);
             ps += p0;
             ps += p1;
             pk[j >> 1] = pk_bf16(p0, p1);
@@ -1188,6 +1204,12 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
                     a.w &= (k0 + 6 < limv ? 0xffffu : 0u) | (k0 + 7 < limv ? 0xffff0000u : 0u);
                 }
                 const v8bf_t vf = __builtin_bit_cast(v8bf_t, a);
+                if (STUDY == 4) {  // study: no P.V MFMAs (keep the operands live)
+                    uint4 pa = __builtin_bit_cast(uint4, s2 ? pb1 : pb0);
+                    reg_fence(a);
+                    reg_fence(pa);
+                    continue;
+                }
                 oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, s2 ? pb1 : pb0, oacc[mt], 0, 0, 0);
             }
         }
@@ -1474,12 +1496,17 @@ int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const 
     if (int rc = prefill_attention_check(Hq, Hkv, pps)) return rc;
     const int var = prefill_attention_variant();
     if ((var == 0 || var >= 10) && !kv8 && pps <= kPfMaxTiles && M % 32 == 0) {
-        const dim3 grid(M / 32, Hkv);
+        // XCD-chunked order when the items split evenly over the 8 XCDs (WF_PF_XCD=0: off)
+        static const bool xcd_on = !getenv("WF_PF_XCD") || atoi(getenv("WF_PF_XCD")) != 0;
+        const int items = (M / 32) * Hkv, xchunk = (xcd_on && items % 8 == 0) ? items / 8 : 0;
+        const dim3 grid = xchunk ? dim3(items) : dim3(M / 32, Hkv);
         const float sl2 = sm_scale * 1.4426950408889634f;
 #define WF_FA(S) hipLaunchKernelGGL((k_attn_prefill_fa<S>), grid, dim3(256), 0, st, q, q_rs, k, v, kv_sb, kv_sh, row_pos, \
-                                    row_slot, M, sl2, pt, pps, npages, kv_pgs, out, o_rs)
+                                    row_slot, M, sl2, pt, pps, npages, kv_pgs, out, o_rs, xchunk)
         if (var == 11) WF_FA(1);       // study: DMA + barriers only
         else if (var == 12) WF_FA(2);  // study: compute on the first ring fill only
+        else if (var == 13) WF_FA(3);  // study: no exponentials
+        else if (var == 14) WF_FA(4);  // study: no P.V MFMAs
         else WF_FA(0);
 #undef WF_FA
     } else if (var == 3) {
