@@ -84,6 +84,7 @@ struct GemvArgs {
     // FP8 (e4m3fn) K/V cache: stored code = e4m3(clamp(y / scale, +-448)), RNE
     int kv8;
     float k_inv, v_inv;
+    int gu_quad;  // GU epilogue: quad-transposed 8-byte act stores (EpiDec; WF_GU_QUAD=0: per element)
 };
 
 __device__ __forceinline__ uint8_t to_fp8(float y) {
@@ -404,6 +405,29 @@ struct EpiDec {
     __device__ __forceinline__ void apply(int r0, int c0, const v4i_t& acc, int l16, int q, const EpiIn& in) {
         const GemvArgs& g = *a;
         const int tile = c0 >> 4, n = c0 + l16, B = g.B, N = g.N;
+        if constexpr (MODE == MODE_GU) {
+            // 16-column fragment = gate columns 8 tile .. + 7 (lanes l16 < 8) and their up columns (l16
+            // + 8): act rows 4q + r, 8 columns. The 4 x 4 blocks of act values in each lane quad are
+            // transposed (4 DPP moves) so that lane (quad k, qi) holds row 4q + qi, columns 4k .. 4k + 3:
+            // one 8-byte store per lane instead of four 2-byte ones (the stores were the epilogue's cost:
+            // a quarter of them took the prefill gate|up GEMM from 570 to 472 us per layer).
+            if (g.gu_quad && ((g.out_stride & 3) | (reinterpret_cast<uintptr_t>(g.out) & 7)) == 0) {
+                const float ws = l16 < 8 ? g.ws0 : g.ws1;
+                float y[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float v = rbf(corrected(acc[r], ws, in.as[r], in.sf[r]));
+                    const float pv = dpp_f<DPP_ROW_ROR8>(v);  // partner column l16 ^ 8 (same rows)
+                    const float gt = fmaxf(v, 0.f);
+                    y[r] = rbf(rbf(gt * gt) * pv);
+                }
+                const int qi = l16 & 3, m = r0 + 4 * q + qi;
+                const uint2 pk = quad_transpose_bf16(y, qi);
+                if (l16 < 8 && m < B && tile * 16 < N)
+                    *reinterpret_cast<uint2*>(g.out + (int64_t)m * g.out_stride + tile * 8 + 4 * (l16 >> 2)) = pk;
+                return;
+            }
+        }
         float ws = g.ws0;
         int proj = 0, head = 0, tt = 0;
         if constexpr (MODE == MODE_QKV) {
@@ -422,6 +446,9 @@ struct EpiDec {
                 const float pv = __shfl_xor(v, 8, 64);  // partner column l16 ^ 8 (same rows)
                 if (m >= B || tile * 16 >= N) continue;
                 if constexpr (MODE == MODE_GU) {
+#ifdef WF_GU_EPI_STUDY  // diagnostic build: a quarter of the act stores (store-issue cost)
+                    if (r != 0) continue;
+#endif
                     if (l16 < 8) {
                         const float gt = fmaxf(v, 0.f);
                         g.out[(int64_t)m * g.out_stride + tile * 8 + l16] = f2bf(rbf(rbf(gt * gt) * pv));
@@ -1666,6 +1693,8 @@ GemvArgs base_args(const wf_model* m, int l) {
     a.v_inv = d.kv_fp8 ? 1.0f / m->kv_scale[2 * l + 1] : 1.0f;
     a.kv_b_stride = (int64_t)d.n_kv_heads * d.max_seq * d.head_dim;
     a.kv_t = m->kv_tiled;
+    static const int gu_quad = getenv("WF_GU_QUAD") ? atoi(getenv("WF_GU_QUAD")) : 1;
+    a.gu_quad = gu_quad;
     return a;
 }
 

@@ -55,7 +55,7 @@ __device__ __forceinline__ void store_from_f32(void* p, int64_t i, int dt, float
 // ~8 cycles per step instead of an LDS-latency ds_bpermute per step.
 // ---------------------------------------------------------------------------------------------
 enum : int { DPP_QP_1032 = 0xB1, DPP_QP_2301 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140,
-             DPP_BCAST15 = 0x142, DPP_BCAST31 = 0x143 };
+             DPP_BCAST15 = 0x142, DPP_BCAST31 = 0x143, DPP_ROW_ROR8 = 0x128 };
 template <int CTRL, int ROW_MASK = 0xF>
 __device__ __forceinline__ int dpp_i(int v, int old = 0) {
     return __builtin_amdgcn_update_dpp(old, v, CTRL, ROW_MASK, 0xF, false);
@@ -69,6 +69,28 @@ __device__ __forceinline__ T dpp_cast(T v, T old = T(0)) {
     if constexpr (__is_same(T, float)) return dpp_f<CTRL, ROW_MASK>(v, old);
     else return dpp_i<CTRL, ROW_MASK>(v, old);
 }
+// 4 x 4 transpose of bf16 values inside each lane quad: lane qi holds y[r] = M[qi][r] (float,
+// bf16-representable); returns row qi of M^T packed as bf16 pairs: (M[0][qi], M[1][qi]),
+// (M[2][qi], M[3][qi]). Two DPP exchanges: 2 x 2 blocks across lanes qi ^ 2, then 16-bit halves
+// across lanes qi ^ 1 (v_perm_b32 selects the halves).
+__device__ __forceinline__ uint2 quad_transpose_bf16(const float (&y)[4], int qi) {
+    const uint32_t A = pk_bf16(y[0], y[1]), B = pk_bf16(y[2], y[3]);
+    const bool hi2 = qi & 2, odd = qi & 1;
+    // own = (M[qi][r0], M[qi][r0 + 1]), other = (M[qi ^ 2][r0], M[qi ^ 2][r0 + 1]), r0 = qi & 2
+    const uint32_t own = hi2 ? B : A;
+    const uint32_t other = (uint32_t)dpp_i<DPP_QP_2301>((int)(hi2 ? A : B));
+    const uint32_t lo = __builtin_amdgcn_perm(other, own, 0x05040100u);  // (own.lo, other.lo)
+    const uint32_t hi = __builtin_amdgcn_perm(other, own, 0x07060302u);  // (own.hi, other.hi)
+    // even lanes keep the low halves (row qi = r0), odd ones the high halves (row r0 + 1)
+    const uint32_t keep = odd ? hi : lo;
+    const uint32_t got = (uint32_t)dpp_i<DPP_QP_1032>((int)(odd ? lo : hi));
+    // keep = (M[qi][qi], M[qi ^ 2][qi]), got = (M[qi ^ 1][qi], M[qi ^ 3][qi])
+    const uint32_t x = odd ? got : keep;  // (M[qi & 2][qi], M[(qi & 2) ^ 2][qi])
+    const uint32_t z = odd ? keep : got;  // (M[(qi & 2) | 1][qi], M[((qi & 2) | 1) ^ 2][qi])
+    const uint32_t p01 = __builtin_amdgcn_perm(z, x, 0x05040100u), p23 = __builtin_amdgcn_perm(z, x, 0x07060302u);
+    return hi2 ? make_uint2(p23, p01) : make_uint2(p01, p23);
+}
+
 struct OpAdd {
     template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return a + b; }
 };
