@@ -817,3 +817,31 @@ def test_prefill_attention_study_variants(variant):
                        env=env, cwd=root, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert f"{len(tests)} passed" in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.parametrize("env", [
+    "WF_PG_WIDE_MIN_N=512",                        # 512-column tiles for gate|up (and o / down: per fragment)
+    "WF_PG_WIDE_MIN_N=512 WF_PF_EPI=2",            # + the staged gate|up epilogue
+    "WF_PG_WIDE_MIN_N=512 WF_PG_ALG=3 WF_PG_ALG8=3",  # column-wave main loops everywhere
+    "WF_PF_EPI=0 WF_GU_QUAD=0 WF_PF_XCD=0",        # per-fragment epilogues, per-element act stores, plain order
+])
+def test_prefill_gemm_and_epilogue_switches(env):
+    """The prefill GEMM's non-default forms -- 128 x 512 tiles at the small test model's widths
+    (WF_PG_WIDE_MIN_N), the column-wave main loop, the staged / per-fragment epilogues, the
+    per-element gate|up stores and the plain attention block order -- pass the same prefill parity
+    tests as the defaults (bit-exact integer GEMM, K/V and logits against teacher-forced decode;
+    chunked = one shot). The switches are read once per process: child process."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    tests = ["test_prefill_matches_teacher_forced_decode", "test_prefill_in_pieces_equals_one_shot",
+             "test_fp8_kv_prefill"]
+    env_d = dict(os.environ)
+    env_d.update(kv.split("=") for kv in env.split())
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
+                        str(root / "tests" / "test_gpu_parity.py"), "-k", " or ".join(tests)],
+                       env=env_d, cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert f"{len(tests)} passed" in r.stdout, r.stdout[-2000:]

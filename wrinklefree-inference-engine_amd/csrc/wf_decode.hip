@@ -878,6 +878,10 @@ __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int b
 // loop removed, the GU epilogue alone took 103 us per layer at 16384 rows (store-issue bound;
 // ~28 us of HBM writes), O / DN 64 us, and with one block per CU it is not overlapped by MFMAs.
 // Needs out_stride % 8 == 0 and a 16-byte aligned out / resid (checked by the host).
+template <int MODE, int TNW>
+constexpr int pf_tile_epilogue_bytes() {  // staged tile + per-row scale / code sum
+    return 128 * ((MODE == MODE_GU ? pg_block_cols<TNW>() / 2 : pg_block_cols<TNW>()) * 2 + 32) + 128 * 8;
+}
 template <int MODE, int TNW, bool CW>
 __device__ __forceinline__ void pf_tile_epilogue(const GemvArgs& g, int bm, int bn, const v4i_t (&acc)[4][TNW],
                                                  uint8_t* lds) {
@@ -886,6 +890,7 @@ __device__ __forceinline__ void pf_tile_epilogue(const GemvArgs& g, int bm, int 
     constexpr int OC = MODE == MODE_GU ? BC / 2 : BC;  // output columns of the block
     constexpr int RS = OC * 2 + 32;                     // LDS row stride: 4 rows of a fragment 8 banks apart
     constexpr int PPR = OC / 8;                         // 16-byte pieces per row
+    static_assert(pf_tile_epilogue_bytes<MODE, TNW>() <= PgCfg<TNW, CW ? 3 : 0>::LDS, "staged tile fits the ring");
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
     constexpr int IT = 128 * PPR / 512;                 // store items per thread
     static_assert(IT * 512 == 128 * PPR, "whole items per thread");
@@ -2012,8 +2017,10 @@ static bool pf_staged_ok(const GemvArgs& a, bool wide) {
 }
 template <int MODE, int TNW, int ALG>
 static void pg_launch(const GemvArgs& a, int nbm, int nbn, hipStream_t st) {
-    if (MODE != MODE_QKV && pf_staged_ok(a, TNW == 8))
-        hipLaunchKernelGGL((k_pgemm_fused<MODE, TNW, ALG, MODE != MODE_QKV>), dim3(nbm * nbn), dim3(512), 0, st, a, nbm, nbn);
+    // (the 512-column o / down tile of a wide model does not fit the staged tile into the ring)
+    constexpr bool kStaged = MODE != MODE_QKV && pf_tile_epilogue_bytes<MODE, TNW>() <= PgCfg<TNW, ALG>::LDS;
+    if (kStaged && pf_staged_ok(a, TNW == 8))
+        hipLaunchKernelGGL((k_pgemm_fused<MODE, TNW, ALG, kStaged>), dim3(nbm * nbn), dim3(512), 0, st, a, nbm, nbn);
     else
         hipLaunchKernelGGL((k_pgemm_fused<MODE, TNW, ALG, false>), dim3(nbm * nbn), dim3(512), 0, st, a, nbm, nbn);
 }

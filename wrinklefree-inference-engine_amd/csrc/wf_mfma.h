@@ -320,13 +320,18 @@ __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const 
             WF_PG_STAMP(2);
             __builtin_amdgcn_s_barrier();
             WF_PG_STAMP(3);
+#if !defined(WF_PG_STUDY) || WF_PG_STUDY != 1  // diagnostic build 1: no ring refills
             if (c + P - 1 < nkb) issue(c + P - 1);
+#endif
             if constexpr (TNW == 4 && !CW) read(nxt, c + 1);
         }
         WF_PG_STAMP(4);
         mma(cur, c);
         WF_PG_STAMP(5);
     };
+#if defined(WF_PG_STUDY) && WF_PG_STUDY == 5  // diagnostic build 5: no main loop (epilogue cost)
+    return;
+#endif
 #pragma unroll
     for (int c = 0; c < P - 1; ++c)
         if (c < nkb) issue(c);
