@@ -845,3 +845,30 @@ def test_prefill_gemm_and_epilogue_switches(env):
                        env=env_d, cwd=root, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert f"{len(tests)} passed" in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.parametrize("env", ["WF_ATTN_VARIANT=1", "WF_ATTN_VARIANT=2", "WF_ATTN_VARIANT=3",
+                                 "WF_ATTN_VARIANT=4", "WF_ATTN_VARIANT=5",
+                                 "WF_ATTN_VARIANT8=2", "WF_ATTN_VARIANT8=3", "WF_ATTN_VARIANT8=4",
+                                 "WF_ATTN_VARIANT8=5"])
+def test_batched_attention_schedule_variants(env):
+    """The batched decode attention's other schedules (WF_ATTN_VARIANT 1-5 for bf16 K/V:
+    round-robin tiles, double-buffered tiles, per-wave records, both, wave-pair records;
+    WF_ATTN_VARIANT8 2-5 for FP8 K/V) pass the batched decode parity tests of the default one
+    (rows vs batch-1 runs, ragged long contexts, paged == dense, FP8 quality). Child process: the
+    choice is read once per process."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    tests = (["test_fp8_kv_codes_and_decode_quality"] if "VARIANT8" in env else
+             ["test_decode_batched_mfma_rows_match_single", "test_decode_batched_long_ragged_context_matches_single",
+              "test_decode_paged_kv_equals_dense"])
+    env_d = dict(os.environ)
+    env_d.update(kv.split("=") for kv in env.split())
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
+                        str(root / "tests" / "test_gpu_parity.py"), "-k", " or ".join(tests)],
+                       env=env_d, cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert f"{len(tests)} passed" in r.stdout, r.stdout[-2000:]
