@@ -326,8 +326,15 @@ __device__ __forceinline__ int64_t bf_tile_off(int r, int p, int H) {
     return ((((int64_t)(r >> 4) * (H >> 5) + (p >> 2)) << 6) + (r & 15) + 16 * (p & 3)) << 3;
 }
 
-constexpr int kAttnPartSplits = 8;    // records per (sequence, query head): batched decode (B >= 16)
-constexpr int kAttnPartSplits1 = 8;   // batch < 16 (16 measured: attention 5.70 -> 5.63 us, O input 6.01 -> 7.27 us)
+// (WF_SPLITS / WF_SPLITS1: study builds only, tools/build_variant.sh; the library uses the defaults)
+#ifndef WF_SPLITS
+#define WF_SPLITS 8
+#endif
+#ifndef WF_SPLITS1
+#define WF_SPLITS1 8
+#endif
+constexpr int kAttnPartSplits = WF_SPLITS;    // records per (sequence, query head): batched decode (B >= 16)
+constexpr int kAttnPartSplits1 = WF_SPLITS1;  // batch < 16 (16 measured: attention 5.70 -> 5.63 us, O input 6.01 -> 7.27 us)
 constexpr int kAttnPartSplitsMax = 16;
 // Float offset of element d of split s's unnormalised o in the decode-attention partials of (b, h)
 // (bh = b * Hq + h; head_dim 128): [bh][split][half = (d >> 2) & 1][d >> 3][4]. The merging reader
