@@ -853,7 +853,9 @@ def test_prefill_gemm_and_epilogue_switches(env):
                                  "WF_ATTN_VARIANT8=5"])
 def test_batched_attention_schedule_variants(env):
     """The batched decode attention's other schedules (WF_ATTN_VARIANT 1-5 for bf16 K/V:
-    round-robin tiles, double-buffered tiles, per-wave records, both, wave-pair records;
+    round-robin tiles, single-buffered tiles at 4 waves per SIMD (the default at 8 splits; the
+    default is double-buffered since the split count became 4), per-wave records, double-buffered
+    per-wave records, wave-pair records;
     WF_ATTN_VARIANT8 2-5 for FP8 K/V) pass the batched decode parity tests of the default one
     (rows vs batch-1 runs, ragged long contexts, paged == dense, FP8 quality). Child process: the
     choice is read once per process."""

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Batched decode attention at 4 splits (the default after tools/ab_splits2.sh): schedule variants
+# (WF_ATTN_VARIANT 1 = round-robin tiles, 2 = double-buffered, 2 waves per SIMD) and FP8 (WF_ATTN_VARIANT8).
+set -u
+mkdir -p gpurun_out/ab
+for V in 0 1 2; do
+  echo "== b128 fixed V=$V";   WF_ATTN_VARIANT=$V bash tools/ab_bench.sh --batch 128 --steps 50 --warmup 5 || exit 1
+  echo "== b128 uniform V=$V"; WF_ATTN_VARIANT=$V bash tools/ab_bench.sh --batch 128 --steps 50 --warmup 5 --ctx-dist uniform --paged || exit 1
+done
+for V in 0 2; do
+  echo "== fp8 fixed V8=$V";   WF_ATTN_VARIANT8=$V bash tools/ab_bench.sh --batch 128 --steps 50 --warmup 5 --kv fp8 || exit 1
+  echo "== fp8 uniform V8=$V"; WF_ATTN_VARIANT8=$V bash tools/ab_bench.sh --batch 128 --steps 50 --warmup 5 --kv fp8 --ctx-dist uniform --paged || exit 1
+done

@@ -1594,12 +1594,12 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
         else if (variant == 1)
             hipLaunchKernelGGL((k_attn_mfma<false, true>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv,
                                S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs, 1.0f);
-        else if (variant == 2)
-            hipLaunchKernelGGL((k_attn_mfma<true, false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv,
-                               S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs, 1.0f);
-        else
+        else if (variant == 2)  // one tile in flight per wave, 4 waves per SIMD (the default at 8 splits)
             hipLaunchKernelGGL((k_attn_mfma<false, false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq,
                                Hkv, S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs, 1.0f);
+        else  // default: double-buffered tiles, 2 waves per SIMD (at 4 splits a wave takes >= 2 tiles at ctx >= 1024)
+            hipLaunchKernelGGL((k_attn_mfma<true, false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv,
+                               S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs, 1.0f);
         return check_launch("decode_attention_partials");
     }
 #define WF_AP(GV)                                                                                                   \

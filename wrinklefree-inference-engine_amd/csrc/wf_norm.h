@@ -328,7 +328,7 @@ __device__ __forceinline__ int64_t bf_tile_off(int r, int p, int H) {
 
 // (WF_SPLITS / WF_SPLITS1: study builds only, tools/build_variant.sh; the library uses the defaults)
 #ifndef WF_SPLITS
-#define WF_SPLITS 8
+#define WF_SPLITS 4
 #endif
 #ifndef WF_SPLITS1
 #define WF_SPLITS1 8
