@@ -1076,7 +1076,10 @@ __global__ void k_bf_tile(const uint16_t* __restrict__ src, int R, int H, uint16
 // Per (row, block) the (max, first index) of the block's 256 logits goes to `part`.
 typedef short v8s_t __attribute__((ext_vector_type(8)));
 typedef float v4f_t __attribute__((ext_vector_type(4)));
-constexpr int kLmStages = 4;
+#ifndef WF_LM_STAGES  // study builds only (tools/build_variant.sh)
+#define WF_LM_STAGES 4
+#endif
+constexpr int kLmStages = WF_LM_STAGES;
 constexpr int kLmStageBytes = 8 * 1024 + 4 * 4096;
 __global__ __launch_bounds__(256) void k_lm_head_mfma(const uint16_t* __restrict__ E, const uint16_t* __restrict__ hn,
                                                       int H, int V, int B, uint16_t* __restrict__ logits,
