@@ -4,7 +4,7 @@ set -u
 mkdir -p gpurun_out/ab
 L=$(pwd)/wrinklefree-inference-engine_amd/lib
 for v in lm3 lm2 s2; do
-  WF_BITNET_LIB=$L/libwfbitnet_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -k "batched or paged" -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/ab/t_$v.log 2>&1 || { tail -30 gpurun_out/ab/t_$v.log; exit 1; }
+  WF_BITNET_LIB=$L/libwfbitnet_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -k "(batched or paged) and not schedule_variants" -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/ab/t_$v.log 2>&1 || { tail -30 gpurun_out/ab/t_$v.log; exit 1; }
   echo "$v tests: $(tail -1 gpurun_out/ab/t_$v.log)"
 done
 echo "== b128 fixed"
