@@ -327,7 +327,11 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
 // fixed number of records, so it needs no sequence length and issues every load before its
 // weight stream.
 // ---------------------------------------------------------------------------------------------
-constexpr int kAttnPartThreads = 256;
+#ifndef WF_AP_THREADS  // study builds only (tools/build_variant.sh): threads per block, keys per lane group and chunk
+#define WF_AP_THREADS 256
+#define WF_AP_U 8
+#endif
+constexpr int kAttnPartThreads = WF_AP_THREADS;
 template <int G, int NS = kAttnPartSplits1>
 __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* __restrict__ q, int64_t q_sb,
                                                                 const uint16_t* __restrict__ K,
@@ -335,7 +339,7 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
                                                                 int64_t kv_sh, int Hq, int Hkv, int S,
                                                                 const int32_t* __restrict__ seq_lens, float sm_scale,
                                                                 float2* __restrict__ ml_out, float* __restrict__ o_out) {
-    constexpr int D = 128, LP = D / 8, NG = kAttnPartThreads / LP, U = 8, CH = U * NG;  // 128 keys per chunk
+    constexpr int D = 128, LP = D / 8, NG = kAttnPartThreads / LP, U = WF_AP_U, CH = U * NG;  // 128 keys per chunk
     // block (s, y, b): query heads hq0 .. hq0 + G - 1 (G = whole GQA group, or 1: one block per query
     // head, 4x the blocks for a group of 4 -- the K/V re-reads hit the caches)
     const int s = blockIdx.x, b = blockIdx.z;
