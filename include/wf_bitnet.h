@@ -219,6 +219,21 @@ enum {
     WF_OP_LM_HEAD = 6     /* tied bf16 LM head + greedy argmax + position advance (layer ignored) */
 };
 int wf_model_launch_op(wf_model* m, int layer, int op, void* stream);
+/* Read-only view of the step's attention hand-off, for kernel-level checks (tests/, profiling):
+ * after WF_OP_QKV and WF_OP_ATTN of a layer, q holds that layer's query rows after RoPE
+ * ([batch, n_heads * head_dim] bf16) and the partial records of the split-K attention: per
+ * (sequence b, query head h, record s < records), part_ml[2 ((b n_heads + h) records + s) + {0, 1}] =
+ * (running max m, sum l) and the unnormalised output o[d] at part_o[((b n_heads + h) records + s) *
+ * 128 + ((d >> 2) & 1) * 64 + (d >> 3) * 4 + (d & 3)] (head_dim 128); the attention output is
+ * sum_s e^(m_s - M) o_s / sum_s e^(m_s - M) l_s, M = max_s m_s (records with l = 0 are empty).
+ * Device pointers owned by the model; valid until wf_model_destroy. */
+typedef struct {
+    const uint16_t* q;
+    const float* part_ml;
+    const float* part_o;
+    int records;
+} wf_model_attn_view;
+int wf_model_attn_view(const wf_model* m, wf_model_attn_view* out);
 /* Prefill (BASELINE configs[2]; the prompt pass that precedes scripts/direct_inference_full.py's
  * decode loop): run prompt tokens of any KV slots through all layers as GEMM rows and write their
  * K/V into the cache (dense planes or pages). Batched matrix-core decoders only (batch >= 16, I2_S

@@ -56,6 +56,7 @@ def _load(path: Path):
         "orc_gemv_lsb_signed": [vp, vp, f32, i32, i32, vp], "orc_enc_sums_i2s": [vp, vp, i32, i32, i32, vp],
         "orc_bitnet_linear_bf16": [vp, vp, f32, i32, i32, vp],
         "orc_attention_gqa_bf16": [vp, vp, vp, i32, i32, i32, i32, i32, f32, vp],
+        "orc_attention_gqa_f32": [vp, vp, vp, i32, i32, i32, i32, i32, f32, vp],
         "orc_decode_step": [vp, i32, i32, vp, vp],
         "orc_msb_ternarize": [vp, i32, i32, i32, f32, vp], "orc_msb_dequant": [vp, i32, i32, f32, vp],
         "orc_msb_linear": [vp, f32, vp, vp, i32, i32, i32, i32, vp],
@@ -66,6 +67,10 @@ def _load(path: Path):
         fn.restype = C.c_int
     L.orc_tq_row_bytes.argtypes = [i32]
     L.orc_tq_row_bytes.restype = i64
+    L.orc_f32_to_e4m3.argtypes = [f32]
+    L.orc_f32_to_e4m3.restype = C.c_uint8
+    L.orc_e4m3_to_f32.argtypes = [C.c_uint8]
+    L.orc_e4m3_to_f32.restype = f32
     L.orc_num_threads.argtypes = []
     L.orc_num_threads.restype = C.c_int
     return L
@@ -213,19 +218,44 @@ def attention_gqa_bf16(q_bits, k_bits, v_bits, s: int, scale: float | None = Non
     return out
 
 
+def attention_gqa_f32(q_bits, k_bits, v_bits, s: int, scale: float | None = None) -> np.ndarray:
+    """attention_gqa_bf16 with the double result rounded to float32 (kernel-level attention check)."""
+    q_bits = np.ascontiguousarray(q_bits, dtype=np.uint16)
+    k_bits = np.ascontiguousarray(k_bits, dtype=np.uint16)
+    v_bits = np.ascontiguousarray(v_bits, dtype=np.uint16)
+    hq, d = q_bits.shape
+    hkv, smax, _ = k_bits.shape
+    out = np.zeros((hq, d), np.float32)
+    sc = float(scale) if scale is not None else 1.0 / float(np.sqrt(np.float32(d)))
+    _ck(lib().orc_attention_gqa_f32(_p(q_bits), _p(k_bits), _p(v_bits), hq, hkv, d, smax, s, sc, _p(out)), "attn32")
+    return out
+
+
+def e4m3_decode_table() -> np.ndarray:
+    """float32 value of every OCP e4m3fn code (the oracle's decoder)."""
+    return np.array([lib().orc_e4m3_to_f32(c) for c in range(256)], dtype=np.float32)
+
+
+def fp8_codes_to_bf16(codes: np.ndarray, scale: float) -> np.ndarray:
+    """bf16 bits of e4m3 code * scale (what the oracle's FP8 K/V rows hold)."""
+    v = e4m3_decode_table()[np.asarray(codes, dtype=np.uint8)] * np.float32(scale)
+    return f32_to_bf16(v.astype(np.float32))
+
+
 class _Model(C.Structure):
     _fields_ = [(n, C.c_int) for n in ("hidden", "layers", "n_heads", "n_kv_heads", "head_dim", "inter", "vocab",
                                         "max_seq")] + [("eps", C.c_float)] + \
                [(n, C.c_void_p) for n in ("embed", "final_norm", "rope_cos", "rope_sin", "ln_in", "ln_post",
                                           "attn_sub", "ffn_sub", "wq", "wk", "wv", "wo", "wg", "wu", "wd", "wscale",
-                                          "k_cache", "v_cache")]
+                                          "k_cache", "v_cache")] + \
+               [("kv_fp8", C.c_int), ("kv_scale", C.c_void_p)]
 
 
 class DecodeModel:
     """Holds a model's host arrays (dict of numpy arrays in the tests/golden/decode.npz layout) for
     orc_decode_step. K/V caches are [layers, n_kv_heads, max_seq, head_dim] bf16 bits."""
 
-    def __init__(self, arrays: dict, libname: str = "liborc.so"):
+    def __init__(self, arrays: dict, libname: str = "liborc.so", kv_fp8: bool = False, kv_scale=None):
         H, L, HQ, HKV, D, I, V, S = (int(x) for x in arrays["cfg"])
         self.cfg = (H, L, HQ, HKV, D, I, V, S)
         self.a = {k: np.ascontiguousarray(v) for k, v in arrays.items()}
@@ -239,14 +269,18 @@ class DecodeModel:
                   "wq", "wk", "wv", "wo", "wg", "wu", "wd", "wscale"):
             setattr(m, n, _p(self.a[n]))
         m.k_cache, m.v_cache = _p(self.k_cache), _p(self.v_cache)
+        self.kv_scale = np.ones((L, 2), np.float32) if kv_scale is None else np.ascontiguousarray(
+            np.broadcast_to(np.asarray(kv_scale, dtype=np.float32), (L, 2)))
+        m.kv_fp8, m.kv_scale = int(kv_fp8), _p(self.kv_scale)
         self.m = m
 
-    def step(self, token: int, pos: int):
-        logits = np.zeros(self.cfg[6], np.uint16)
+    def step(self, token: int, pos: int, logits: bool = True):
+        """One token; logits=False appends the K/V rows only (no LM head) and returns (None, -1)."""
+        out = np.zeros(self.cfg[6], np.uint16) if logits else None
         nxt = C.c_int()
-        _ck(self._lib.orc_decode_step(C.addressof(self.m), int(token), int(pos), _p(logits), C.addressof(nxt)),
-            "decode_step")
-        return logits, nxt.value
+        _ck(self._lib.orc_decode_step(C.addressof(self.m), int(token), int(pos), _p(out) if logits else None,
+                                      C.addressof(nxt)), "decode_step")
+        return out, nxt.value
 
 
 def num_threads(libname: str = "liborc.so") -> int:

@@ -1,0 +1,363 @@
+"""Oracle parity at the BASELINE configurations' real shapes (VERDICT r02 "Next round" item 1).
+
+The decode step, the step's own attention kernels and the prefill are compared with the CPU
+oracle (oracle/wf_oracle.c: orc_decode_step, orc_attention_gqa_f32), not with each other, at the
+bitnet-b1.58-2B-4T geometry (scripts/direct_inference_full.py:84-89: hidden 2560, intermediate
+6912, 20 / 5 heads x 128, vocab 128256) with 1-2 full-width layers of random-init weights:
+
+  (a) batch 1 (BASELINE configs[1]) at contexts 1024 and 4096, 4 graph-replayed steps each;
+  (b) batch 128 on paged KV with contexts U[1, 4096) (configs[3]), bf16 and FP8 K/V, 8 rows;
+  (c) the step's attention partials (k_attn_part, k_attn_mfma bf16 / FP8, the untiled batched
+      fallback) at S in {1, 31, 32, 33, 1024, 4096}, merged from the records the O projection reads;
+  (d) prefill of 8 x 2048 tokens (configs[2]) against the oracle's teacher-forced decode.
+
+Tolerances (north_star: "within 1e-3 rel on bf16 activations"): logits and appended K/V rows
+rel-L2 <= 1e-3; attention outputs (fp32, before the consumer's bf16 rounding) rel-L2 <= 2e-4 per
+head. The q / k projection scales are 0.05 where a test says "trained-like": with the random-init
+scales (1.5-2) attention scores are ~+-70 and the softmax is one-hot, so a long context would test
+nothing but an argmax.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+FULL = dict(hidden=2560, n_heads=20, n_kv_heads=5, head_dim=128, inter=6912)
+ATTN_S = [1, 31, 32, 33, 1024, 4096]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from wfamd import _lib
+    assert _lib.kernel_available(), "gfx950 kernels must load on the GPU box (no fallback)"
+    torch.cuda.set_device(0)
+
+
+def bits(t: torch.Tensor) -> np.ndarray:
+    return t.contiguous().view(torch.int16).cpu().numpy().view(np.uint16)
+
+
+def rel_l2(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def make_cfg(layers, vocab, max_seq):
+    from wfamd.model import BitNetConfig
+    return BitNetConfig(layers=layers, vocab=vocab, max_seq=max_seq, **FULL)
+
+
+def make_weights(cfg, seed, trained_like):
+    from wfamd.model import synthetic_weights
+    w = synthetic_weights(cfg, seed=seed, device="cuda")
+    if trained_like:
+        w["wscale"][:, :2] = 0.05
+    return w
+
+
+def oracle_arrays(cfg, w) -> dict:
+    """The decoder's weights in the oracle's layout (tests/golden/decode.npz keys)."""
+    from wfamd.model import rope_tables
+    cos, sin = rope_tables(cfg.head_dim, cfg.max_seq, cfg.rope_theta)
+    a = {"cfg": np.array([cfg.hidden, cfg.layers, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, cfg.inter, cfg.vocab,
+                          cfg.max_seq], dtype=np.int64),
+         "eps": np.float32(cfg.eps), "rope_cos": bits(cos), "rope_sin": bits(sin),
+         "wscale": w["wscale"].detach().cpu().numpy().astype(np.float32)}
+    for n in ("wq", "wk", "wv", "wo", "wg", "wu", "wd"):
+        a[n] = w[n].cpu().numpy()
+    for n in ("embed", "final_norm", "ln_in", "ln_post", "attn_sub", "ffn_sub"):
+        a[n] = bits(w[n])
+    return a
+
+
+def logical_kv(dec, layer, b, n):
+    """Logical K / V [Hkv, n, D] of sequence b (dense, tile-layout or paged storage); uint8 codes for
+    FP8 caches, bf16 otherwise."""
+    from wfamd.model import from_kv_tiles
+    H, D = dec.cfg.n_kv_heads, dec.cfg.head_dim
+    if dec.paged:
+        nblk = (n + 31) // 32
+        ids = torch.from_numpy(dec.seq_pages[b][:nblk].astype(np.int64)).cuda()
+        kt = dec.k_cache[layer].index_select(0, ids).transpose(0, 1).reshape(H, nblk * 32, D)
+        vt = dec.v_cache[layer].index_select(0, ids).transpose(0, 1).reshape(H, nblk * 32, D)
+        k, v = from_kv_tiles(kt, vt)
+    elif dec.kv_tiled:
+        k, v = from_kv_tiles(dec.k_cache[layer, b], dec.v_cache[layer, b])
+    else:
+        k, v = dec.k_cache[layer, b], dec.v_cache[layer, b]
+    return k[:, :n], v[:, :n]
+
+
+def kv_bits(dec, t: torch.Tensor, layer: int, which: int) -> np.ndarray:
+    """bf16 bits of stored K (which=0) / V (1) rows: FP8 codes dequantised with the layer's scale."""
+    from oracle import oracle as orc
+    if dec.kv_fp8:
+        return orc.fp8_codes_to_bf16(t.cpu().numpy(), float(dec.kv_scale[layer, which]))
+    return bits(t)
+
+
+def merge_records(ml: torch.Tensor, o: torch.Tensor) -> np.ndarray:
+    """The attention output the O projection's input stage forms from the partial records:
+    sum_s e^(m_s - M) o_s / sum_s e^(m_s - M) l_s (float64 here)."""
+    ml = ml.double().cpu().numpy()
+    o = o.double().cpu().numpy()
+    m, l = ml[..., 0], ml[..., 1]
+    M = np.max(np.where(l > 0, m, -np.inf), axis=-1, keepdims=True)
+    wgt = np.where(l > 0, np.exp(np.where(l > 0, m, 0.0) - M), 0.0)
+    return (wgt[..., None] * o).sum(-2) / (wgt * l).sum(-1)[..., None]
+
+
+# ------------------------------------------------------------------------------------------------
+# (a) batch 1, full width, contexts 1024 / 4096 (BASELINE configs[1])
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("ctx,trained", [(1024, False), (1024, True), (4096, True)])
+def test_decode_batch1_full_width_vs_oracle(orc, ctx, trained):
+    """4 graph-replayed decode steps after a `ctx`-key random history (same history in the oracle's
+    cache), teacher-forced by the oracle's greedy tokens: bf16 logits and the K/V rows each step
+    appends (both layers) within 1e-3 rel-L2 of orc_decode_step; greedy token equal where the top-2
+    gap is clear (scripts/direct_inference_full.py:267-302)."""
+    from wfamd.model import BitNetDecoder
+    cfg = make_cfg(2, 128256, 4128)
+    w = make_weights(cfg, seed=1, trained_like=trained)
+    dec = BitNetDecoder(cfg, w, batch=1)
+    m = orc.DecodeModel(oracle_arrays(cfg, w))
+    del w
+    gen = torch.Generator(device="cuda").manual_seed(ctx)
+    for l in range(cfg.layers):
+        k = torch.randn(1, cfg.n_kv_heads, ctx, cfg.head_dim, generator=gen, device="cuda").to(torch.bfloat16)
+        v = torch.randn(1, cfg.n_kv_heads, ctx, cfg.head_dim, generator=gen, device="cuda").to(torch.bfloat16)
+        dec.load_kv(l, k, v)
+        m.k_cache[l, :, :ctx] = bits(k[0])
+        m.v_cache[l, :, :ctx] = bits(v[0])
+    tok = 4242
+    worst = 0.0
+    for i in range(4):
+        pos = ctx + i
+        dec.set_state([tok], [pos])
+        dec.step(graph=True)
+        torch.cuda.synchronize()
+        ologits, onext = m.step(tok, pos)
+        got, ref = orc.bf16_to_f32(bits(dec.logits[0])), orc.bf16_to_f32(ologits)
+        err = rel_l2(got, ref)
+        worst = max(worst, err)
+        assert err < 1e-3, (i, err)
+        top2 = np.sort(ref)[-2:]
+        if top2[1] - top2[0] > 1e-2 * abs(top2[1]):
+            assert int(dec.tokens[0]) == onext, i
+        assert int(dec.positions[0]) == pos + 1
+        for l in range(cfg.layers):
+            kg, vg = logical_kv(dec, l, 0, pos + 1)
+            for got_t, ref_c in ((kg[:, pos], m.k_cache[l, :, pos]), (vg[:, pos], m.v_cache[l, :, pos])):
+                e = rel_l2(orc.bf16_to_f32(bits(got_t)), orc.bf16_to_f32(ref_c))
+                assert e < 1e-3, (i, l, e)
+        tok = onext
+    print(f"batch 1 ctx {ctx} trained={trained}: worst logits rel-L2 {worst:.2e}")
+
+
+# ------------------------------------------------------------------------------------------------
+# (b) batch 128, paged KV, contexts U[1, 4096) (BASELINE configs[3])
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("kv", ["bf16", "fp8"])
+def test_decode_batch128_paged_full_width_vs_oracle(orc, kv):
+    """The batched matrix-core step (int8 MFMA GEMMs, MFMA attention on paged tile-layout K/V, MFMA
+    LM head) at batch 128 with contexts drawn from U[1, 4096) (seed 0): 3 steps,
+    8 sampled rows (shortest, longest, and 6 more) each against its own orc_decode_step with the
+    same history. FP8: the oracle stores every appended row through the same e4m3 rounding
+    (orc_model.kv_fp8, power-of-two scales so the dequantised values are exact bf16)."""
+    from wfamd.model import BitNetDecoder
+    cfg = make_cfg(2, 128256, 4128)
+    w = make_weights(cfg, seed=2, trained_like=True)
+    B, steps = 128, 3
+    ctxs = np.random.default_rng(0).integers(1, 4096, size=B)
+    fp8 = kv == "fp8"
+    scale = [(0.5, 0.25), (1.0, 0.5)]
+    pages = int(sum((c + steps + 31) // 32 for c in ctxs))
+    dec = BitNetDecoder(cfg, w, batch=B, num_pages=pages, page_seed=0, kv_dtype=kv,
+                        kv_scale=scale if fp8 else None)
+    a = oracle_arrays(cfg, w)
+    del w
+    rows = sorted({int(np.argmin(ctxs)), int(np.argmax(ctxs)), 0, 1, 17, 64, 100, 127})
+    gen = torch.Generator(device="cuda").manual_seed(77)
+    cmax = int(ctxs.max())
+    models = {b: orc.DecodeModel(a, kv_fp8=fp8, kv_scale=scale if fp8 else None) for b in rows}
+    for l in range(cfg.layers):
+        k = torch.randn(B, cfg.n_kv_heads, cmax, cfg.head_dim, generator=gen, device="cuda").to(torch.bfloat16)
+        v = torch.randn(B, cfg.n_kv_heads, cmax, cfg.head_dim, generator=gen, device="cuda").to(torch.bfloat16)
+        dec.load_kv(l, k, v, lengths=ctxs)
+        for b in rows:
+            c = int(ctxs[b])
+            kb, vb = logical_kv(dec, l, b, c)
+            models[b].k_cache[l, :, :c] = kv_bits(dec, kb, l, 0)
+            models[b].v_cache[l, :, :c] = kv_bits(dec, vb, l, 1)
+        del k, v
+    for b in range(B):
+        dec.reserve(b, int(ctxs[b]) + steps + 1)
+    dec.set_state([(97 * b + 11) % cfg.vocab for b in range(B)], [int(c) for c in ctxs])
+    worst = 0.0
+    for i in range(steps):
+        toks = dec.tokens.cpu().numpy().copy()
+        dec.step(graph=True)
+        torch.cuda.synchronize()
+        for b in rows:
+            pos = int(ctxs[b]) + i
+            ologits, onext = models[b].step(int(toks[b]), pos)
+            got, ref = orc.bf16_to_f32(bits(dec.logits[b])), orc.bf16_to_f32(ologits)
+            err = rel_l2(got, ref)
+            worst = max(worst, err)
+            assert err < 1e-3, (kv, i, b, pos, err)
+            top2 = np.sort(ref)[-2:]
+            if top2[1] - top2[0] > 1e-2 * abs(top2[1]):
+                assert int(dec.tokens[b]) == onext, (i, b)
+            for l in range(cfg.layers):
+                kg, vg = logical_kv(dec, l, b, pos + 1)
+                ek = rel_l2(orc.bf16_to_f32(kv_bits(dec, kg[:, pos], l, 0)), orc.bf16_to_f32(models[b].k_cache[l, :, pos]))
+                ev = rel_l2(orc.bf16_to_f32(kv_bits(dec, vg[:, pos], l, 1)), orc.bf16_to_f32(models[b].v_cache[l, :, pos]))
+                assert ek < 1e-3 and ev < 1e-3, (kv, i, b, l, ek, ev)
+    print(f"batch 128 paged {kv}: worst logits rel-L2 {worst:.2e} over rows {rows}")
+
+
+# ------------------------------------------------------------------------------------------------
+# (c) the step's own attention kernels, long and edge contexts
+# ------------------------------------------------------------------------------------------------
+def _attn_case(variant):
+    """(decoder kwargs, batch, max_seq) of each attention code path of the decode step."""
+    from wfamd._lib import WF_FMT_TQ
+    return {
+        "b1": (dict(), 1, 4096),                                     # k_attn_part<1, 8>
+        "b128_paged_bf16": (dict(kv_dtype="bf16"), 128, 4096),       # k_attn_mfma (double-buffered), pages
+        "b128_paged_fp8": (dict(kv_dtype="fp8", kv_scale=(0.5, 0.25)), 128, 4096),  # k_attn_mfma FP8
+        "b16_dense_tiled": (dict(), 16, 4096),                       # k_attn_mfma on dense tile planes
+        "b16_tq_untiled": (dict(wfmt=WF_FMT_TQ), 16, 4096),         # k_attn_part<4, 4> (untiled fallback)
+        "b16_seq4100_untiled": (dict(), 16, 4100),                   # max_seq % 32 != 0: untiled fallback
+    }[variant]
+
+
+@pytest.mark.parametrize("variant", ["b1", "b128_paged_bf16", "b128_paged_fp8", "b16_dense_tiled",
+                                     "b16_tq_untiled", "b16_seq4100_untiled"])
+def test_step_attention_kernels_vs_oracle(orc, variant):
+    """WF_OP_QKV then WF_OP_ATTN of layer 0 on a full-geometry model (20 / 5 heads x 128), every
+    row at its own context S (the list ATTN_S, then random lengths): the attention output merged
+    from the partial records (include/wf_bitnet.h wf_model_attn_view: exactly what the O
+    projection's input stage reads) against orc_attention_gqa_f32 on the step's own q and the K/V
+    the cache holds (the row the QKV epilogue appended included), rel-L2 <= 2e-4 per (row, head)."""
+    from wfamd import _lib
+    from wfamd.model import BitNetDecoder
+    kw, B, smax = _attn_case(variant)
+    cfg = make_cfg(1, 1024, smax)
+    w = make_weights(cfg, seed=3, trained_like=True)
+    rng = np.random.default_rng(5)
+    S = np.array([ATTN_S[b] if b < len(ATTN_S) else int(rng.integers(1, 4097)) for b in range(B)])
+    if B == 1:
+        cases = [np.array([s]) for s in ATTN_S]
+    else:
+        cases = [S]
+    worst = 0.0
+    for S in cases:
+        paged = variant.startswith("b128")
+        pages = int(sum((s + 31) // 32 for s in S)) if paged else 0
+        dec = BitNetDecoder(cfg, w, batch=len(S), num_pages=pages, page_seed=1 if paged else None, **kw)
+        gen = torch.Generator(device="cuda").manual_seed(int(S.sum()))
+        hist = int(S.max()) - 1
+        if hist > 0:
+            k = torch.randn(len(S), cfg.n_kv_heads, hist, 128, generator=gen, device="cuda").to(torch.bfloat16)
+            v = torch.randn(len(S), cfg.n_kv_heads, hist, 128, generator=gen, device="cuda").to(torch.bfloat16)
+            dec.load_kv(0, k, v, lengths=S - 1)
+            del k, v
+        if paged:
+            for b in range(len(S)):
+                dec.reserve(b, int(S[b]))
+        dec.set_state([(31 * b + 3) % cfg.vocab for b in range(len(S))], [int(s) - 1 for s in S])
+        for op in (_lib.WF_OP_EMBED, _lib.WF_OP_QKV, _lib.WF_OP_ATTN):
+            dec.launch_op(0, op)
+        torch.cuda.synchronize()
+        q, ml, o = dec.attention_records()
+        got = merge_records(ml, o)
+        check = range(len(S)) if len(S) <= 16 else list(range(12)) + [40, 77, 100, 127]
+        for b in check:
+            s = int(S[b])
+            kb, vb = logical_kv(dec, 0, b, s)
+            ref = orc.attention_gqa_f32(bits(q[b]), kv_bits(dec, kb, 0, 0), kv_bits(dec, vb, 0, 1), s)
+            for h in range(cfg.n_heads):
+                e = rel_l2(got[b, h], ref[h])
+                worst = max(worst, e)
+                assert e < 2e-4, (variant, b, s, h, e)
+        del dec
+    print(f"attention {variant}: worst rel-L2 {worst:.2e}")
+
+
+@pytest.mark.parametrize("ctx", [1024, 4096])
+def test_fp8_kv_attention_cosine_reference_bar(orc, ctx):
+    """The reference's quantized-KV quality bar (docs/research/notebook.md:690-700,
+    legacy/benchmark/kv_cache_bench.py:208-315: cosine of one attention output vs BF16 K/V, min >=
+    0.998) on the step's own kernels: the same q and the same history (FP8 = e4m3 codes of the bf16
+    values, scale 1) through k_attn_mfma bf16 and FP8, every (sequence, head) of a 16-sequence batch
+    at context `ctx`."""
+    from wfamd import _lib
+    from wfamd.model import BitNetDecoder
+    cfg = make_cfg(1, 1024, 4096)
+    w = make_weights(cfg, seed=4, trained_like=True)
+    B = 16
+    gen = torch.Generator(device="cuda").manual_seed(ctx)
+    k = torch.randn(B, cfg.n_kv_heads, ctx - 1, 128, generator=gen, device="cuda").to(torch.bfloat16)
+    v = torch.randn(B, cfg.n_kv_heads, ctx - 1, 128, generator=gen, device="cuda").to(torch.bfloat16)
+    outs = []
+    for kvd in ("bf16", "fp8"):
+        dec = BitNetDecoder(cfg, w, batch=B, kv_dtype=kvd)
+        dec.load_kv(0, k, v)
+        dec.set_state([(13 * b + 1) % cfg.vocab for b in range(B)], [ctx - 1] * B)
+        for op in (_lib.WF_OP_EMBED, _lib.WF_OP_QKV, _lib.WF_OP_ATTN):
+            dec.launch_op(0, op)
+        torch.cuda.synchronize()
+        outs.append(merge_records(*dec.attention_records()[1:]))
+        del dec
+    a, b = outs[0].reshape(-1, 128), outs[1].reshape(-1, 128)
+    cos = (a * b).sum(-1) / np.linalg.norm(a, axis=-1) / np.linalg.norm(b, axis=-1)
+    print(f"FP8 K/V ctx {ctx}: attention-output cosine vs bf16 min {cos.min():.5f} mean {cos.mean():.5f}")
+    assert cos.min() >= 0.998, (cos.min(), cos.mean())
+
+
+# ------------------------------------------------------------------------------------------------
+# (d) prefill 8 x 2048 (BASELINE configs[2])
+# ------------------------------------------------------------------------------------------------
+def test_prefill_8x2048_full_width_vs_oracle(orc):
+    """wf_model_prefill of 8 sequences x 2048 tokens (16384 GEMM rows: the 128 x 512 gate|up tiles
+    and every full-size prefill kernel) through 2 full-width layers, then one decode step per
+    sequence, against the oracle's teacher-forced decode of the same tokens
+    (orc_decode_step over every prompt position): the K/V rows of all 2048 positions of sequence 0
+    and the first 512 of sequence 5, both layers, rel-L2 <= 1e-3 per 256-position chunk; the
+    next-step logits of sequence 0 rel-L2 <= 1e-3."""
+    from wfamd.model import BitNetDecoder
+    cfg = make_cfg(2, 128256, 2080)
+    w = make_weights(cfg, seed=6, trained_like=True)
+    B, n = 16, 2048
+    dec = BitNetDecoder(cfg, w, batch=B)
+    a = oracle_arrays(cfg, w)
+    del w
+    rng = np.random.default_rng(12)
+    prompts = [rng.integers(0, cfg.vocab, size=n + 1).tolist() for _ in range(8)]
+    dec.prefill([(b, prompts[b][:n], 0) for b in range(8)], chunk_rows=16384)
+    for b in range(8):
+        dec.tokens[b] = prompts[b][n]
+        dec.positions[b] = n
+    dec.step(graph=False)
+    torch.cuda.synchronize()
+    for b, npos in ((0, n), (5, 512)):
+        m = orc.DecodeModel(a)
+        for t in range(npos):
+            m.step(prompts[b][t], t, logits=False)
+        for l in range(cfg.layers):
+            kg, vg = logical_kv(dec, l, b, npos)
+            kg, vg = orc.bf16_to_f32(bits(kg)), orc.bf16_to_f32(bits(vg))
+            kr, vr = orc.bf16_to_f32(m.k_cache[l, :, :npos]), orc.bf16_to_f32(m.v_cache[l, :, :npos])
+            for c0 in range(0, npos, 256):
+                ek = rel_l2(kg[:, c0:c0 + 256], kr[:, c0:c0 + 256])
+                ev = rel_l2(vg[:, c0:c0 + 256], vr[:, c0:c0 + 256])
+                assert ek < 1e-3 and ev < 1e-3, (b, l, c0, ek, ev)
+        if b == 0:
+            ologits, onext = m.step(prompts[0][n], n)
+            err = rel_l2(orc.bf16_to_f32(bits(dec.logits[0])), orc.bf16_to_f32(ologits))
+            assert err < 1e-3, err
+            print(f"prefill 8 x 2048: next-step logits rel-L2 {err:.2e}")

@@ -793,84 +793,3 @@ def test_mfma_tile_format_roundtrip_and_gemv(orc):
             off = 32 * kb + 16 * h + 4 * (lane >> 4)
             assert mfn[t] == p[row, off:off + 4].view(np.uint32)[0]
         assert np.array_equal(ops.mfma_to_i2s(mf).cpu().numpy(), p)
-
-
-@pytest.mark.parametrize("variant", ["1", "2", "3"])
-def test_prefill_attention_study_variants(variant):
-    """The other prefill attention kernels (WF_PF_ATTN=1: the row-split register kernel
-    k_attn_prefill, which the default keeps for FP8 K/V; 2: its LDS-staged variant, bf16 only; 3:
-    keys split over the block's waves, k_attn_prefill_ks, bf16 and FP8) pass the same prefill
-    parity tests as the default flash-style kernel. The choice is read once per process, so the
-    tests run in a child process with the variable set."""
-    import os
-    import subprocess
-    import sys
-    from pathlib import Path
-    root = Path(__file__).resolve().parents[1]
-    tests = ["test_prefill_matches_teacher_forced_decode", "test_prefill_in_pieces_equals_one_shot"]
-    if variant in ("1", "3"):
-        tests.append("test_fp8_kv_prefill")  # their FP8 instantiations
-    env = dict(os.environ, WF_PF_ATTN=variant)
-    sel = " or ".join(tests)
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
-                        str(root / "tests" / "test_gpu_parity.py"), "-k", sel],
-                       env=env, cwd=root, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    assert f"{len(tests)} passed" in r.stdout, r.stdout[-2000:]
-
-
-@pytest.mark.parametrize("env", [
-    "WF_PG_WIDE_MIN_N=512",                        # 512-column tiles for gate|up (and o / down: per fragment)
-    "WF_PG_WIDE_MIN_N=512 WF_PF_EPI=2",            # + the staged gate|up epilogue
-    "WF_PG_WIDE_MIN_N=512 WF_PG_ALG=3 WF_PG_ALG8=3",  # column-wave main loops everywhere
-    "WF_PF_EPI=0 WF_GU_QUAD=0 WF_PF_XCD=0",        # per-fragment epilogues, per-element act stores, plain order
-])
-def test_prefill_gemm_and_epilogue_switches(env):
-    """The prefill GEMM's non-default forms -- 128 x 512 tiles at the small test model's widths
-    (WF_PG_WIDE_MIN_N), the column-wave main loop, the staged / per-fragment epilogues, the
-    per-element gate|up stores and the plain attention block order -- pass the same prefill parity
-    tests as the defaults (bit-exact integer GEMM, K/V and logits against teacher-forced decode;
-    chunked = one shot). The switches are read once per process: child process."""
-    import os
-    import subprocess
-    import sys
-    from pathlib import Path
-    root = Path(__file__).resolve().parents[1]
-    tests = ["test_prefill_matches_teacher_forced_decode", "test_prefill_in_pieces_equals_one_shot",
-             "test_fp8_kv_prefill"]
-    env_d = dict(os.environ)
-    env_d.update(kv.split("=") for kv in env.split())
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
-                        str(root / "tests" / "test_gpu_parity.py"), "-k", " or ".join(tests)],
-                       env=env_d, cwd=root, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    assert f"{len(tests)} passed" in r.stdout, r.stdout[-2000:]
-
-
-@pytest.mark.parametrize("env", ["WF_ATTN_VARIANT=1", "WF_ATTN_VARIANT=2", "WF_ATTN_VARIANT=3",
-                                 "WF_ATTN_VARIANT=4", "WF_ATTN_VARIANT=5",
-                                 "WF_ATTN_VARIANT8=2", "WF_ATTN_VARIANT8=3", "WF_ATTN_VARIANT8=4",
-                                 "WF_ATTN_VARIANT8=5"])
-def test_batched_attention_schedule_variants(env):
-    """The batched decode attention's other schedules (WF_ATTN_VARIANT 1-5 for bf16 K/V:
-    round-robin tiles, single-buffered tiles at 4 waves per SIMD (the default at 8 splits; the
-    default is double-buffered since the split count became 4), per-wave records, double-buffered
-    per-wave records, wave-pair records;
-    WF_ATTN_VARIANT8 2-5 for FP8 K/V) pass the batched decode parity tests of the default one
-    (rows vs batch-1 runs, ragged long contexts, paged == dense, FP8 quality). Child process: the
-    choice is read once per process."""
-    import os
-    import subprocess
-    import sys
-    from pathlib import Path
-    root = Path(__file__).resolve().parents[1]
-    tests = (["test_fp8_kv_codes_and_decode_quality"] if "VARIANT8" in env else
-             ["test_decode_batched_mfma_rows_match_single", "test_decode_batched_long_ragged_context_matches_single",
-              "test_decode_paged_kv_equals_dense"])
-    env_d = dict(os.environ)
-    env_d.update(kv.split("=") for kv in env.split())
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
-                        str(root / "tests" / "test_gpu_parity.py"), "-k", " or ".join(tests)],
-                       env=env_d, cwd=root, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    assert f"{len(tests)} passed" in r.stdout, r.stdout[-2000:]

@@ -332,7 +332,7 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
 #define WF_AP_U 8
 #endif
 constexpr int kAttnPartThreads = WF_AP_THREADS;
-template <int G, int NS = kAttnPartSplits1>
+template <int G, int NS>
 __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* __restrict__ q, int64_t q_sb,
                                                                 const uint16_t* __restrict__ K,
                                                                 const uint16_t* __restrict__ V, int64_t kv_sb,
@@ -883,150 +883,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __res
     }
 }
 
-// The same prefill attention with the K/V tiles staged once per block in LDS: the block's 4 waves
-// (16 consecutive rows of one slot: half a kPrefillRowGroup) need the same tiles, so each wave DMAs
-// a quarter of every 16 KiB tile (4 x 1 KiB LDS-DMA, inline asm: hipcc does not drain the ring
-// before the fragment reads) into a P-slot ring, with P - 2 tiles in flight beyond the one being
-// read; the fragments come from LDS (contiguous KiB per wave-instruction). 4x less L2 / MALL
-// traffic than every wave loading its own copy, and a deeper pipeline than registers allow.
-constexpr int kPfStages = 4;  // 64 KiB ring + page ids: two blocks per CU
 constexpr int kPfMaxTiles = 256;  // 32-key tiles per sequence (max_seq <= 8192)
-template <int P>
-__global__ __launch_bounds__(256, 2) void k_attn_prefill_lds(const uint16_t* __restrict__ q, int64_t q_rs,
-                                                             const uint16_t* __restrict__ K,
-                                                             const uint16_t* __restrict__ Vt, int64_t kv_sb,
-                                                             int64_t kv_sh, int Hq, int Hkv,
-                                                             const int32_t* __restrict__ row_pos,
-                                                             const int32_t* __restrict__ row_slot, int M,
-                                                             float sm_scale, const int32_t* __restrict__ pt, int pps,
-                                                             int npages, int64_t kv_pgs, uint16_t* __restrict__ out,
-                                                             int64_t o_rs) {
-    constexpr int D = 128;
-    __shared__ __attribute__((aligned(16))) uint8_t ring[P * 16384];
-    __shared__ int s_page[kPfMaxTiles];  // the block's page ids (LDS reads: no vmcnt in the loop)
-    const int g = blockIdx.y, hq0 = g * 4;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
-    const int rb = blockIdx.x * 16;
-    if (rb >= M) return;  // whole block
-    const int r0 = rb + wave * 4;
-    const int slot = __builtin_amdgcn_readfirstlane(row_slot[rb]);  // uniform: page ids are scalar loads
-    const int lim_c = row_pos[min(r0 + (l16 >> 2), M - 1)] + 1;
-    int lim_b = 0;
-    for (int t = 0; t < 16; ++t) lim_b = max(lim_b, row_pos[min(rb + t, M - 1)] + 1);
-    const int ntiles_v = (lim_b + 31) >> 5;
-    v8s_t qf[4];
-    {
-        const uint16_t* qp = q + (int64_t)min(r0 + (l16 >> 2), M - 1) * q_rs + (int64_t)(hq0 + (l16 & 3)) * D + 8 * q4;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) qf[c] = __builtin_bit_cast(v8s_t, *reinterpret_cast<const uint4*>(qp + 32 * c));
-    }
-    // wait for q here, before the ring's asm DMAs exist: hipcc cannot count those, and a wait for q
-    // placed inside the loop would drain the ring every tile
-#pragma unroll
-    for (int c = 0; c < 4; ++c) asm volatile("" : "+v"(qf[c]));
-    const int ntiles = __builtin_amdgcn_readfirstlane(ntiles_v);
-    const uint16_t* Kg = K + (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;
-    const uint16_t* Vg = Vt + (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;
-    if (pt) {
-        for (int t = threadIdx.x; t < ntiles; t += 256) s_page[t] = min(max(pt[(int64_t)slot * pps + t], 0), npages - 1);
-        __syncthreads();
-    }
-    auto issue = [&](int t) {  // wave w DMAs pieces 4w .. 4w + 3 of tile t (K fragments 0..7, V 8..15)
-        const int64_t blk = pt ? (int64_t)s_page[t] * kv_pgs : (int64_t)t * 4096;
-        uint8_t* st = ring + (t % P) * 16384;
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-            const int j = wave * 4 + jj;
-            glds16_asm((j < 8 ? Kg : Vg) + blk + (j & 7) * 512, st + j * 1024);
-        }
-    };
-    float m_run = -INFINITY, l_run = 0.f;
-    v4f_t acc[8];
-#pragma unroll
-    for (int n = 0; n < 8; ++n) acc[n] = v4f_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < P - 1; ++t)
-        if (t < ntiles) issue(t);
-    for (int t = 0; t < ntiles; ++t) {
-        if (t + P - 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (P - 2)) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (t + P - 1 < ntiles) issue(t + P - 1);  // the slot of tile t - 1, read before this barrier
-        const uint8_t* st = ring + (t % P) * 16384;
-        uint4 kr[2][4], vr[8];
-#pragma unroll
-        for (int tau = 0; tau < 2; ++tau)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) kr[tau][c] = *reinterpret_cast<const uint4*>(st + (tau * 4 + c) * 1024 + lane * 16);
-#pragma unroll
-        for (int n = 0; n < 8; ++n) vr[n] = *reinterpret_cast<const uint4*>(st + (8 + n) * 1024 + lane * 16);
-        const int bs = 32 * t;
-        v4f_t sc[2];
-#pragma unroll
-        for (int tau = 0; tau < 2; ++tau) {
-            sc[tau] = v4f_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                sc[tau] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8s_t, kr[tau][c]), qf[c], sc[tau],
-                                                                  0, 0, 0);
-        }
-        const int lim = lim_c - bs - 8 * q4;
-        float x[8], mx = -INFINITY;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            x[e] = e < lim ? sc[e >> 2][e & 3] * sm_scale : -INFINITY;
-            mx = fmaxf(mx, x[e]);
-        }
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mnew = fmaxf(m_run, mx);  // finite: key 0 is valid for every column
-        const float alpha = __expf(m_run - mnew);
-        m_run = mnew;
-        float p[8], ps = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            p[e] = __expf(x[e] - mnew);
-            ps += p[e];
-        }
-        l_run = l_run * alpha + ps;
-        uint32_t hi[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) hi[j] = pk_bf16(p[2 * j], p[2 * j + 1]);
-        const v8s_t ph = __builtin_bit_cast(v8s_t, make_uint4(hi[0], hi[1], hi[2], hi[3]));
-        const bool resc = __any(alpha != 1.0f);
-        float ar[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ar[r] = __shfl(alpha, 4 * q4 + r, 64);
-        const int limv = lim_b - bs - 8 * q4;  // V rows past the block's last position: zero (stale)
-        uint32_t vm[4] = {~0u, ~0u, ~0u, ~0u};
-        if (limv < 8) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) vm[j] = (2 * j < limv ? 0xffffu : 0u) | (2 * j + 1 < limv ? 0xffff0000u : 0u);
-        }
-#pragma unroll
-        for (int n = 0; n < 8; ++n) {
-            if (resc) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) acc[n][r] *= ar[r];
-            }
-            const v8s_t vf =
-                __builtin_bit_cast(v8s_t, make_uint4(vr[n].x & vm[0], vr[n].y & vm[1], vr[n].z & vm[2], vr[n].w & vm[3]));
-            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vf, acc[n], 0, 0, 0);
-        }
-    }
-    l_run += __shfl_xor(l_run, 16, 64);
-    l_run += __shfl_xor(l_run, 32, 64);
-    const int row = r0 + q4;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const float inv = 1.0f / __shfl(l_run, 4 * q4 + r, 64);
-        if (row < M) {
-#pragma unroll
-            for (int n = 0; n < 8; ++n)
-                out[(int64_t)row * o_rs + (int64_t)(hq0 + r) * D + 16 * n + l16] = f2bf(rbf(acc[n][r] * inv));
-        }
-    }
-}
 
 // Prefill attention, flash style on 32 x 32 bf16 matrix cores (the default for bf16 K/V): block =
 // one row group of kPrefillRowGroup = 32 consecutive rows of one slot x kv head g; wave w takes
@@ -1055,7 +912,9 @@ __device__ __forceinline__ float swap32_sum(float v) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
-template <int STUDY>
+#ifndef WF_FA_STUDY  // diagnostic builds only (tools/build_variant.sh): 1 DMA + barriers only, 2 compute on the
+#define WF_FA_STUDY 0  // first ring fill only, 3 no exponentials, 4 no P.V MFMAs; never libwfbitnet.so
+#endif
 __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __restrict__ q, int64_t q_rs,
                                                             const uint16_t* __restrict__ K,
                                                             const uint16_t* __restrict__ Vt, int64_t kv_sb,
@@ -1064,6 +923,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
                                                             float sl2, const int32_t* __restrict__ pt, int pps,
                                                             int npages, int64_t kv_pgs, uint16_t* __restrict__ out,
                                                             int64_t o_rs, int xchunk) {
+    constexpr int STUDY = WF_FA_STUDY;
     constexpr int D = 128, P = kFaStages;
     constexpr int kSlot = 16384;  // K 8 KiB + V 8 KiB of one 32-key tile, as in the cache
     __shared__ __attribute__((aligned(16))) uint8_t ring[P * kSlot];
@@ -1091,8 +951,10 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
     const int lim_q = row_pos[qrow] + 1;  // keys [0, lim_q) of column c
     int lim_b = 0;
     for (int t = 0; t < 32; ++t) lim_b = max(lim_b, row_pos[rb + t] + 1);
-    lim_b = __builtin_amdgcn_readfirstlane(lim_b);
-    const float flq = (float)lim_q;  // positions < 2^24: exact
+    // the C-ABI only documents row_pos < max_seq: clamp, so a bad position cannot run the page fill
+    // (s_page[kPfMaxTiles]) or the DMAs past the slot's cache (k_attn_prefill clamps the same way)
+    lim_b = __builtin_amdgcn_readfirstlane(min(lim_b, 32 * min(pps, kPfMaxTiles)));
+    const float flq = (float)min(lim_q, lim_b);  // positions < 2^24: exact
     const int lim_w = (int)wave_max(flq), lim_min = (int)-wave_max(-flq);
     v8bf_t qf[8];  // Q^T fragments: column c, dims 16 s + 8 h .. + 7
     {
@@ -1262,223 +1124,6 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
     }
 }
 
-// Prefill attention with the keys split over the block's waves: block = one row group
-// (16 consecutive rows of one slot: half a kPrefillRowGroup) x kv head g. Every wave holds all 64 query
-// columns of the group (CG = 4 column groups of 4 tokens x 4 heads) and streams key tiles w, w + 4,
-// w + 8, ... in registers (its next K tile in flight during the softmax, the next V tile during the
-// P.V), so a K/V fragment is loaded once per block and feeds 4 MFMAs -- the row-split kernel above
-// runs one QK -> softmax -> P.V chain per 16 columns. The four partial (max, sum, o) sets merge
-// through LDS in fixed wave order (flash-decoding's combine inside the block); a wave with no valid
-// key for a column contributes 0. A column's result depends only on its own key range, so chunked
-// prefill stays bit-exact.
-template <bool KV8>
-__global__ __launch_bounds__(256, 1) void k_attn_prefill_ks(const uint16_t* __restrict__ q, int64_t q_rs,
-                                                            const uint16_t* __restrict__ K,
-                                                            const uint16_t* __restrict__ Vt, int64_t kv_sb,
-                                                            int64_t kv_sh, const int32_t* __restrict__ row_pos,
-                                                            const int32_t* __restrict__ row_slot, int M,
-                                                            float sm_scale, const int32_t* __restrict__ pt, int pps,
-                                                            int npages, int64_t kv_pgs, uint16_t* __restrict__ out,
-                                                            int64_t o_rs, float v_scale) {
-    constexpr int D = 128, CG = 4, kOs = D + 4;
-    using KF = KvFrag<KV8>;
-    using FT = typename KF::T;
-    __shared__ float s_ml[4][CG][2][16];                                // (wave, group, max | sum, column)
-    __shared__ __attribute__((aligned(16))) float s_o[CG][3][16][kOs];  // group u's o from the other waves
-    // ~103 KB of static LDS: needs gfx950's 160 KiB per CU (one block per CU, launch bounds (256, 1))
-    static_assert(sizeof(s_o) + sizeof(s_ml) <= 160 * 1024, "k_attn_prefill_ks exceeds the gfx950 LDS");
-    const int g = blockIdx.y, hq0 = g * 4;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
-    const int rb = blockIdx.x * 16;
-    if (rb >= M) return;  // whole block
-    const int slot = row_slot[rb];
-    const int kmax = 32 * pps;  // keys a slot holds
-    int lim_c[CG], lim_b = 0;   // column l16 of group u = (token 4u + (l16 >> 2), head l16 & 3)
-#pragma unroll
-    for (int u = 0; u < CG; ++u) lim_c[u] = min(row_pos[min(rb + 4 * u + (l16 >> 2), M - 1)] + 1, kmax);
-#pragma unroll
-    for (int t = 0; t < 16; ++t) lim_b = max(lim_b, min(row_pos[min(rb + t, M - 1)] + 1, kmax));
-    const int ntiles = (lim_b + 31) >> 5;
-    const int64_t kvo = (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;  // element offset
-    const int32_t* ptb = pt ? pt + (int64_t)slot * pps : nullptr;
-    v8s_t qf[CG][4];
-#pragma unroll
-    for (int u = 0; u < CG; ++u) {
-        const uint16_t* qp =
-            q + (int64_t)min(rb + 4 * u + (l16 >> 2), M - 1) * q_rs + (int64_t)(hq0 + (l16 & 3)) * D + 8 * q4;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) qf[u][c] = __builtin_bit_cast(v8s_t, *reinterpret_cast<const uint4*>(qp + 32 * c));
-    }
-    auto blk_of = [&](int t) -> int64_t {  // element offset of key tile t (wave-uniform t)
-        return ptb ? (int64_t)min(max(ptb[__builtin_amdgcn_readfirstlane(t)], 0), npages - 1) * kv_pgs
-                   : (int64_t)t * 4096;
-    };
-    auto load_k = [&](FT (&kr)[2][4], int64_t blk) {
-#pragma unroll
-        for (int tau = 0; tau < 2; ++tau)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) kr[tau][c] = KF::ld(K, kvo + blk + (tau * 4 + c) * 512);
-    };
-    auto load_v = [&](FT (&vr)[8], int64_t blk) {
-#pragma unroll
-        for (int n = 0; n < 8; ++n) vr[n] = KF::ld(Vt, kvo + blk + n * 512);
-    };
-    float m_run[CG], l_run[CG];
-    v4f_t acc[CG][8];
-#pragma unroll
-    for (int u = 0; u < CG; ++u) {
-        m_run[u] = -INFINITY;
-        l_run[u] = 0.f;
-#pragma unroll
-        for (int n = 0; n < 8; ++n) acc[u][n] = v4f_t{0.f, 0.f, 0.f, 0.f};
-    }
-    FT kA[2][4], vA[8];
-    if (wave < ntiles) {
-        const int64_t b0 = blk_of(wave);
-        load_k(kA, b0);
-        load_v(vA, b0);
-    }
-    for (int t = wave; t < ntiles; t += 4) {
-        const int bs = 32 * t;
-        const bool more = t + 4 < ntiles;
-        const int64_t nblk = more ? blk_of(t + 4) : 0;
-        uint4 kb[2][4];
-#pragma unroll
-        for (int tau = 0; tau < 2; ++tau)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) kb[tau][c] = KF::bf(kA[tau][c]);
-        v4f_t sc[CG][2];
-#pragma unroll
-        for (int u = 0; u < CG; ++u)
-#pragma unroll
-            for (int tau = 0; tau < 2; ++tau) {
-                sc[u][tau] = v4f_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    sc[u][tau] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8s_t, kb[tau][c]), qf[u][c],
-                                                                         sc[u][tau], 0, 0, 0);
-            }
-        if (more) load_k(kA, nblk);  // the wave's next K tile, in flight during the softmax and the P.V
-        v8s_t ph[CG];
-        float ar[CG][4];
-        bool resc[CG];
-#pragma unroll
-        for (int u = 0; u < CG; ++u) {
-            const int lim = lim_c[u] - bs - 8 * q4;  // valid keys of column l16 among this lane's 8
-            float x[8], mx = -INFINITY;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                x[e] = e < lim ? sc[u][e >> 2][e & 3] * sm_scale : -INFINITY;
-                mx = fmaxf(mx, x[e]);
-            }
-            mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-            // this wave may hold no valid key of a column yet (only wave 0 sees key 0): m stays
-            // -inf, p = 0 and acc = 0 (exp against 0, not -inf - -inf)
-            const float mnew = fmaxf(m_run[u], mx);
-            const float mref = mnew == -INFINITY ? 0.f : mnew;
-            const float alpha = __expf(m_run[u] - mref);
-            m_run[u] = mnew;
-            float p[8], ps = 0.f;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                p[e] = __expf(x[e] - mref);
-                ps += p[e];
-            }
-            l_run[u] = l_run[u] * alpha + ps;
-            uint32_t hi[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) hi[j] = pk_bf16(p[2 * j], p[2 * j + 1]);
-            ph[u] = __builtin_bit_cast(v8s_t, make_uint4(hi[0], hi[1], hi[2], hi[3]));
-            resc[u] = __any(alpha != 1.0f);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) ar[u][r] = __shfl(alpha, 4 * q4 + r, 64);
-        }
-        const int limv = lim_b - bs - 8 * q4;  // V rows past the group's last position: zero (stale)
-        v8s_t vf[8];
-#pragma unroll
-        for (int n = 0; n < 8; ++n) vf[n] = __builtin_bit_cast(v8s_t, KF::bf(KF::mask(vA[n], limv)));
-        if (more) load_v(vA, nblk);  // next V tile, in flight during the P.V and the next QK
-#pragma unroll
-        for (int u = 0; u < CG; ++u)
-#pragma unroll
-            for (int n = 0; n < 8; ++n) {
-                if (resc[u]) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) acc[u][n][r] *= ar[u][r];
-                }
-                acc[u][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph[u], vf[n], acc[u][n], 0, 0, 0);
-            }
-    }
-    // combine: column c = 4 q4 + r of group u is acc[u][*][r]; its (m, l) sit at s_ml[w][u][*][c]
-#pragma unroll
-    for (int u = 0; u < CG; ++u) {
-        float lr = l_run[u];
-        lr += __shfl_xor(lr, 16, 64);
-        lr += __shfl_xor(lr, 32, 64);
-        if (q4 == 0) {
-            s_ml[wave][u][0][l16] = m_run[u];
-            s_ml[wave][u][1][l16] = lr;
-        }
-    }
-    __syncthreads();
-    float fw[CG][4];  // this wave's weight exp(m_w - m) per (group, column)
-#pragma unroll
-    for (int u = 0; u < CG; ++u)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int c = 4 * q4 + r;
-            const float m = fmaxf(fmaxf(s_ml[0][u][0][c], s_ml[1][u][0][c]), fmaxf(s_ml[2][u][0][c], s_ml[3][u][0][c]));
-            const float mw = s_ml[wave][u][0][c];
-            fw[u][r] = mw == -INFINITY ? 0.f : __expf(mw - m);
-        }
-#pragma unroll
-    for (int u = 0; u < CG; ++u) {
-        if (u == wave) continue;
-        const int si = wave - (wave > u);
-#pragma unroll
-        for (int n = 0; n < 8; ++n)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) s_o[u][si][4 * q4 + r][16 * n + l16] = acc[u][n][r] * fw[u][r];
-    }
-    __syncthreads();
-    // wave w finishes group w: the four weighted partials summed in wave order 0..3
-#pragma unroll
-    for (int u = 0; u < CG; ++u) {
-        if (u != wave) continue;
-        const int row = rb + 4 * u + q4;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int c = 4 * q4 + r;
-            const float m = fmaxf(fmaxf(s_ml[0][u][0][c], s_ml[1][u][0][c]), fmaxf(s_ml[2][u][0][c], s_ml[3][u][0][c]));
-            float l = 0.f;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                const float mw = s_ml[w][u][0][c];
-                l += mw == -INFINITY ? 0.f : s_ml[w][u][1][c] * __expf(mw - m);
-            }
-            const float inv = (KV8 ? v_scale : 1.0f) / l;
-#pragma unroll
-            for (int n = 0; n < 8; ++n) {
-                float o = 0.f;
-#pragma unroll
-                for (int w = 0; w < 4; ++w) o += w == u ? acc[u][n][r] * fw[u][r] : s_o[u][w - (w > u)][c][16 * n + l16];
-                if (row < M) out[(int64_t)row * o_rs + (int64_t)(hq0 + r) * D + 16 * n + l16] = f2bf(rbf(o * inv));
-            }
-        }
-    }
-}
-
-// Prefill attention kernel, chosen once per process from WF_PF_ATTN (unset / 0: the flash-style
-// 32 x 32 matrix-core kernel k_attn_prefill_fa for bf16 K/V, the row-split register kernel
-// k_attn_prefill for FP8 K/V; 1: the row-split kernel for both; 2: its LDS-staged variant
-// k_attn_prefill_lds; 3: the keys split over the block's waves, k_attn_prefill_ks -- one wave per
-// SIMD, 512 registers with spills). The guard and the launch read this one value.
-int prefill_attention_variant() {
-    static const int var = getenv("WF_PF_ATTN") ? atoi(getenv("WF_PF_ATTN")) : 0;
-    return var;
-}
-
 // Contract of prefill_attention, checked by wf_model_prefill before its first launch (so a refused
 // call leaves the cache untouched).
 int prefill_attention_check(int Hq, int Hkv, int pps) {
@@ -1486,48 +1131,28 @@ int prefill_attention_check(int Hq, int Hkv, int pps) {
         set_error("prefill_attention: GQA group %d != 4 not supported", Hq / Hkv);
         return WF_EINVAL;
     }
-    if (pps > kPfMaxTiles && prefill_attention_variant() == 2) {
-        set_error("prefill_attention: the LDS-staged kernel supports max_seq <= %d", 32 * kPfMaxTiles);
-        return WF_EINVAL;
-    }
     return WF_OK;
 }
 
+// bf16 K/V: the flash-style 32 x 32 matrix-core kernel k_attn_prefill_fa, its blocks in XCD-chunked
+// order when the items split evenly over the 8 XCDs (each XCD streams one (slot, kv head) K/V at a
+// time from its own L2: 333 -> 250 us per layer at 8 x 2048); FP8 K/V, or a bf16 cache longer than
+// kPfMaxTiles tiles: the row-split register kernel k_attn_prefill ("Causal attention").
 int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                       int64_t kv_sh, int Hq, int Hkv, const int32_t* row_pos, const int32_t* row_slot, int M,
                       float sm_scale, const int32_t* pt, int pps, int npages, int64_t kv_pgs, uint16_t* out,
                       int64_t o_rs, hipStream_t st, int kv8, float k_scale, float v_scale) {
     if (int rc = prefill_attention_check(Hq, Hkv, pps)) return rc;
-    const int var = prefill_attention_variant();
-    if ((var == 0 || var >= 10) && !kv8 && pps <= kPfMaxTiles && M % 32 == 0) {
-        // XCD-chunked order when the items split evenly over the 8 XCDs (WF_PF_XCD=0: off)
-        static const bool xcd_on = !getenv("WF_PF_XCD") || atoi(getenv("WF_PF_XCD")) != 0;
-        const int items = (M / 32) * Hkv, xchunk = (xcd_on && items % 8 == 0) ? items / 8 : 0;
+    if (!kv8 && pps <= kPfMaxTiles && M % 32 == 0) {
+        const int items = (M / 32) * Hkv, xchunk = items % 8 == 0 ? items / 8 : 0;
         const dim3 grid = xchunk ? dim3(items) : dim3(M / 32, Hkv);
         const float sl2 = sm_scale * 1.4426950408889634f;
-#define WF_FA(S) hipLaunchKernelGGL((k_attn_prefill_fa<S>), grid, dim3(256), 0, st, q, q_rs, k, v, kv_sb, kv_sh, row_pos, \
-                                    row_slot, M, sl2, pt, pps, npages, kv_pgs, out, o_rs, xchunk)
-        if (var == 11) WF_FA(1);       // study: DMA + barriers only
-        else if (var == 12) WF_FA(2);  // study: compute on the first ring fill only
-        else if (var == 13) WF_FA(3);  // study: no exponentials
-        else if (var == 14) WF_FA(4);  // study: no P.V MFMAs
-        else WF_FA(0);
-#undef WF_FA
-    } else if (var == 3) {
-        const dim3 grid((M + 15) / 16, Hkv);
-        if (kv8)
-            hipLaunchKernelGGL((k_attn_prefill_ks<true>), grid, dim3(256), 0, st, q, q_rs, k, v, kv_sb, kv_sh, row_pos,
-                               row_slot, M, sm_scale * k_scale, pt, pps, npages, kv_pgs, out, o_rs, v_scale);
-        else
-            hipLaunchKernelGGL((k_attn_prefill_ks<false>), grid, dim3(256), 0, st, q, q_rs, k, v, kv_sb, kv_sh, row_pos,
-                               row_slot, M, sm_scale, pt, pps, npages, kv_pgs, out, o_rs, 1.0f);
+        hipLaunchKernelGGL(k_attn_prefill_fa, grid, dim3(256), 0, st, q, q_rs, k, v, kv_sb, kv_sh, row_pos, row_slot, M,
+                           sl2, pt, pps, npages, kv_pgs, out, o_rs, xchunk);
     } else if (kv8)
         hipLaunchKernelGGL((k_attn_prefill<1, 2, true>), dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v, kv_sb,
                            kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale * k_scale, pt, pps, npages, kv_pgs, out, o_rs,
                            v_scale);
-    else if (var == 2)
-        hipLaunchKernelGGL((k_attn_prefill_lds<kPfStages>), dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v,
-                           kv_sb, kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale, pt, pps, npages, kv_pgs, out, o_rs);
     else
         hipLaunchKernelGGL((k_attn_prefill<1, 2>), dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v, kv_sb,
                            kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale, pt, pps, npages, kv_pgs, out, o_rs, 1.0f);
@@ -1547,7 +1172,7 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
         // one block per query head (G = 1): 4x the blocks of one per kv head at Hq/Hkv = 4, a quarter
         // of the per-lane arithmetic (at batch 1 the kernel is latency-bound on its score/softmax
         // chain; the K/V re-reads of the group's heads hit L2)
-        hipLaunchKernelGGL((k_attn_part<1>), dim3(kAttnPartSplits1, Hq, B), dim3(kAttnPartThreads), 0, st, q, q_sb, k, v,
+        hipLaunchKernelGGL((k_attn_part<1, kAttnPartSplits1>), dim3(kAttnPartSplits1, Hq, B), dim3(kAttnPartThreads), 0, st, q, q_sb, k, v,
                            kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, ml, o);
         return check_launch("decode_attention_partials");
     }
@@ -1558,57 +1183,19 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
             set_error("decode_attention_partials: tiled K/V need S %% 32 == 0 (S=%d)", S);
             return WF_EINVAL;
         }
-        static const int variant = getenv("WF_ATTN_VARIANT") ? atoi(getenv("WF_ATTN_VARIANT")) : 0;
-        static const int variant8 = getenv("WF_ATTN_VARIANT8") ? atoi(getenv("WF_ATTN_VARIANT8")) : 0;
-        if (kv8) {  // FP8 caches: K scale folded into the score scale
-            const dim3 wg(kAttnPartSplits / 4, Hkv, B);
-            if (variant8 == 5)
-                hipLaunchKernelGGL((k_attn_mfma<false, false, false, true, true>), dim3(kAttnPartSplits / 2, Hkv, B),
-                                   dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale,
-                                   ml, o, pt, pps, npages, kv_pgs, v_scale);
-            else if (variant8 == 4)
-                hipLaunchKernelGGL((k_attn_mfma<true, false, true, true>), wg, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
-                                   kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale, ml, o, pt, pps, npages, kv_pgs,
-                                   v_scale);
-            else if (variant8 == 3)
-                hipLaunchKernelGGL((k_attn_mfma<false, false, true, true>), wg, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
-                                   kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale, ml, o, pt, pps, npages, kv_pgs,
-                                   v_scale);
-            else if (variant8 == 2)
-                hipLaunchKernelGGL((k_attn_mfma<true, false, false, true>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
-                                   kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale, ml, o, pt, pps, npages, kv_pgs,
-                                   v_scale);
-            else
-                hipLaunchKernelGGL((k_attn_mfma<false, false, false, true>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
-                                   kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale, ml, o, pt, pps, npages, kv_pgs,
-                                   v_scale);
-            return check_launch("decode_attention_partials");
-        }
-        const dim3 wgrid(kAttnPartSplits / 4, Hkv, B);
-        if (variant == 5)
-            hipLaunchKernelGGL((k_attn_mfma<false, false, false, false, true>), dim3(kAttnPartSplits / 2, Hkv, B),
-                               dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, ml, o, pt,
-                               pps, npages, kv_pgs, 1.0f);
-        else if (variant == 3)
-            hipLaunchKernelGGL((k_attn_mfma<false, false, true>), wgrid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq,
-                               Hkv, S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs, 1.0f);
-        else if (variant == 4)
-            hipLaunchKernelGGL((k_attn_mfma<true, false, true>), wgrid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq,
-                               Hkv, S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs, 1.0f);
-        else if (variant == 1)
-            hipLaunchKernelGGL((k_attn_mfma<false, true>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv,
-                               S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs, 1.0f);
-        else if (variant == 2)  // one tile in flight per wave, 4 waves per SIMD (the default at 8 splits)
-            hipLaunchKernelGGL((k_attn_mfma<false, false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq,
-                               Hkv, S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs, 1.0f);
-        else  // default: double-buffered tiles, 2 waves per SIMD (at 4 splits a wave takes >= 2 tiles at ctx >= 1024)
+        if (kv8)  // FP8 caches: K scale folded into the score scale; one tile in flight per wave, 4 waves per SIMD
+            hipLaunchKernelGGL((k_attn_mfma<false, false, false, true>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
+                               kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale, ml, o, pt, pps, npages, kv_pgs, v_scale);
+        else  // bf16: double-buffered tiles, 2 waves per SIMD (at 4 splits a wave takes >= 2 tiles at ctx >= 1024)
             hipLaunchKernelGGL((k_attn_mfma<true, false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv,
                                S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs, 1.0f);
         return check_launch("decode_attention_partials");
     }
+    // batch >= 16 on untiled caches (TQ weights, or max_seq % 32 != 0): the VALU kernel, one block per
+    // kv head, with the batched record count (the reader, k_rownorm_attn, merges kAttnPartSplits)
 #define WF_AP(GV)                                                                                                   \
-    hipLaunchKernelGGL((k_attn_part<GV>), grid, dim3(kAttnPartThreads), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, \
-                       seq_lens, sm_scale, ml, o)
+    hipLaunchKernelGGL((k_attn_part<GV, kAttnPartSplits>), grid, dim3(kAttnPartThreads), 0, st, q, q_sb, k, v, kv_sb,  \
+                       kv_sh, Hq, Hkv, S, seq_lens, sm_scale, ml, o)
     if (grp == 1) WF_AP(1);
     else if (grp == 2) WF_AP(2);
     else if (grp <= 4) WF_AP(4);

@@ -84,7 +84,6 @@ struct GemvArgs {
     // FP8 (e4m3fn) K/V cache: stored code = e4m3(clamp(y / scale, +-448)), RNE
     int kv8;
     float k_inv, v_inv;
-    int gu_quad;  // GU epilogue: quad-transposed 8-byte act stores (EpiDec; WF_GU_QUAD=0: per element)
 };
 
 __device__ __forceinline__ uint8_t to_fp8(float y) {
@@ -411,7 +410,7 @@ struct EpiDec {
             // transposed (4 DPP moves) so that lane (quad k, qi) holds row 4q + qi, columns 4k .. 4k + 3:
             // one 8-byte store per lane instead of four 2-byte ones (the stores were the epilogue's cost:
             // a quarter of them took the prefill gate|up GEMM from 570 to 472 us per layer).
-            if (g.gu_quad && ((g.out_stride & 3) | (reinterpret_cast<uintptr_t>(g.out) & 7)) == 0) {
+            if (((g.out_stride & 3) | (reinterpret_cast<uintptr_t>(g.out) & 7)) == 0) {
                 const float ws = l16 < 8 ? g.ws0 : g.ws1;
                 float y[4];
 #pragma unroll
@@ -1701,8 +1700,6 @@ GemvArgs base_args(const wf_model* m, int l) {
     a.v_inv = d.kv_fp8 ? 1.0f / m->kv_scale[2 * l + 1] : 1.0f;
     a.kv_b_stride = (int64_t)d.n_kv_heads * d.max_seq * d.head_dim;
     a.kv_t = m->kv_tiled;
-    static const int gu_quad = getenv("WF_GU_QUAD") ? atoi(getenv("WF_GU_QUAD")) : 1;
-    a.gu_quad = gu_quad;
     return a;
 }
 
@@ -1941,6 +1938,15 @@ int wf_model_launch_op(wf_model* m, int layer, int op, void* stream) {
     return run_op(m, layer, op, as_stream(stream));
 }
 
+int wf_model_attn_view(const wf_model* m, wf_model_attn_view* out) {
+    WF_REQUIRE(m && out, "model_attn_view: null argument");
+    out->q = m->qbuf;
+    out->part_ml = reinterpret_cast<const float*>(m->part_ml);
+    out->part_o = m->part_o;
+    out->records = m->d.batch < 16 ? kAttnPartSplits1 : kAttnPartSplits;
+    return WF_OK;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Prefill: the prompt tokens of any KV slots as GEMM rows (BASELINE configs[2]). Per layer:
 // row norm + quantize (tile order) -> fused prefill GEMM (k_pgemm_fused) for QKV (+ RoPE, K/V
@@ -2007,16 +2013,13 @@ static void prefill_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, co
 #undef WF_RN8
 }
 
-// LDS-staged row-tile epilogue (pf_tile_epilogue) where the output rows are 16-byte pieces
-// (WF_PF_EPI=0: per-fragment EpiDec, for A/B studies)
+// LDS-staged row-tile epilogue (pf_tile_epilogue) where the output rows are 16-byte pieces: o / down
+// (256-column tiles; measured o 141 -> 131, down 275 -> 262 us per layer at 16384 rows); the
+// 512-column gate|up tile stays per fragment (staged: 570 -> 614 us)
 static bool pf_staged_ok(const GemvArgs& a, bool wide) {
-    // default: O / DN (256-column tiles; measured o 141 -> 131, down 275 -> 262 us per layer at 16384
-    // rows); the 512-column gate|up tile stays per fragment (staged: 570 -> 614 us)
-    static const int mode = getenv("WF_PF_EPI") ? atoi(getenv("WF_PF_EPI")) : 1;
-    const bool on = mode == 2 || (mode == 1 && !wide);
     const bool al = a.out_stride % 8 == 0 && reinterpret_cast<uintptr_t>(a.out) % 16 == 0 &&
                     (!a.resid || reinterpret_cast<uintptr_t>(a.resid) % 16 == 0);
-    return on && al;
+    return !wide && al;
 }
 template <int MODE, int TNW, int ALG>
 static void pg_launch(const GemvArgs& a, int nbm, int nbn, hipStream_t st) {
@@ -2027,21 +2030,16 @@ static void pg_launch(const GemvArgs& a, int nbm, int nbn, hipStream_t st) {
     else
         hipLaunchKernelGGL((k_pgemm_fused<MODE, TNW, ALG, false>), dim3(nbm * nbn), dim3(512), 0, st, a, nbm, nbn);
 }
-template <int MODE, int TNW>
-static void pg_launch_alg(int alg, const GemvArgs& a, int nbm, int nbn, hipStream_t st) {
-    if (alg == 3) pg_launch<MODE, TNW, 3>(a, nbm, nbn, st);
-    else pg_launch<MODE, TNW, 0>(a, nbm, nbn, st);
-}
 template <int MODE>
 static void prefill_gemm(const GemvArgs& a, hipStream_t st) {
     const int nbm = (a.B + 127) / 128;
     if constexpr (MODE != MODE_QKV) {
         if (pg_wide(a.N)) {  // gate|up: 128 x 512 tiles
-            pg_launch_alg<MODE, 8>(pg_alg(true, 0), a, nbm, (a.N + 511) / 512, st);
+            pg_launch<MODE, 8, 0>(a, nbm, (a.N + 511) / 512, st);
             return;
         }
     }
-    pg_launch_alg<MODE, 4>(pg_alg(false, 0), a, nbm, (a.N + 255) / 256, st);
+    pg_launch<MODE, 4, 0>(a, nbm, (a.N + 255) / 256, st);
 }
 }  // extern "C++"
 

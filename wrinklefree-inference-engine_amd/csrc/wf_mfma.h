@@ -148,11 +148,8 @@ constexpr int pg_stages() { return TNW == 4 ? kPgStages : 4; }
 template <int TNW>
 constexpr int pg_block_cols() { return TNW * 64; }
 // 512-column tiles where N fills them and there are enough of them for the chip
-// (WF_PG_WIDE_MIN_N: study override of the 8192 threshold)
-inline bool pg_wide(int N) {
-    static const int min_n = getenv("WF_PG_WIDE_MIN_N") ? atoi(getenv("WF_PG_WIDE_MIN_N")) : 8192;
-    return N % 512 == 0 && N >= min_n;
-}
+constexpr int kPgWideMinN = 8192;
+inline bool pg_wide(int N) { return N % 512 == 0 && N >= kPgWideMinN; }
 
 // XCD-aware grouped tile order (measured: 4 % less time than plain row-major order)
 __device__ __forceinline__ void pg_tile_of(int bid, int nbm, int nbn, int& bm, int& bn) {
@@ -370,13 +367,4 @@ __device__ __forceinline__ void pg_main(const uint8_t* __restrict__ W, const int
                                         int K, int bm, int bn, uint8_t* lds, v4i_t (&acc)[4][TNW]) {
     pgemm_tile<PgCfg<TNW, ALG>::P, TNW, PgCfg<TNW, ALG>::CW>(W, A, M, N, K, bm, bn, lds, acc);
 }
-// study switches (read once): WF_PG_ALG for the 256-column tiles, WF_PG_ALG8 for the 512-column
-// ones (def: the default of the caller)
-inline int pg_alg(bool wide, int def) {
-    static const int alg = getenv("WF_PG_ALG") ? atoi(getenv("WF_PG_ALG")) : -1;
-    static const int alg8 = getenv("WF_PG_ALG8") ? atoi(getenv("WF_PG_ALG8")) : -1;
-    const int a = wide ? alg8 : alg;
-    return (a == 0 || a == 3) ? a : def;
-}
-
 }  // namespace wf

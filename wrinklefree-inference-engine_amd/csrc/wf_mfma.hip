@@ -155,15 +155,10 @@ extern "C" int wf_bitnet_gemm_tiled(const uint8_t* w, const int8_t* a, float sca
 #define WF_PGT(TNWV, ALGV, NBN) \
     hipLaunchKernelGGL((k_pgemm_t<TNWV, ALGV>), dim3(nbm * (NBN)), dim3(512), 0, as_stream(stream), w, a, scale, M, N, K, y, \
                        ldy, nbm, NBN)
-    if (pg_wide(N)) {  // 512-column tiles: CW main loop by default
-        const int nbn = (N + 511) / 512;
-        if (pg_alg(true, 3) == 3) WF_PGT(8, 3, nbn);
-        else WF_PGT(8, 0, nbn);
-    } else {
-        const int nbn = (N + 255) / 256;
-        if (pg_alg(false, 0) == 3) WF_PGT(4, 3, nbn);
-        else WF_PGT(4, 0, nbn);
-    }
+    if (pg_wide(N))  // 512-column tiles: column-wave (CW) main loop (standalone gate|up 565 -> 523 us)
+        WF_PGT(8, 3, (N + 511) / 512);
+    else  // 256-column tiles: 2 x 4 wave grid (CW reads all 8 A row tiles per stage: over the LDS rate)
+        WF_PGT(4, 0, (N + 255) / 256);
 #undef WF_PGT
     return check_launch("gemm_tiled");
 }

@@ -336,6 +336,9 @@ __device__ __forceinline__ int64_t bf_tile_off(int r, int p, int H) {
 constexpr int kAttnPartSplits = WF_SPLITS;    // records per (sequence, query head): batched decode (B >= 16)
 constexpr int kAttnPartSplits1 = WF_SPLITS1;  // batch < 16 (16 measured: attention 5.70 -> 5.63 us, O input 6.01 -> 7.27 us)
 constexpr int kAttnPartSplitsMax = 16;
+static_assert(kAttnPartSplits <= kAttnPartSplitsMax && kAttnPartSplits1 <= kAttnPartSplitsMax,
+              "part_ml / part_o are sized for kAttnPartSplitsMax records per (sequence, head)");
+static_assert(kAttnPartSplits % 4 == 0 && kAttnPartSplits1 % 2 == 0, "record counts: whole 4-wave blocks / pairs");
 // Float offset of element d of split s's unnormalised o in the decode-attention partials of (b, h)
 // (bh = b * Hq + h; head_dim 128): [bh][split][half = (d >> 2) & 1][d >> 3][4]. The merging reader
 // (AttnRow) gives each thread the 8-wide piece d0 = 8 t of every split and loads it as two halves:

@@ -61,6 +61,7 @@ SIGNATURES = {
     "wf_model_step": (i32, [vp, vp]),
     "wf_model_graph_launch": (i32, [vp, vp]),
     "wf_model_launch_op": (i32, [vp, i32, i32, vp]),
+    "wf_model_attn_view": (i32, [vp, vp]),
     "wf_model_prefill_reserve": (i32, [vp, i32]),
     "wf_model_prefill": (i32, [vp, vp, vp, vp, i32, vp]),
 }
@@ -76,6 +77,11 @@ class WFModelDesc(C.Structure):
                                           "tokens", "positions", "logits", "k_cache", "v_cache")] + \
                [("debug_flags", C.c_int), ("page_table", C.c_void_p), ("num_pages", C.c_int),
                 ("kv_fp8", C.c_int), ("kv_scale", C.c_void_p)]
+
+
+class WFAttnView(C.Structure):
+    """Mirror of wf_model_attn_view (include/wf_bitnet.h)."""
+    _fields_ = [("q", C.c_void_p), ("part_ml", C.c_void_p), ("part_o", C.c_void_p), ("records", C.c_int)]
 
 
 class KernelError(RuntimeError):

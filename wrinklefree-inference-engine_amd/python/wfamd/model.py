@@ -458,6 +458,29 @@ class BitNetDecoder:
         st = torch.cuda.current_stream().cuda_stream
         call("wf_model_graph_launch" if graph else "wf_model_step", self._h, st)
 
+    def attention_records(self):
+        """The last WF_OP_QKV / WF_OP_ATTN hand-off (include/wf_bitnet.h wf_model_attn_view) as torch
+        tensors on the device: q [B, Hq, D] bf16, ml [B, Hq, R, 2] (m, l), o [B, Hq, R, D] float
+        (unnormalised, logical dim order). For kernel-level checks; copies, not views."""
+        v = _lib.WFAttnView()
+        call("wf_model_attn_view", self._h, C.addressof(v))
+        cfg, B = self.cfg, self.batch
+        Hq, D, R = cfg.n_heads, cfg.head_dim, int(v.records)
+        if D != 128:
+            raise ValueError("attention records need head_dim 128")
+
+        q = torch.empty(B, Hq, D, dtype=torch.bfloat16, device=self.dev)
+        ml = torch.empty(B, Hq, R, 2, dtype=torch.float32, device=self.dev)
+        o = torch.empty(B * Hq * R * D, dtype=torch.float32, device=self.dev)
+        ops.device_copy(q.data_ptr(), v.q, q.numel() * 2)
+        ops.device_copy(ml.data_ptr(), v.part_ml, ml.numel() * 4)
+        ops.device_copy(o.data_ptr(), v.part_o, o.numel() * 4)
+        # record layout: element d at ((d >> 2) & 1) * 64 + (d >> 3) * 4 + (d & 3)
+        d = torch.arange(D, device=self.dev)
+        idx = ((d >> 2) & 1) * 64 + (d >> 3) * 4 + (d & 3)
+        o = o.view(B, Hq, R, D)[..., idx]
+        return q, ml, o
+
     @property
     def weight_bytes(self) -> int:
         return sum(t.numel() for t in (self.w_qkv, self.w_o, self.w_gu, self.w_d)) + self.embed.numel() * 2

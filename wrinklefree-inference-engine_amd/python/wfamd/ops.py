@@ -48,6 +48,23 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
 
+_hip_rt = None
+
+
+def device_copy(dst: int, src: int, nbytes: int) -> None:
+    """Stream-ordered device-to-device copy between raw device pointers (hipMemcpyAsync on torch's
+    current stream): reads library-owned buffers exposed by the C-ABI (wf_model_attn_view)."""
+    global _hip_rt
+    if _hip_rt is None:
+        import ctypes as C
+        _hip_rt = C.CDLL("libamdhip64.so")
+        _hip_rt.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+        _hip_rt.hipMemcpyAsync.restype = C.c_int
+    rc = _hip_rt.hipMemcpyAsync(dst, src, nbytes, 3, _stream())  # hipMemcpyDeviceToDevice
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpyAsync failed ({rc})")
+
+
 def check_kernel_available() -> bool:
     return _lib.kernel_available()
 
