@@ -232,8 +232,8 @@ typedef struct {
     const float* part_ml;
     const float* part_o;
     int records;
-} wf_model_attn_view;
-int wf_model_attn_view(const wf_model* m, wf_model_attn_view* out);
+} wf_attn_records;
+int wf_model_attn_view(const wf_model* m, wf_attn_records* out);
 /* Prefill (BASELINE configs[2]; the prompt pass that precedes scripts/direct_inference_full.py's
  * decode loop): run prompt tokens of any KV slots through all layers as GEMM rows and write their
  * K/V into the cache (dense planes or pages). Batched matrix-core decoders only (batch >= 16, I2_S

@@ -1938,7 +1938,7 @@ int wf_model_launch_op(wf_model* m, int layer, int op, void* stream) {
     return run_op(m, layer, op, as_stream(stream));
 }
 
-int wf_model_attn_view(const wf_model* m, wf_model_attn_view* out) {
+int wf_model_attn_view(const wf_model* m, wf_attn_records* out) {
     WF_REQUIRE(m && out, "model_attn_view: null argument");
     out->q = m->qbuf;
     out->part_ml = reinterpret_cast<const float*>(m->part_ml);

@@ -80,7 +80,7 @@ class WFModelDesc(C.Structure):
 
 
 class WFAttnView(C.Structure):
-    """Mirror of wf_model_attn_view (include/wf_bitnet.h)."""
+    """Mirror of wf_attn_records (include/wf_bitnet.h wf_model_attn_view)."""
     _fields_ = [("q", C.c_void_p), ("part_ml", C.c_void_p), ("part_o", C.c_void_p), ("records", C.c_int)]
 
 
