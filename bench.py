@@ -8,13 +8,15 @@ One "step" = one decode token for every sequence of the batch through all 30 lay
 LM head (greedy), replayed as one HIP graph; inputs (weights, KV context, token) resident in HBM.
 Default workload = BASELINE configs[1]: batch 1 on one MI355X, synthetic random-init weights of the
 2B-4T architecture (no checkpoint offline), KV context pre-filled to --ctx positions.
-N > 1 (torch.distributed.run, one rank per GPU): independent replicas, no data-path collective
-(SURVEY §8e); value = all ranks' tokens / max-over-ranks time.
+N > 1 (torch.distributed.run, one rank per GPU): independent replicas, each pinned to its own slice
+of the host cores, no data-path collective and no RCCL communicator (a gloo barrier on the host;
+SURVEY §8e); value = all ranks' tokens / max-over-ranks time.
 
 Also measured live: per-op kernel durations with HIP events (graph replays of each op's 30
 launches, each after a full decode step so caches are in their in-step state), the dominant
 kernel's achieved HBM GB/s vs the 8 TB/s peak (PMC traffic from profiles/pmc_traffic.json), and the
-CPU oracle's decode speed on this host's cores (rank 0, N = 1).
+CPU baseline (oracle/cpu_baseline.py: AVX512-VNNI build of the oracle's decode step) on this host's
+cores, all cores and pinned to 8 (rank 0, N = 1).
 """
 from __future__ import annotations
 
@@ -41,7 +43,7 @@ def parse():
     ap.add_argument("--ctx", type=int, default=1024)
     ap.add_argument("--wfmt", choices=["tq", "i2s"], default="i2s")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-op-timing", action="store_true")
     ap.add_argument("--max-seq", type=int, default=0, help="KV rows per (sequence, kv head); 0 = model default")
     ap.add_argument("--ctx-dist", choices=["fixed", "uniform"], default="fixed",
@@ -147,82 +149,36 @@ def gemv_bench(rotate_bytes: float = 1.2e9, reps: int = 3):
     return out
 
 
-def cpu_gemv(seconds_per_shape: float = 1.5):
-    """The oracle's I2_S GEMV (oracle/wf_oracle.c, OpenMP) on the same shapes on the host cores."""
-    import numpy as np
-    from oracle import oracle as orc
-    rng = np.random.default_rng(0)
-    out = {}
-    for name, N, K in GEMV_SHAPES:
-        p = (rng.integers(0, 256, size=(N, K // 4), dtype=np.uint8) & 0xAA).astype(np.uint8)
-        a = rng.integers(-128, 128, size=K, dtype=np.int8)
-        orc.gemv_i2s(p, a, 0.01)
-        n, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < seconds_per_shape:
-            orc.gemv_i2s(p, a, 0.01)
-            n += 1
-        us = 1e6 * (time.perf_counter() - t0) / n
-        nbytes = N * K // 4 + K + 4 * N
-        out[name] = {"us": round(us, 1), "gbs": round(nbytes / us / 1e3, 2)}
-    return out
-
-
-def cpu_baseline(ctx: int, seconds: float):
-    """The C oracle's full decode step (oracle/wf_oracle.c orc_decode_step) of the same 2B model shape
-    on this host's cores; random weights (timing only), bounded sample."""
-    import numpy as np
-    import torch
-    from oracle import oracle as orc
-    from wfamd.model import BITNET_2B as cfg, rope_tables
-    libname = "liborc_native.so"
-    try:
-        orc.build(march="native", name=libname)
-    except Exception:
-        libname = "liborc.so"
-        orc.build()
-    rng = np.random.default_rng(0)
-    H, L, HQ, HKV, D, I, V = cfg.hidden, cfg.layers, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, cfg.inter, cfg.vocab
-    S = ctx + 2048  # room for a time-bounded sample (~30 tok/s on 16 cores)
-    lut = np.array([((v // 27) % 3) << 6 | ((v // 9) % 3) << 4 | ((v // 3) % 3) << 2 | (v % 3) for v in range(81)],
-                   dtype=np.uint8)
-
-    def tern(*shape):
-        return lut[rng.integers(0, 81, size=shape, dtype=np.uint8)]
-
-    def bf16_small(*shape):  # random bf16 bit patterns of magnitude ~0.01 (timing only)
-        sign = rng.integers(0, 2, size=shape, dtype=np.uint16) << 15
-        return (0x3C00 + rng.integers(0, 0x100, size=shape, dtype=np.uint16)) | sign
-
-    def bf16_one(*shape):
-        return np.full(shape, 0x3F80, dtype=np.uint16)
-
-    cos, sin = rope_tables(D, S, cfg.rope_theta)
-    a = {
-        "cfg": np.array([H, L, HQ, HKV, D, I, V, S], dtype=np.int64), "eps": np.float32(cfg.eps),
-        "embed": bf16_small(V, H), "final_norm": bf16_one(H),
-        "rope_cos": cos.view(torch.int16).numpy().view(np.uint16),
-        "rope_sin": sin.view(torch.int16).numpy().view(np.uint16),
-        "ln_in": bf16_one(L, H), "ln_post": bf16_one(L, H), "attn_sub": bf16_one(L, H), "ffn_sub": bf16_one(L, I),
-        "wq": tern(L, H, H // 4), "wk": tern(L, HKV * D, H // 4), "wv": tern(L, HKV * D, H // 4),
-        "wo": tern(L, H, H // 4), "wg": tern(L, I, H // 4), "wu": tern(L, I, H // 4), "wd": tern(L, H, I // 4),
-        "wscale": np.full((L, 7), 1.75, dtype=np.float32),
-    }
-    m = orc.DecodeModel(a, libname)
-    m.k_cache[:, :, :ctx] = bf16_small(L, HKV, ctx, D)
-    m.v_cache[:, :, :ctx] = bf16_small(L, HKV, ctx, D)
-    m.step(1, ctx)  # warm (page in weights)
-    n, t0 = 0, time.perf_counter()
-    tok = 1
-    while True:
-        _, tok = m.step(tok, ctx + 1 + n)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or ctx + 2 + n >= S:
-            break
-    return {"value": round(n / el, 3), "unit": "tokens/s", "cores": orc.num_threads(libname), "kind": "port",
-            "sample": f"oracle/wf_oracle.c orc_decode_step, full 30-layer bitnet-b1.58-2B-4T shape, batch 1, "
-                      f"ctx {ctx}, {n} tokens in {el:.1f}s (random weights)",
-            "ms_per_token": round(1000 * el / n, 2)}
+def cpu_baseline(ctx: int, seconds: float, pin_cores: int = 8):
+    """The CPU baseline on this host (oracle/cpu_baseline.py, run as a child process so its core
+    affinity and OpenMP pool are its own): the oracle's full decode step of the 2B model shape and the
+    standalone GEMV shapes, AVX512-VNNI build where the host has it, timed (1) on every core of this
+    process's affinity mask with the environment's OMP_NUM_THREADS and (2) pinned to `pin_cores`
+    cores with as many threads (the reference's server pin, scripts/launch_sglang_bitnet.sh:61).
+    Bounded samples of `seconds` each; random weights (timing only)."""
+    import subprocess
+    runs = {}
+    for name, cores in (("all", 0), (f"pin{pin_cores}", pin_cores)):
+        env = dict(os.environ)
+        if cores:
+            env["OMP_NUM_THREADS"] = str(cores)
+        cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--ctx", str(ctx), "--seconds", str(seconds),
+               "--gemv-seconds", "1.0", "--cores", str(cores)]
+        r = subprocess.run(cmd, cwd=str(ROOT), env=env, capture_output=True, text=True, timeout=600)
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not lines:
+            raise RuntimeError(f"cpu baseline ({name}) failed: {r.stderr[-1500:]}")
+        runs[name] = json.loads(lines[-1])
+    a, p = runs["all"], runs[f"pin{pin_cores}"]
+    return {"value": a["decode"]["tokens_per_s"], "unit": "tokens/s", "cores": a["threads"], "kind": "port",
+            "sample": f"oracle/wf_oracle.c orc_decode_step ({a['build']}), full 30-layer bitnet-b1.58-2B-4T shape, "
+                      f"batch 1, ctx {ctx}, {a['decode']['tokens']} tokens in {a['decode']['seconds']}s (random weights)",
+            "ms_per_token": a["decode"]["ms_per_token"], "cpu_model": a["cpu_model"], "isa": a["isa"],
+            "omp_threads": a["threads"], "affinity_cpus": a["affinity_cpus"],
+            "logical_cpus_total": a["logical_cpus_total"],
+            f"pinned_{pin_cores}_cores": {"value": p["decode"]["tokens_per_s"], "omp_threads": p["threads"],
+                                          "ms_per_token": p["decode"]["ms_per_token"], "gemv": p["gemv"]},
+            "gemv": a["gemv"]}
 
 
 def main():
@@ -231,14 +187,23 @@ def main():
     import torch.distributed as dist
     from wfamd import WF_FMT_I2S, WF_FMT_TQ, _lib
     from wfamd.model import BITNET_2B, BitNetDecoder, synthetic_weights
-    from wfamd.replicas import replica_rate, timed_steps
+    from wfamd.replicas import pin_host_cores, replica_rate, timed_steps
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    # the CPU baseline runs in child processes BEFORE this process touches the GPU (no fork of a
+    # GPU-initialised process; the host is idle while it runs)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(max(1, min(args.ctx, 4096 - args.warmup - args.steps - 2)), args.cpu_seconds)
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # independent replicas: a disjoint host-core slice per rank, set before the
+        # first GPU call; a host (gloo) barrier only -- no RCCL communicator exists
+        pin_host_cores(local, local_world)
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
     if not _lib.kernel_available():
         raise SystemExit("gfx950 HIP kernels unavailable: build with __graft_entry__.build()")
 
@@ -272,7 +237,7 @@ def main():
     for _ in range(args.warmup):
         dec.step(graph=True)
     el = timed_steps(lambda: dec.step(graph=True), args.steps, torch.cuda.synchronize,
-                     dist if world > 1 else None, device="cuda")
+                     dist if world > 1 else None)
     tok_s = replica_rate(B, args.steps, world, el)
     ms_step = 1000.0 * el / args.steps
 
@@ -295,12 +260,10 @@ def main():
     kv_esz = 1 if args.kv == "fp8" else 2
     step_bytes = cfg.weight_bytes_per_token(wfmt) + B * cfg.kv_bytes_per_token(ctx + total // 2) * kv_esz // 2
     gemv = None if (args.no_gemv or B != 1) else gemv_bench()
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(ctx, args.cpu_seconds)
+    if cpu:
+        cpu_gemv = cpu.pop("gemv")
         if gemv:
-            cg = cpu_gemv()
-            for k, v in cg.items():
+            for k, v in cpu_gemv.items():
                 gemv[k]["cpu_us"], gemv[k]["cpu_gbs"] = v["us"], v["gbs"]
 
     if rank == 0:

@@ -17,7 +17,9 @@ _HERE = Path(__file__).resolve().parent
 _lib = None
 
 
-def build(march: str | None = None, name: str = "liborc.so") -> Path:
+def build(march: str | None = None, name: str = "liborc.so", defines=()) -> Path:
+    """liborc.so = the checker (make); any other name = a CPU-baseline build for this host
+    (-march=native; defines=("ORC_VNNI",) for the AVX512-VNNI / BF16 kernels)."""
     args = ["make", "-s", "-C", str(_HERE), name] if name == "liborc.so" else None
     if name == "liborc.so":
         if march:
@@ -25,8 +27,8 @@ def build(march: str | None = None, name: str = "liborc.so") -> Path:
         subprocess.run(args, check=True)
     else:  # a separately named build (e.g. -march=native for the CPU baseline on the GPU box's host)
         out = _HERE / name
-        subprocess.run(["gcc", "-O3", f"-march={march or 'native'}", "-fopenmp", "-fPIC", "-std=c11", "-shared",
-                        "-o", str(out), str(_HERE / "wf_oracle.c"), "-lm"], check=True)
+        subprocess.run(["gcc", "-O3", f"-march={march or 'native'}", "-fopenmp", "-fPIC", "-std=c11", "-shared"] +
+                       [f"-D{d}" for d in defines] + ["-o", str(out), str(_HERE / "wf_oracle.c"), "-lm"], check=True)
     return _HERE / name
 
 
@@ -71,6 +73,8 @@ def _load(path: Path):
     L.orc_f32_to_e4m3.restype = C.c_uint8
     L.orc_e4m3_to_f32.argtypes = [C.c_uint8]
     L.orc_e4m3_to_f32.restype = f32
+    L.orc_vnni_build.argtypes = []
+    L.orc_vnni_build.restype = C.c_int
     L.orc_num_threads.argtypes = []
     L.orc_num_threads.restype = C.c_int
     return L
