@@ -332,15 +332,26 @@ def test_fp8_kv_attention_cosine_reference_bar(orc, ctx):
 def test_prefill_8x2048_full_width_vs_oracle(orc):
     """wf_model_prefill of 8 sequences x 2048 tokens (16384 GEMM rows: the 128 x 512 gate|up tiles
     and every full-size prefill kernel) through 2 full-width layers, then one decode step per
-    sequence, against the oracle's teacher-forced decode of the same tokens
-    (orc_decode_step over every prompt position): the K/V rows of all 2048 positions of sequence 0
-    and the first 512 of sequence 5, both layers, rel-L2 <= 1e-3 per 256-position chunk; the
-    next-step logits of sequence 0 rel-L2 <= 1e-3."""
+    sequence, against the oracle's teacher-forced decode of the same tokens (orc_decode_step over
+    every prompt position) for sequence 0 (all 2048 positions) and sequence 5 (first 512).
+
+    Bar: layer 0's K/V rows bit-exact; layer 1 no further from the oracle than the batch-1 decode
+    step of the same tokens (teacher-forced through the graph, seq 0): positions > 1e-3 at most
+    1.5x the decode's + 0.5 % of the positions, whole-layer rel-L2 at most 1.5x the decode's and
+    < 5e-3; the next-step logits of sequence 0 within 1e-3. Why not 1e-3 at every position: both
+    paths sum attention in fp32 (the oracle in double); where a layer-0 attention output lands
+    within an fp32 rounding of a bf16 boundary the two round apart, the int8 requantisation
+    downstream (attn_sub_norm, ffn_sub_norm) turns that into whole code steps, and that one
+    position's layer-1 K/V moves by ~1e-2 while its neighbours stay bit-exact. Measured at 2048
+    positions (tools/diag_prefill.py --n 2048 --oracle --trained --batch 1): batch-1 decode 32
+    positions, rel-L2 2.95e-3; prefill 41, 3.29e-3 (with P.V in two bf16 terms instead of three:
+    71, 4.28e-3)."""
     from wfamd.model import BitNetDecoder
     cfg = make_cfg(2, 128256, 2080)
     w = make_weights(cfg, seed=6, trained_like=True)
     B, n = 16, 2048
     dec = BitNetDecoder(cfg, w, batch=B)
+    one = BitNetDecoder(cfg, w, batch=1)
     a = oracle_arrays(cfg, w)
     del w
     rng = np.random.default_rng(12)
@@ -350,19 +361,32 @@ def test_prefill_8x2048_full_width_vs_oracle(orc):
         dec.tokens[b] = prompts[b][n]
         dec.positions[b] = n
     dec.step(graph=False)
+    for t in range(n):  # the batch-1 decode path, teacher-forced over seq 0's prompt
+        one.set_state([prompts[0][t]], [t])
+        one.step(graph=True)
     torch.cuda.synchronize()
+
+    def layer_err(model, b, l, npos, kr, vr):
+        kg, vg = logical_kv(model, l, b, npos)
+        kg, vg = orc.bf16_to_f32(bits(kg)), orc.bf16_to_f32(bits(vg))
+        per = np.array([max(rel_l2(kg[:, t], kr[:, t]), rel_l2(vg[:, t], vr[:, t])) for t in range(npos)])
+        return int((per > 1e-3).sum()), max(rel_l2(kg, kr), rel_l2(vg, vr)), per.max()
+
     for b, npos in ((0, n), (5, 512)):
         m = orc.DecodeModel(a)
         for t in range(npos):
             m.step(prompts[b][t], t, logits=False)
         for l in range(cfg.layers):
-            kg, vg = logical_kv(dec, l, b, npos)
-            kg, vg = orc.bf16_to_f32(bits(kg)), orc.bf16_to_f32(bits(vg))
             kr, vr = orc.bf16_to_f32(m.k_cache[l, :, :npos]), orc.bf16_to_f32(m.v_cache[l, :, :npos])
-            for c0 in range(0, npos, 256):
-                ek = rel_l2(kg[:, c0:c0 + 256], kr[:, c0:c0 + 256])
-                ev = rel_l2(vg[:, c0:c0 + 256], vr[:, c0:c0 + 256])
-                assert ek < 1e-3 and ev < 1e-3, (b, l, c0, ek, ev)
+            bad, whole, mx = layer_err(dec, b, l, npos, kr, vr)
+            print(f"prefill seq {b} layer {l}: {bad}/{npos} positions > 1e-3 (max {mx:.2e}), layer rel-L2 {whole:.2e}")
+            if l == 0:
+                assert bad == 0, (b, l, mx)
+            if b == 0:
+                dbad, dwhole, _ = layer_err(one, 0, l, npos, kr, vr)
+                print(f"  batch-1 decode seq 0 layer {l}: {dbad}/{npos} positions > 1e-3, layer rel-L2 {dwhole:.2e}")
+                assert bad <= 1.5 * dbad + 0.005 * npos and whole <= max(1.5 * dwhole, 1e-4), (l, bad, dbad, whole, dwhole)
+            assert bad <= 0.03 * npos and whole < 5e-3, (b, l, bad, whole)
         if b == 0:
             ologits, onext = m.step(prompts[0][n], n)
             err = rel_l2(orc.bf16_to_f32(bits(dec.logits[0])), orc.bf16_to_f32(ologits))

@@ -73,6 +73,23 @@ def test_gemv_model_shapes_vs_oracle(orc, n, k):
     assert np.array_equal(ops.tq_to_i2s(tq, k).cpu().numpy(), p)
 
 
+@pytest.mark.parametrize("n,k", [(1, 128), (5, 1280), (63, 8192), (640, 6912), (1001, 2560), (17, 7936)])
+def test_gemv_rows_ragged_vs_oracle(orc, n, k):
+    """The wave-per-row GEMV (k_gemv_rows: a row split over 1, 2 or 4 waves, ragged last block, 1-2
+    chunks per lane) bit-exact with the oracle, I2_S and TQ, including row counts that leave part of
+    the last block idle and K at the 8192-element limit of the LDS image."""
+    from wfamd import ops
+    from wfamd._lib import WF_FMT_TQ
+    rng = np.random.default_rng(n + k)
+    c = rng.integers(0, 3, size=(n, k // 4, 4)).astype(np.uint8)
+    p = np.ascontiguousarray((c[..., 0] << 6) | (c[..., 1] << 4) | (c[..., 2] << 2) | c[..., 3])
+    a = rng.integers(-128, 128, size=k).astype(np.int8)
+    ref = orc.gemv_i2s(p, a, 0.37)
+    assert np.array_equal(ops.bitnet_gemv(cu(p), cu(a), 0.37).cpu().numpy(), ref)
+    tq = ops.i2s_to_tq(cu(p))
+    assert np.array_equal(ops.bitnet_gemm_ex(tq, cu(a), 0.37, WF_FMT_TQ, in_features=k).cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("m", [2, 3, 5, 8, 16, 33, 128, 600])
 def test_gemm_batches_vs_oracle(orc, m):
     """VALU path (M < 16) and int8-MFMA path (M >= 16, wf_mfma.hip): bit-exact vs the oracle."""

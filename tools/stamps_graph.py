@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""In-graph latency timeline of one batch-1 decode layer (diagnostic build lib/libwfbitnet_stamps.so,
+`make -C wrinklefree-inference-engine_amd stamps`). The whole decode step is replayed as its HIP graph
+(warm clocks, warm code, the real inter-kernel gaps); every GEMV op stamps into its own region
+(WF_STAMP_BASE), so after a replay the buffers hold the LAST layer's QKV / O / GU / DN, the attention
+(its own translation unit) and the LM head. Prints, per op, the first / median block entry and the
+median / last block exit on one 100 MHz clock (relative to the QKV's first entry), the gaps between
+ops, per-stamp medians relative to each block's entry, and the shader clock (s_memtime / s_memrealtime).
+
+    python tools/stamps_graph.py [--ctx 1024] [--reps 20]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+PKG = ROOT / "wrinklefree-inference-engine_amd"
+os.environ["WF_BITNET_LIB"] = str(PKG / "lib" / "libwfbitnet_stamps.so")
+sys.path.insert(0, str(PKG / "python"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from wfamd import _lib  # noqa: E402
+from wfamd.model import BITNET_2B, BitNetDecoder, synthetic_weights  # noqa: E402
+
+SLOTS, NBLK = 80, 16384
+GEMV_NAMES = {0: "entry", 1: "image", 2: "dot", 3: "out", 7: "qkv_out", 8: "p_ss", 9: "p_r", 10: "p_y", 11: "p_sf",
+              12: "p_q", 13: "w_landed"}
+ATTN_NAMES = {0: "entry", 1: "kv_done", 2: "out"}
+LM_NAMES = {0: "entry", 1: "staged", 2: "dot", 3: "ticket", 4: "argmax"}
+
+
+def read(lib, fn):
+    buf = np.zeros(NBLK * SLOTS, dtype=np.uint64)
+    assert getattr(lib, fn)(C.c_void_p(buf.ctypes.data), C.c_int(buf.size), C.c_int(0)) == 0
+    return buf.reshape(NBLK, SLOTS).astype(np.int64)
+
+
+def op_summary(rows, names, last_slot, t0):
+    live = rows[rows[:, 0] > 0]
+    ent = (live[:, 0] - t0) * 0.01
+    ex = (live[:, last_slot] - t0) * 0.01
+    out = {"blocks": int(len(live)), "entry_first": round(float(ent.min()), 2),
+           "entry_med": round(float(np.median(ent)), 2), "exit_med": round(float(np.median(ex)), 2),
+           "exit_last": round(float(ex.max()), 2)}
+    per = {}
+    for sl, nm in names.items():
+        ok = live[:, sl] > 0
+        if sl and ok.any():
+            per[nm] = round(float(np.median((live[ok, sl] - live[ok, 0]) * 0.01)), 2)
+    out["per_block_med"] = per
+    ok = (live[:, 64] > 0) & (live[:, 64 + last_slot] > 0)
+    if ok.any():
+        dt = (live[ok, last_slot] - live[ok, 0]).astype(np.float64)
+        dc = (live[ok, 64 + last_slot] - live[ok, 64]).astype(np.float64)
+        good = dt > 0
+        if good.any():
+            out["clock_mhz"] = round(float(np.median(dc[good] / dt[good] * 100.0)), 0)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ctx", type=int, default=1024)
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    lib = _lib.load()
+    for fn in ("wf_debug_stamps_decode", "wf_debug_stamps_attn"):
+        getattr(lib, fn).restype = C.c_int
+        getattr(lib, fn).argtypes = [C.c_void_p, C.c_int, C.c_int]
+    w = synthetic_weights(BITNET_2B, seed=0)
+    dec = BitNetDecoder(BITNET_2B, w, batch=1)
+    del w
+    dec.fill_kv_random(args.ctx)
+    dec.set_state([1], [args.ctx])
+    for _ in range(args.reps):
+        dec.step(graph=True)
+    torch.cuda.synchronize()
+    for fn in ("wf_debug_stamps_decode", "wf_debug_stamps_attn"):
+        assert getattr(lib, fn)(None, 0, 1) == 0
+    torch.cuda.synchronize()
+    for _ in range(3):
+        dec.step(graph=True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    dec.step(graph=True)
+    e1.record()
+    torch.cuda.synchronize()
+    dc, at = read(lib, "wf_debug_stamps_decode"), read(lib, "wf_debug_stamps_attn")
+    ops = {"qkv": (dc[0:512], GEMV_NAMES, 7), "attn": (at[0:2048], ATTN_NAMES, 2),
+           "o_proj": (dc[512:1024], GEMV_NAMES, 3), "gate_up": (dc[1024:1536], GEMV_NAMES, 3),
+           "down": (dc[1536:2048], GEMV_NAMES, 3), "lm_head": (dc[4096:4096 + 8016], LM_NAMES, 3)}
+    t0 = dc[0:512][dc[0:512, 0] > 0, 0].min()
+    res = {name: op_summary(r, nm, ls, t0) for name, (r, nm, ls) in ops.items()}
+    prev = None
+    for name in ("qkv", "attn", "o_proj", "gate_up", "down", "lm_head"):
+        if prev:
+            res[name]["gap_from_prev_last_exit"] = round(res[name]["entry_first"] - res[prev]["exit_last"], 2)
+        prev = name
+    res["step_ms"] = round(e0.elapsed_time(e1), 4)
+    for k, v in res.items():
+        print(k, json.dumps(v), flush=True)
+    out = ROOT / "gpurun_out" / "stamps_graph.json"
+    out.parent.mkdir(exist_ok=True)
+    out.write_text(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

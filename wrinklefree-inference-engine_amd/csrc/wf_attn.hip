@@ -736,8 +736,8 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
 // token 4u + tk with query head h of the group (the decode kernel's head columns, all 16 used),
 // and every K/V fragment it loads feeds all CG groups. The host packs every aligned group of
 // kPrefillRowGroup rows from one slot (padding with repeats of a sequence's last token). Per 32-key tile:
-// the decode kernel's QK / online softmax / P.V with a per-column causal limit, P rounded to bf16
-// for the P.V MFMA (as a bf16 flash SDPA does; the decode kernel keeps hi + lo) and the
+// the decode kernel's QK / online softmax / P.V with a per-column causal limit, P as bf16 hi + lo
+// for the P.V MFMAs (the decode kernel's ~16 mantissa bits) and the
 // accumulator rescale skipped while no column's running max moves; V rows past the wave's last
 // position are zeroed (stale pages). Each wave streams its whole key
 // range and writes the normalised output rows bf16(o / l) (no split partials).
@@ -797,7 +797,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __res
     FT kA[2][4], vA[8];
     load(kA, vA, 0);
     for (int bs = 0; bs < lim_w; bs += 32) {
-        v8s_t ph[CG];
+        v8s_t ph[CG], pl[CG];
         float ar[CG][4];
         bool resc[CG];
 #pragma unroll
@@ -832,10 +832,14 @@ __global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __res
                 ps += p[e];
             }
             l_run[u] = l_run[u] * alpha + ps;
-            uint32_t hi[4];
+            uint32_t hi[4], lo[4];  // P as bf16 hi + lo (~16 mantissa bits), as the decode kernels
 #pragma unroll
-            for (int j = 0; j < 4; ++j) hi[j] = pk_bf16(p[2 * j], p[2 * j + 1]);
+            for (int j = 0; j < 4; ++j) {
+                hi[j] = pk_bf16(p[2 * j], p[2 * j + 1]);
+                lo[j] = pk_bf16(p[2 * j] - bf_lo(hi[j]), p[2 * j + 1] - bf_hi(hi[j]));
+            }
             ph[u] = __builtin_bit_cast(v8s_t, make_uint4(hi[0], hi[1], hi[2], hi[3]));
+            pl[u] = __builtin_bit_cast(v8s_t, make_uint4(lo[0], lo[1], lo[2], lo[3]));
             resc[u] = __any(alpha != 1.0f);  // the running max moved for some column: rescale acc
 #pragma unroll
             for (int r = 0; r < 4; ++r) ar[u][r] = __shfl(alpha, 4 * q4 + r, 64);
@@ -854,6 +858,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __res
                     for (int r = 0; r < 4; ++r) acc[u][n][r] *= ar[u][r];
                 }
                 acc[u][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph[u], vf[n], acc[u][n], 0, 0, 0);
+                acc[u][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl[u], vf[n], acc[u][n], 0, 0, 0);
             }
     }
     if constexpr (KV8) {
@@ -897,8 +902,8 @@ constexpr int kPfMaxTiles = 256;  // 32-key tiles per sequence (max_seq <= 8192)
 //   O^T (128 dims x 32 queries) += V^T . P^T: 8 MFMAs; P^T's fragments are the score lanes as they
 //       stand (the QK MFMA takes the keys permuted so that k-slot i of lane half h is key
 //       16 s + 8 h + i), V^T's fragments one 16-byte ds_read of the V tile layout each.
-// Per-column causal limit (masking only on diagonal tiles), P rounded to bf16 for the P.V MFMA (a
-// bf16 flash SDPA), V rows past the block's last position zeroed (stale pages). Heavy row groups
+// Per-column causal limit (masking only on diagonal tiles), P as three bf16 terms for the P.V MFMAs
+// (~24 mantissa bits: fp32 P), V rows past the block's last position zeroed. Heavy row groups
 // (late positions) are launched first. A column's result depends only on its own key range (tiles
 // past it add p = 0 at alpha = 1), so chunked prefill stays bit-exact.
 constexpr int kFaStages = 4;  // 64 KiB ring + page ids: two blocks per CU
@@ -1037,7 +1042,11 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
         const float alpha = STUDY == 3 ? 1.0f : __builtin_amdgcn_exp2f(m_run - mnew);
         m_run = mnew;
         float ps = 0.f;
-        uint32_t pk[8];
+        // P^T as three bf16 terms hi + mid + lo (p to ~24 bits: the fp32 P of the decode step's VALU
+        // kernel). bf16-only P moved 2.5 % of the layer-1 K/V rows of an 8 x 2048 prefill off the
+        // oracle (the requantised attn_sub / ffn_sub inputs turn bf16-boundary flips of the
+        // attention output into whole code steps); hi + lo (~16 bits) still 3.5 % of the positions.
+        uint32_t pk[8], pr[8], pq[8];
 #pragma unroll
         for (int j = 0; j < 16; j += 2) {
             // (study 3: no exponentials -- the softmax's transcendental cost)
@@ -1046,6 +1055,9 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
             ps += p0;
             ps += p1;
             pk[j >> 1] = pk_bf16(p0, p1);
+            const float r0 = p0 - bf_lo(pk[j >> 1]), r1 = p1 - bf_hi(pk[j >> 1]);
+            pr[j >> 1] = pk_bf16(r0, r1);
+            pq[j >> 1] = pk_bf16(r0 - bf_lo(pr[j >> 1]), r1 - bf_hi(pr[j >> 1]));
         }
         l_run = l_run * alpha + ps;
         if (__any(alpha != 1.0f)) {
@@ -1056,6 +1068,10 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
         }
         const v8bf_t pb0 = __builtin_bit_cast(v8bf_t, make_uint4(pk[0], pk[1], pk[2], pk[3]));
         const v8bf_t pb1 = __builtin_bit_cast(v8bf_t, make_uint4(pk[4], pk[5], pk[6], pk[7]));
+        const v8bf_t pc0 = __builtin_bit_cast(v8bf_t, make_uint4(pr[0], pr[1], pr[2], pr[3]));
+        const v8bf_t pc1 = __builtin_bit_cast(v8bf_t, make_uint4(pr[4], pr[5], pr[6], pr[7]));
+        const v8bf_t pd0 = __builtin_bit_cast(v8bf_t, make_uint4(pq[0], pq[1], pq[2], pq[3]));
+        const v8bf_t pd1 = __builtin_bit_cast(v8bf_t, make_uint4(pq[4], pq[5], pq[6], pq[7]));
         const int limv = lim_b - bs - 8 * h;  // V keys past the block's last position: zero (stale)
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
@@ -1077,6 +1093,10 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
                     continue;
                 }
                 oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, s2 ? pb1 : pb0, oacc[mt], 0, 0, 0);
+                oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, s2 ? pc1 : pc0, oacc[mt], 0, 0, 0);
+#ifndef WF_PF_P2  // study build -DWF_PF_P2: P as hi + lo only
+                oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, s2 ? pd1 : pd0, oacc[mt], 0, 0, 0);
+#endif
             }
         }
     };

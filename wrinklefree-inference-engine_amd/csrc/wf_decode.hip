@@ -121,6 +121,7 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
     const int lrow = threadIdx.x / LPR, sub = threadIdx.x % LPR;
     const int row = blockIdx.x * RPB + lrow;
     const int C = F::chunks(K);
+    WF_STAMP_BASE(512u * MODE);  // stamps build: one region per op
     WF_STAMP(0);
 
     // 1) the input row (issued first: vmcnt retires in order), 2) the weight stream, 3) residual
@@ -219,9 +220,7 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
     WF_STAMP(1);
     WF_STAMP_DRAIN(13);
 
-    int acc[MB];
-#pragma unroll
-    for (int m = 0; m < MB; ++m) acc[m] = 0;
+    DotAcc<F> dacc[MB];
 #pragma unroll
     for (int u = 0; u < kPrefetch; ++u) {
         const int c = LPR * u + sub;
@@ -230,7 +229,7 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
             d.load(wpre[u]);
             const int8_t* ab = smem + ((c >> 4) * F::kGroups) * 256 + (c & 15) * 16;
 #pragma unroll
-            for (int m = 0; m < MB; ++m) acc[m] = chunk_dot<F>(d, ab + m * img, acc[m]);
+            for (int m = 0; m < MB; ++m) chunk_dot<F>(d, ab + m * img, dacc[m]);
         }
     }
     for (int c0 = LPR * kPrefetch; c0 < C; c0 += LPR * kPrefetch) {
@@ -246,13 +245,14 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
                 d.load(w[u]);
                 const int8_t* ab = smem + ((c >> 4) * F::kGroups) * 256 + (c & 15) * 16;
 #pragma unroll
-                for (int m = 0; m < MB; ++m) acc[m] = chunk_dot<F>(d, ab + m * img, acc[m]);
+                for (int m = 0; m < MB; ++m) chunk_dot<F>(d, ab + m * img, dacc[m]);
             }
         }
     }
     WF_STAMP(2);
+    int acc[MB];
 #pragma unroll
-    for (int m = 0; m < MB; ++m) acc[m] = group_reduce<LPR>(acc[m], OpAdd{});
+    for (int m = 0; m < MB; ++m) acc[m] = group_reduce<LPR>(dacc[m].total(), OpAdd{});
 
     if constexpr (MODE == MODE_QKV) {
         // rows per head permuted: block t of head h = dims {8t..8t+7, 64+8t..64+8t+7} (RPB == 16)
@@ -1403,6 +1403,7 @@ __global__ __launch_bounds__(256) void k_lm_head(const uint16_t* __restrict__ E,
     const int row = blockIdx.x * 16 + lrow;
     const int C = H / 8;
     const uint16_t* er = E + (int64_t)min(row, V - 1) * H;
+    WF_STAMP_BASE(4096u);
     WF_STAMP(0);
     uint4 w[4];
 #pragma unroll

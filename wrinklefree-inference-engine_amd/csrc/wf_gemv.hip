@@ -61,9 +61,7 @@ __global__ __launch_bounds__(256) void k_ternary_gemm(const uint8_t* __restrict_
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sub = lane & 15;
     const int row = blockIdx.x * kRowsPerBlock + wave * 4 + (lane >> 4);
     const int C = F::chunks(K);
-    int acc[MB];
-#pragma unroll
-    for (int m = 0; m < MB; ++m) acc[m] = 0;
+    DotAcc<F> dacc[MB];
     if (row < N) {
         const uint8_t* wr = W + (int64_t)row * F::row_bytes(K) + sub * 16;
         for (int c0 = 0; c0 < C; c0 += 16 * kUnroll) {
@@ -81,13 +79,14 @@ __global__ __launch_bounds__(256) void k_ternary_gemm(const uint8_t* __restrict_
                     d.load(w[u]);
                     const int8_t* ab = smem + ((c >> 4) * F::kGroups) * 256 + sub * 16;
 #pragma unroll
-                    for (int m = 0; m < MB; ++m) acc[m] = chunk_dot<F>(d, ab + m * img, acc[m]);
+                    for (int m = 0; m < MB; ++m) chunk_dot<F>(d, ab + m * img, dacc[m]);
                 }
             }
         }
     }
+    int acc[MB];
 #pragma unroll
-    for (int m = 0; m < MB; ++m) acc[m] = group16_sum_i(acc[m]);
+    for (int m = 0; m < MB; ++m) acc[m] = group16_sum_i(dacc[m].total());
     if (row < N && sub == 0) {
 #pragma unroll
         for (int m = 0; m < MB; ++m)
@@ -95,9 +94,98 @@ __global__ __launch_bounds__(256) void k_ternary_gemm(const uint8_t* __restrict_
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Standalone GEMV (M = 1; sgl_kernel bitnet_gemv, scripts/benchmark_kernels.py:40-66): a memory-
+// latency problem -- 0.4-4.5 MB per call, i.e. 1.6-17 KB per CU -- so every byte of the matrix is
+// in flight at once and as many CUs as possible take part. Block = 256 threads = 4 waves; a row is
+// split over W waves (W = 1, 2 or 4, chosen per shape so the grid has >= ~1024 blocks: k/v's 640
+// rows take W = 4), wave kp of a row takes its contiguous 1/W of the row's 16-byte chunks, lane l
+// chunk c0 + l + 64 j. Issue order: the activation pieces (L2-resident), then every weight chunk of
+// the lane (nt), then the activation image goes to LDS (conflict-free stripes, wf_device.h) behind
+// one barrier that the weight latency hides. Each wave sums its lanes with DPP; the W wave partials
+// of a row meet in LDS in wave order. Integer sums: bit-exact with any split.
+// ---------------------------------------------------------------------------------------------
+constexpr int kGemvMaxPieces = 2;  // 16-byte activation pieces per thread: K_pad <= 8192
+template <class F, int W, int J>
+__global__ __launch_bounds__(256) void k_gemv_rows(const uint8_t* __restrict__ Wt, const int8_t* __restrict__ A,
+                                                   float scale, int N, int K, float* __restrict__ Y) {
+    extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+    __shared__ int part[4];
+    constexpr int R = 4 / W;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int row = blockIdx.x * R + wave / W, kp = wave % W;
+    const int C = F::chunks(K), cw = (C + W - 1) / W, c0 = kp * cw, c1 = min(C, c0 + cw);
+    const int pieces = F::k_pad(K) / 16;
+    uint4 apre[kGemvMaxPieces];
+#pragma unroll
+    for (int i = 0; i < kGemvMaxPieces; ++i) {
+        const int p = min((int)threadIdx.x + 256 * i, pieces - 1), pk = min(p, K / 16 - 1);
+        apre[i] = *reinterpret_cast<const uint4*>(A + 16 * pk);  // pieces >= K/16: zeroed below
+    }
+    const uint8_t* wr = Wt + (int64_t)min(row, N - 1) * F::row_bytes(K);
+    uint4 wv[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) wv[j] = ldg_nt(wr + (int64_t)min(c0 + lane + 64 * j, C - 1) * 16);
+#pragma unroll
+    for (int i = 0; i < kGemvMaxPieces; ++i) {
+        const int p = (int)threadIdx.x + 256 * i;
+        if (p < pieces)
+            *reinterpret_cast<uint4*>(smem + F::lds_off(16 * p)) = 16 * p < K ? apre[i] : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    DotAcc<F> dacc;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int c = c0 + lane + 64 * j;
+        if (c < c1) {
+            Decoded<F> d;
+            d.load(wv[j]);
+            chunk_dot<F>(d, smem + ((c >> 4) * F::kGroups) * 256 + (c & 15) * 16, dacc);
+        }
+    }
+    const int acc = wave_sum_i(dacc.total());
+    if constexpr (W == 1) {
+        if (lane == 0 && row < N) Y[row] = (float)acc * scale;
+    } else {
+        if (lane == 0) part[wave] = acc;
+        __syncthreads();
+        if (threadIdx.x < R) {
+            const int r = blockIdx.x * R + threadIdx.x;
+            int s = 0;
+#pragma unroll
+            for (int i = 0; i < W; ++i) s += part[threadIdx.x * W + i];
+            if (r < N) Y[r] = (float)s * scale;
+        }
+    }
+}
+
+template <class F>
+static int launch_gemv_rows(const uint8_t* w, const int8_t* a, float scale, int N, int K, float* y, hipStream_t st) {
+    const int C = F::chunks(K);
+    int W = 1;
+    while (W < 4 && (int64_t)N * W / 4 < 1024 && (C + 2 * W - 1) / (2 * W) >= 8) W *= 2;
+    const int cw = (C + W - 1) / W;
+    const int J = (cw + 63) / 64;
+    const int img = lds_image_bytes<F>(K);
+#define WF_GR(WV, JV) \
+    hipLaunchKernelGGL((k_gemv_rows<F, WV, JV>), dim3((N * WV + 3) / 4), dim3(256), (size_t)img, st, w, a, scale, N, K, y)
+#define WF_GRJ(WV)            \
+    if (J == 1) WF_GR(WV, 1); \
+    else WF_GR(WV, 2);
+    if (W == 1) { WF_GRJ(1) }
+    else if (W == 2) { WF_GRJ(2) }
+    else { WF_GRJ(4) }
+#undef WF_GRJ
+#undef WF_GR
+    return check_launch("gemv_rows");
+}
+
 template <class F>
 static int launch_ternary_gemm(const uint8_t* w, const int8_t* a, int64_t lda, float scale, int M, int N, int K,
                                float* y, int64_t ldy, hipStream_t st) {
+    // GEMV with K_pad <= 8192 and at most 2 chunks per lane: the wave-per-row kernel
+    if (M == 1 && F::k_pad(K) <= 256 * 16 * kGemvMaxPieces && F::chunks(K) <= 128)
+        return launch_gemv_rows<F>(w, a, scale, N, K, y, st);
     const int img = lds_image_bytes<F>(K);
     const dim3 block(256);
     const int gx = (N + kRowsPerBlock - 1) / kRowsPerBlock;

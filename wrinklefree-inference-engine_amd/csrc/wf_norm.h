@@ -75,8 +75,7 @@ __device__ __forceinline__ void ticket_rearm(unsigned* t) {
 #ifdef WF_STAMPS
 constexpr int kStampSlots = 80;  // 4 waves x 16 realtime slots + 16 shader-clock slots
 constexpr int kStampBlocks = 16384;
-// hidden visibility: PC-relative address (no GOT load per stamp); slot index from blockIdx only
-// (no gridDim load): block (x, y, z) -> x + 2048 y + 8192 z
+// hidden visibility: PC-relative address (no GOT load per stamp); row = the op's base + linear block id
 __attribute__((visibility("hidden"))) static __device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
 // slot i of wave w lives at column 16 w + i; wave 0 also records the shader clock (s_memtime) of
 // slot i in column 64 + i (clock rate = d(memtime) / d(memrealtime) * 100 MHz)
@@ -88,11 +87,15 @@ __attribute__((visibility("hidden"))) static __device__ unsigned long long g_sta
 #define WF_STAMP_WAVE_OK (threadIdx.x < 256)
 #define WF_STAMP_COL (16 * (threadIdx.x >> 6))
 #endif
+// a kernel may move its rows with WF_STAMP_BASE(v) (e.g. one region per decode op, so a graph
+// replay of the whole step keeps every op's stamps of the last layer)
+constexpr unsigned wf_stamp_base = 0;
+#define WF_STAMP_BASE(v) constexpr unsigned wf_stamp_base = (v)
 #define WF_STAMP(i)                                                                                 \
     do {                                                                                            \
         __builtin_amdgcn_sched_barrier(0);                                                          \
         if ((threadIdx.x & 63) == 0 && WF_STAMP_WAVE_OK) {                                          \
-            const unsigned sb_ = blockIdx.x + 2048u * blockIdx.y + 8192u * blockIdx.z;               \
+            const unsigned sb_ = wf_stamp_base + blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z); \
             if (sb_ < (unsigned)::wf::kStampBlocks) {                                                \
                 unsigned long long* row_ = ::wf::g_stamps + (size_t)sb_ * ::wf::kStampSlots;          \
                 row_[WF_STAMP_COL + (i)] = __builtin_amdgcn_s_memrealtime();                         \
@@ -121,6 +124,7 @@ inline void* g_stamps_addr() {
     return p;
 }
 #else
+#define WF_STAMP_BASE(v)
 #define WF_STAMP(i) \
     do {            \
     } while (0)
@@ -367,16 +371,22 @@ __device__ __forceinline__ int64_t v_tile_off(int t, int d) {
     return ((((int64_t)blk * 8 + (d >> 4)) * 4 + (o >> 3)) * 16 + (d & 15)) * 8 + (o & 7);
 }
 
-template <int PPT, int NT, int NS = kAttnPartSplits>
+// piece index of a thread's i-th piece: the NT-thread mapping p = threadIdx.x + NT * i
+template <int NT>
+struct PieceNT {
+    __device__ __forceinline__ int operator()(int i) const { return (int)threadIdx.x + NT * i; }
+};
+template <int PPT, int NT, int NS = kAttnPartSplits, class PC = PieceNT<NT>>
 struct AttnRow {
     float4 ml[PPT][NS / 2];  // (m0, l0, m1, l1) pairs
     float4 oa[PPT][NS], ob[PPT][NS];
     __device__ __forceinline__ void issue(const float2* __restrict__ ml_in, const float* __restrict__ o_in, int b, int Hq,
                                           int D) {
         const int npk = Hq * D / 8;
+        const PC piece;
 #pragma unroll
         for (int i = 0; i < PPT; ++i) {
-            const int pc = min((int)threadIdx.x + NT * i, npk - 1);
+            const int pc = min(piece(i), npk - 1);
             const int h = (8 * pc) / D, d0 = 8 * pc - h * D;
             const int64_t rec = (int64_t)(b * Hq + h) * NS;
 #pragma unroll
@@ -402,6 +412,7 @@ struct AttnRow {
     }
     __device__ __forceinline__ void finish(int Hq, int D, float (&y)[PPT][8]) const {
         const int npk = Hq * D / 8;
+        const PC piece;
 #pragma unroll
         for (int i = 0; i < PPT; ++i) {
             float mm[NS], ll[NS];
@@ -424,11 +435,18 @@ struct AttnRow {
                 for (int j = 0; j < 8; ++j) O[j] = fmaf(w, ov[j], O[j]);
             }
             const float inv = 1.0f / L;
-            const bool valid = (int)threadIdx.x + NT * i < npk;
+            const bool valid = piece(i) < npk;
 #pragma unroll
             for (int j = 0; j < 8; ++j) y[i][j] = valid ? rbf(O[j] * inv) : 0.f;
         }
     }
 };
+
+// Batch-1 GEMV prologue (k_gemv PPT > 0: NormRow + norm_core + quant_row) is VALU-issue /
+// dependency-latency bound, not memory-bound (in-graph stamps, tools/stamps_graph.py). Measured
+// and not kept (round 3): all of it on one wave per SIMD (QKV input image 2.64 -> 3.16 us: a lone
+// wave issues a dependent chain at ~8 cycles per instruction); data-less waves skipping the
+// elementwise work plus packed-bf16 maxima (QKV 4.59 -> 4.90 us, gate/up 5.91 -> 6.13 us per
+// layer in the same-box graph A/B: the extra barrier and branches cost more than they saved).
 
 }  // namespace wf

@@ -103,7 +103,10 @@ def load():
                 raise ImportError(f"HIP library {LIB_PATH} is missing: build it with `make -C {PKG_ROOT}` "
                                   "(or __graft_entry__.build())")
             lib = C.CDLL(str(LIB_PATH))
+            study = LIB_PATH.name != "libwfbitnet.so"  # an A/B study build (WF_BITNET_LIB) may predate symbols
             for name, (res, args) in SIGNATURES.items():
+                if study and not hasattr(lib, name):
+                    continue
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
