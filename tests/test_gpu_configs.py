@@ -295,8 +295,10 @@ def test_fp8_kv_attention_cosine_reference_bar(orc, ctx):
     normal K/V and query; its FP8 row reports min 0.9985 over 20 runs, docs/research/notebook.md:
     690-700) on the step's own kernels: the same q and history (FP8 = e4m3 codes of the bf16 values,
     scale 1) through k_attn_mfma bf16 and FP8 for 16 sequences at context `ctx`, q projection
-    scale 0.024 so q ~ N(0, 1) per element like the reference's randn query. Bar: min over the
-    sequences >= 0.998 (the per-head minimum is printed, not asserted)."""
+    scale set so the q the kernels see has unit standard deviation like the reference's randn query
+    (measured on a first bf16 pass: e4m3's attention error grows with the score spread, ~0.9992 at
+    q ~ N(0, 1) and ~0.997 at 2.5x that at any context, numpy restatement). Bar: min over the
+    sequences >= 0.998 (the reference's own code asserts > 0.99; per-head minimum printed)."""
     from wfamd import _lib
     from wfamd.model import BitNetDecoder
     cfg = make_cfg(1, 1024, 4096)
@@ -306,16 +308,24 @@ def test_fp8_kv_attention_cosine_reference_bar(orc, ctx):
     gen = torch.Generator(device="cuda").manual_seed(ctx)
     k = torch.randn(B, cfg.n_kv_heads, ctx - 1, 128, generator=gen, device="cuda").to(torch.bfloat16)
     v = torch.randn(B, cfg.n_kv_heads, ctx - 1, 128, generator=gen, device="cuda").to(torch.bfloat16)
-    outs = []
-    for kvd in ("bf16", "fp8"):
+
+    def run(kvd):
         dec = BitNetDecoder(cfg, w, batch=B, kv_dtype=kvd)
         dec.load_kv(0, k, v)
         dec.set_state([(13 * b + 1) % cfg.vocab for b in range(B)], [ctx - 1] * B)
         for op in (_lib.WF_OP_EMBED, _lib.WF_OP_QKV, _lib.WF_OP_ATTN):
             dec.launch_op(0, op)
         torch.cuda.synchronize()
-        outs.append(merge_records(*dec.attention_records()[1:]))
-        del dec
+        q, ml, o = dec.attention_records()
+        return float(q.float().std()), merge_records(ml, o)
+
+    q_std, _ = run("bf16")
+    w["wscale"][:, 0] = 0.024 / q_std
+    q_std1, ref = run("bf16")
+    _, got = run("fp8")
+    outs = [ref, got]
+    print(f"q std {q_std:.3f} at scale 0.024 -> {q_std1:.3f}")
+    assert abs(q_std1 - 1.0) < 0.05, q_std1
 
     def cos(a, b):
         return (a * b).sum(-1) / np.linalg.norm(a, axis=-1) / np.linalg.norm(b, axis=-1)

@@ -7,7 +7,10 @@
 median / last block exit on one 100 MHz clock (relative to the QKV's first entry), the gaps between
 ops, per-stamp medians relative to each block's entry, and the shader clock (s_memtime / s_memrealtime).
 
-    python tools/stamps_graph.py [--ctx 1024] [--reps 20]
+    python tools/stamps_graph.py [--ctx 1024] [--reps 20] [--batch 128]
+
+At batch > 1 the ops are the row norms (k_rownorm: ln_in and ln_post share a region, so the
+ln_post one is shown; k_rownorm_attn), the k_dec_gemm_t GEMMs and k_attn_mfma.
 """
 import argparse
 import ctypes as C
@@ -32,6 +35,8 @@ GEMV_NAMES = {0: "entry", 1: "image", 2: "dot", 3: "out", 7: "qkv_out", 8: "p_ss
               12: "p_q", 13: "w_landed"}
 ATTN_NAMES = {0: "entry", 1: "kv_done", 2: "out"}
 LM_NAMES = {0: "entry", 1: "staged", 2: "dot", 3: "ticket", 4: "argmax"}
+GEMM_NAMES = {0: "entry", 1: "issued", 2: "first_mma", 3: "mma_done", 4: "combined", 5: "epilogue"}
+RN_NAMES = {0: "entry", 1: "normed", 2: "done"}
 
 
 def read(lib, fn):
@@ -67,16 +72,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ctx", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=1)
     args = ap.parse_args()
     lib = _lib.load()
     for fn in ("wf_debug_stamps_decode", "wf_debug_stamps_attn"):
         getattr(lib, fn).restype = C.c_int
         getattr(lib, fn).argtypes = [C.c_void_p, C.c_int, C.c_int]
     w = synthetic_weights(BITNET_2B, seed=0)
-    dec = BitNetDecoder(BITNET_2B, w, batch=1)
+    B = args.batch
+    dec = BitNetDecoder(BITNET_2B, w, batch=B)
     del w
     dec.fill_kv_random(args.ctx)
-    dec.set_state([1], [args.ctx])
+    dec.set_state([1 + b for b in range(B)], [args.ctx] * B)
     for _ in range(args.reps):
         dec.step(graph=True)
     torch.cuda.synchronize()
@@ -91,20 +98,28 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     dc, at = read(lib, "wf_debug_stamps_decode"), read(lib, "wf_debug_stamps_attn")
-    ops = {"qkv": (dc[0:512], GEMV_NAMES, 7), "attn": (at[0:2048], ATTN_NAMES, 2),
-           "o_proj": (dc[512:1024], GEMV_NAMES, 3), "gate_up": (dc[1024:1536], GEMV_NAMES, 3),
-           "down": (dc[1536:2048], GEMV_NAMES, 3), "lm_head": (dc[4096:4096 + 8016], LM_NAMES, 3)}
+    if B == 1:
+        order = ("qkv", "attn", "o_proj", "gate_up", "down", "lm_head")
+        ops = {"qkv": (dc[0:512], GEMV_NAMES, 7), "attn": (at[0:2048], ATTN_NAMES, 2),
+               "o_proj": (dc[512:1024], GEMV_NAMES, 3), "gate_up": (dc[1024:1536], GEMV_NAMES, 3),
+               "down": (dc[1536:2048], GEMV_NAMES, 3), "lm_head": (dc[4096:4096 + 8016], LM_NAMES, 3)}
+    else:
+        order = ("qkv", "attn", "rn_attn", "o_proj", "rn_post", "gate_up", "rn_ffn", "down")
+        ops = {"qkv": (dc[0:512], GEMM_NAMES, 5), "attn": (at[0:16384], ATTN_NAMES, 2),
+               "rn_attn": (dc[2560:2560 + B], RN_NAMES, 2), "o_proj": (dc[512:1024], GEMM_NAMES, 5),
+               "rn_post": (dc[2048:2048 + B], RN_NAMES, 2), "gate_up": (dc[1024:1536], GEMM_NAMES, 5),
+               "rn_ffn": (dc[2304:2304 + B], RN_NAMES, 2), "down": (dc[1536:2048], GEMM_NAMES, 5)}
     t0 = dc[0:512][dc[0:512, 0] > 0, 0].min()
     res = {name: op_summary(r, nm, ls, t0) for name, (r, nm, ls) in ops.items()}
     prev = None
-    for name in ("qkv", "attn", "o_proj", "gate_up", "down", "lm_head"):
+    for name in order:
         if prev:
             res[name]["gap_from_prev_last_exit"] = round(res[name]["entry_first"] - res[prev]["exit_last"], 2)
         prev = name
     res["step_ms"] = round(e0.elapsed_time(e1), 4)
     for k, v in res.items():
         print(k, json.dumps(v), flush=True)
-    out = ROOT / "gpurun_out" / "stamps_graph.json"
+    out = ROOT / "gpurun_out" / f"stamps_graph_b{B}.json"
     out.parent.mkdir(exist_ok=True)
     out.write_text(json.dumps(res, indent=1))
 

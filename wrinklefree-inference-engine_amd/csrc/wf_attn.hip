@@ -1045,7 +1045,9 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
         // P^T as three bf16 terms hi + mid + lo (p to ~24 bits: the fp32 P of the decode step's VALU
         // kernel). bf16-only P moved 2.5 % of the layer-1 K/V rows of an 8 x 2048 prefill off the
         // oracle (the requantised attn_sub / ffn_sub inputs turn bf16-boundary flips of the
-        // attention output into whole code steps); hi + lo (~16 bits) still 3.5 % of the positions.
+        // attention output into whole code steps). At 2048 positions, layer 1 vs the oracle: hi + lo
+        // 71 positions > 1e-3 (rel-L2 4.28e-3), hi + mid + lo 41 (3.29e-3; the batch-1 decode path
+        // itself 32, 2.95e-3) for +2 % prefill time (51.0 -> 52.0 ms).
         uint32_t pk[8], pr[8], pq[8];
 #pragma unroll
         for (int j = 0; j < 16; j += 2) {
@@ -1094,9 +1096,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
                 }
                 oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, s2 ? pb1 : pb0, oacc[mt], 0, 0, 0);
                 oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, s2 ? pc1 : pc0, oacc[mt], 0, 0, 0);
-#ifndef WF_PF_P2  // study build -DWF_PF_P2: P as hi + lo only
                 oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, s2 ? pd1 : pd0, oacc[mt], 0, 0, 0);
-#endif
             }
         }
     };

@@ -678,6 +678,7 @@ __global__ __launch_bounds__(NW * 64) void k_dec_gemm_t(GemvArgs a) {
         }
     };
     const int cnt = (nkb - wave + NW - 1) / NW;
+    WF_STAMP_BASE(512u * MODE);  // stamps build: one region per op (batch > 1; k_gemv's at batch 1)
     WF_STAMP(0);
     EpiDec<MODE> e{&a};
     int er0[EPT], ec0[EPT];
@@ -1225,6 +1226,9 @@ __global__ __launch_bounds__(kNT) void k_rownorm(const uint16_t* __restrict__ x,
     __shared__ float red[2 * kNT / 64];
     __shared__ int red_i[kNT / 64];
     const int b = blockIdx.x;
+    // stamps build: ln_in / ln_post share a region (the later one stays), ffn_sub and final apart
+    WF_STAMP_BASE(Y16 ? 3072u : (PPT == 1 ? 2048u : 2304u));
+    WF_STAMP(0);
     NormRow<PPT, kNT> nr;
     nr.issue(x + (int64_t)b * xs, nw, K);
     float y[PPT][8];
@@ -1240,6 +1244,7 @@ __global__ __launch_bounds__(kNT) void k_rownorm(const uint16_t* __restrict__ x,
         }
     } else {
         const float s = norm_row(nr, K, eps, y, red);
+        WF_STAMP(1);
         int as;
         if constexpr (TL) as = quant_row_tiled<PPT, kNT>(y, s, K / 8, q8, b, K >> 7);
         else as = quant_row<PPT, kNT>(y, s, K / 8, q8 + (int64_t)b * q8s, [](int p) { return 8 * p; });
@@ -1252,6 +1257,7 @@ __global__ __launch_bounds__(kNT) void k_rownorm(const uint16_t* __restrict__ x,
             asum[b] = t;
             sf[b] = s;
         }
+        WF_STAMP(2);
     }
 }
 
@@ -1362,6 +1368,8 @@ __global__ __launch_bounds__(kNT) void k_rownorm_attn(const float2* __restrict__
     __shared__ float red[2 * kNT / 64];
     __shared__ int red_i[kNT / 64];
     const int b = blockIdx.x, K = Hq * 128;
+    WF_STAMP_BASE(2560u);
+    WF_STAMP(0);
     AttnRow<PPT, kNT, NS> ar;
     ar.issue(ml, o, b, Hq, 128);
     NormRow<PPT, kNT> nr;
@@ -1369,6 +1377,7 @@ __global__ __launch_bounds__(kNT) void k_rownorm_attn(const float2* __restrict__
     float y[PPT][8];
     ar.finish(Hq, 128, y);
     const float s = norm_core(nr, K, eps, y, red);
+    WF_STAMP(1);
     int as;
     if constexpr (TL) as = quant_row_tiled<PPT, kNT>(y, s, K / 8, q8, b, K >> 7);
     else as = quant_row<PPT, kNT>(y, s, K / 8, q8 + (int64_t)b * q8s, [](int p) { return 8 * p; });
@@ -1381,6 +1390,7 @@ __global__ __launch_bounds__(kNT) void k_rownorm_attn(const float2* __restrict__
         asum[b] = t;
         sf[b] = s;
     }
+    WF_STAMP(2);
 }
 
 // logits[b, v] = bf16(sum_k hn[b,k] * E[v,k]) (F.linear, fp32 accumulation); 16 lanes per vocab

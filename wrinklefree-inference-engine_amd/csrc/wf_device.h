@@ -295,12 +295,12 @@ struct DotAcc<FmtTQ> {
     __device__ __forceinline__ DotAcc() : s{0} {}
     __device__ __forceinline__ int total() const { return s[0]; }
 };
-#ifndef WF_DOT_V0
 // I2S, the GEMV form: the 2-bit field of group g is masked in place (d & 0x30303030 = 16 x code,
 // d & 0x0c0c0c0c = 4 x code, d & 0x03030303 = code; group 0's top field is shifted once, 32 x code
 // <= 64 stays a positive int8), 5 VALU per dword instead of 7 for shift + mask per group; each group
 // accumulates on its own (four independent dot4 chains per chunk instead of one of 16) and its scale
-// is divided out once at the end (DotAcc::total, exact).
+// is divided out once at the end (DotAcc::total, exact). Same-box graph A/B against the round-2
+// decode (shift + mask per group, one accumulator): equal batch-1 step time (1045 vs 1040 tok/s).
 template <>
 struct Decoded<FmtI2S> {
     uint32_t e[4][4];
@@ -321,19 +321,6 @@ struct DotAcc<FmtI2S> {
     __device__ __forceinline__ DotAcc() : s{0, 0, 0, 0} {}
     __device__ __forceinline__ int total() const { return s[3] + (s[2] >> 2) + (s[1] >> 4) + (s[0] >> 5); }
 };
-#else  // study build -DWF_DOT_V0: the round-2 decode (shift + mask per group, one accumulator)
-template <>
-struct Decoded<FmtI2S> {
-    uint32_t e[4][4];
-    __device__ __forceinline__ void load(const uint4 w) { decode_i2s(w, e); }
-};
-template <>
-struct DotAcc<FmtI2S> {
-    int s[1];
-    __device__ __forceinline__ DotAcc() : s{0} {}
-    __device__ __forceinline__ int total() const { return s[0]; }
-};
-#endif
 
 // sum_g,t dot4(e[g][t], act[g][t]) with act read from the LDS image at stripe base `abase`
 // (abase = image + (i*G)*256 + sub*16; group g adds g*256).
@@ -342,7 +329,7 @@ __device__ __forceinline__ void chunk_dot(const Decoded<F>& dw, const int8_t* ab
 #pragma unroll
     for (int g = 0; g < F::kGroups; ++g) {
         const uint4 a = *reinterpret_cast<const uint4*>(abase + g * 256);
-        int& r = acc.s[(__is_same(F, FmtI2S) && sizeof(acc.s) == 4 * sizeof(int)) ? g : 0];
+        int& r = acc.s[__is_same(F, FmtI2S) ? g : 0];
         r = sdot4(dw.e[g][0], a.x, r);
         r = sdot4(dw.e[g][1], a.y, r);
         r = sdot4(dw.e[g][2], a.z, r);
