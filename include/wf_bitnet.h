@@ -234,6 +234,11 @@ typedef struct {
     int records;
 } wf_attn_records;
 int wf_model_attn_view(const wf_model* m, wf_attn_records* out);
+/* Which batched GEMM ops (flags[0..3] = QKV, O, gate|up, down) run their input row norm inside the
+ * GEMM launch instead of a separate row-norm launch (batch >= 16 on WF_FMT_I2S_MFMA weights, when
+ * the whole grid fits the device at once; decided at wf_model_create). Diagnostic / bench query:
+ * the step's results do not depend on it. */
+int wf_model_fused_norm(const wf_model* m, int* flags4);
 /* Prefill (BASELINE configs[2]; the prompt pass that precedes scripts/direct_inference_full.py's
  * decode loop): run prompt tokens of any KV slots through all layers as GEMM rows and write their
  * K/V into the cache (dense planes or pages). Batched matrix-core decoders only (batch >= 16, I2_S

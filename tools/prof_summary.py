@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 --kernel-trace output (rocpd SQLite .db or kernel_trace.csv) per kernel:
-calls, total/avg/min/max duration in microseconds, sorted by total time."""
+calls, total/avg/median/min/max duration in microseconds, sorted by total time."""
 import csv
 import glob
 import sqlite3
@@ -35,7 +35,8 @@ def summarize(rows):
     tot = sum(sum(v) for v in agg.values())
     lines = []
     for n, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
-        lines.append((n, len(v), sum(v), sum(v) / len(v), min(v), max(v), 100.0 * sum(v) / tot))
+        v = sorted(v)
+        lines.append((n, len(v), sum(v), sum(v) / len(v), v[len(v) // 2], min(v), max(v), 100.0 * sum(v) / tot))
     return lines
 
 
@@ -48,10 +49,10 @@ def main():
     else:
         cands = glob.glob(f"{path}/**/*kernel_trace.csv", recursive=True) or glob.glob(f"{path}/**/*.db", recursive=True)
         rows = from_csv(cands[0]) if cands[0].endswith(".csv") else from_db(cands[0])
-    print(f"{'calls':>7} {'total_us':>12} {'avg_us':>10} {'min_us':>9} {'max_us':>9} {'pct':>6}  kernel")
-    for n, c, t, a, mn, mx, p in summarize(rows):
+    print(f"{'calls':>7} {'total_us':>12} {'avg_us':>10} {'med_us':>9} {'min_us':>9} {'max_us':>9} {'pct':>6}  kernel")
+    for n, c, t, a, md, mn, mx, p in summarize(rows):
         short = n if len(n) < 110 else n[:107] + "..."
-        print(f"{c:7d} {t:12.1f} {a:10.3f} {mn:9.3f} {mx:9.3f} {p:6.2f}  {short}")
+        print(f"{c:7d} {t:12.1f} {a:10.3f} {md:9.3f} {mn:9.3f} {mx:9.3f} {p:6.2f}  {short}")
 
 
 if __name__ == "__main__":

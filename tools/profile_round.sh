@@ -50,6 +50,14 @@ for B in 1 128; do
     python3 tools/pmc_traffic.py "$O/pmc_FETCH_SIZE_b$B" "$O/pmc_WRITE_SIZE_b$B" "$TAG" $STEM > /dev/null || exit $?
     cp profiles/$STEM.json "$O/" && rm -rf "$O/pmc_FETCH_SIZE_b$B" "$O/pmc_WRITE_SIZE_b$B"
 done
+step gemv
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_gemv" -o run -- python3 "$R/tools/gemv_bench.py" > "$O/prof_gemv.log" 2>&1 || exit $?
+cd "$R" && python3 tools/prof_summary.py "$O/prof_gemv" > "$O/kernel_stats_gemv.txt" 2>&1 || exit $?
+rm -rf "$O/prof_gemv"
+tail -1 "$O/prof_gemv.log" | cut -c1-300
+step replicas-same-gpu
+timeout -k 10 300 python tools/replica_node.py --replicas 2 --same-gpu --steps 50 > "$O/replicas.log" 2>&1 || exit $?
+tail -1 "$O/replicas.log" | cut -c1-300
 step prefill
 timeout -k 10 300 python tools/prefill_gemm_bench.py > "$O/prefill.log" 2>&1 || exit $?
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_prefill" -o run -- python3 "$R/tools/prefill_gemm_bench.py" --iters 10 > "$O/prof_prefill.log" 2>&1 || exit $?

@@ -35,7 +35,8 @@ GEMV_NAMES = {0: "entry", 1: "image", 2: "dot", 3: "out", 7: "qkv_out", 8: "p_ss
               12: "p_q", 13: "w_landed"}
 ATTN_NAMES = {0: "entry", 1: "kv_done", 2: "out"}
 LM_NAMES = {0: "entry", 1: "staged", 2: "dot", 3: "ticket", 4: "argmax"}
-GEMM_NAMES = {0: "entry", 1: "issued", 2: "first_mma", 3: "mma_done", 4: "combined", 5: "epilogue"}
+GEMM_NAMES = {0: "entry", 14: "norm_published", 15: "rows_ready", 1: "issued", 2: "first_mma", 3: "mma_done",
+              4: "combined", 5: "epilogue"}
 RN_NAMES = {0: "entry", 1: "normed", 2: "done"}
 
 
@@ -110,7 +111,8 @@ def main():
                "rn_post": (dc[2048:2048 + B], RN_NAMES, 2), "gate_up": (dc[1024:1536], GEMM_NAMES, 5),
                "rn_ffn": (dc[2304:2304 + B], RN_NAMES, 2), "down": (dc[1536:2048], GEMM_NAMES, 5)}
     t0 = dc[0:512][dc[0:512, 0] > 0, 0].min()
-    res = {name: op_summary(r, nm, ls, t0) for name, (r, nm, ls) in ops.items()}
+    res = {name: op_summary(r, nm, ls, t0) for name, (r, nm, ls) in ops.items() if (r[:, 0] > 0).any()}
+    order = [n for n in order if n in res]  # batch > 1 with the norm fused into the GEMMs: no k_rownorm
     prev = None
     for name in order:
         if prev:

@@ -84,7 +84,11 @@ struct GemvArgs {
     // FP8 (e4m3fn) K/V cache: stored code = e4m3(clamp(y / scale, +-448)), RNE
     int kv8;
     float k_inv, v_inv;
+    // batched decode with the row norm fused into the GEMM launch (k_dec_gemm_t PRO != 0): arrival
+    // and pass words per 32-sequence tile ([kSeamTiles] each), zero between launches
+    unsigned* seam;
 };
+constexpr int kSeamTiles = 8;  // 32-sequence tiles: batch <= 256 (kDecGemmMaxB)
 
 __device__ __forceinline__ uint8_t to_fp8(float y) {
     const float c = fminf(fmaxf(y, -448.f), 448.f);
@@ -369,14 +373,16 @@ template <int MODE>
 struct EpiDec {
     const GemvArgs* a;
     // independent per-row loads (issue before the fragment loads) ...
+    // SC1: the scale / code sum were published in this launch (fused row norm): sc1 loads
+    template <bool SC1 = false>
     __device__ __forceinline__ void load(int r0, int c0, int l16, int q, EpiIn& in) const {
         const GemvArgs& g = *a;
         const int n = min(c0 + l16, g.N - 1);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int mc = min(r0 + 4 * q + r, g.B - 1);
-            in.sf[r] = g.act_sf[mc];
-            in.as[r] = g.act_sum[mc];
+            in.sf[r] = SC1 ? ld_sc1(g.act_sf + mc) : g.act_sf[mc];
+            in.as[r] = SC1 ? ld_sc1(g.act_sum + mc) : g.act_sum[mc];
             if constexpr (MODE == MODE_QKV) in.pos[r] = g.positions[mc];
             if constexpr (MODE == MODE_O || MODE == MODE_DN) in.res[r] = g.resid[(int64_t)mc * g.out_stride + n];
         }
@@ -629,8 +635,123 @@ __global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm(GemvArgs a) {
 // wave-instruction, whatever the bytes used). Lane (l16, q), block kb, half h: A = 16 codes of
 // k = 128 kb + 16 h + 4 q + jj + 32 g at [4g + jj]; B dword h = I2_S bytes [32 kb + 16 h + 4 q, +4)
 // of its column, decoded into the 4 groups g by shift 6 - 2g -- the same k for both operands.
-template <int TMT, int TNT, int NB, int MODE, int NW = kDgWaves>
-__global__ __launch_bounds__(NW * 64) void k_dec_gemm_t(GemvArgs a) {
+// PRO != 0: the row norm of the GEMM's input is fused into the launch (no k_rownorm launch and no
+// kernel boundary before the GEMM). Block (x, y) with x < rows of sequence tile y normalises and
+// quantises row 32 y + x exactly like k_rownorm / k_rownorm_attn (the 512-thread tree; 4-wave blocks
+// replay it with two chains per lane), stores its codes, scale and code sum write-through (sc1),
+// drains, and bumps the tile's arrival word; every block of the tile waits for all of its rows
+// (one polling lane, bounded), then reads the codes with sc1 loads. The weight fragments are issued
+// before the norm, so the weight stream overlaps it. The last block of the tile to pass the wait
+// re-arms both words (arrivals / passes), so the words are zero at every launch boundary. Needs the
+// whole grid co-resident (host: wf_model_create checks the occupancy, else the two-launch form) and
+// gridDim.x >= 32. PRO 1: rms_norm of x (a.x, a.nw); PRO 2: the attention row merged from the
+// decode-attention records (a.part_ml / a.part_o, kAttnPartSplits per head), then rms_norm.
+constexpr unsigned kSeamSpin = 1u << 22;  // polls before a waiting block gives up (never in a valid launch)
+template <int PPT2>
+__device__ __forceinline__ float norm_core_e512(const NormRow<PPT2, 256>& r, int K, float eps, float (&y)[PPT2][8],
+                                                float* red) {
+    // 256 threads replaying the 512-thread norm_core: virtual thread t + 256 j owns pieces 2 i + j
+    static_assert(PPT2 % 2 == 0, "two virtual threads per lane");
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float ss[2] = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < PPT2 / 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ss[j] = fmaf(y[2 * i + j][e], y[2 * i + j][e], ss[j]);
+    ss[0] = wave_sum(ss[0]);
+    ss[1] = wave_sum(ss[1]);
+    if (lane == 0) {
+        red[wave] = ss[0];
+        red[wave + 4] = ss[1];
+    }
+    __syncthreads();
+    const float rr = rbf(1.0f / sqrtf(tree_sum<8>(red) / (float)K + eps));
+    float mx = 0.f;
+#pragma unroll
+    for (int i = 0; i < PPT2; ++i) {
+        const uint32_t n4[4] = {r.w[i].x, r.w[i].y, r.w[i].z, r.w[i].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t a = pk_bf16(y[i][2 * j] * rr, y[i][2 * j + 1] * rr);
+            const uint32_t b = pk_bf16(bf_lo(a) * bf_lo(n4[j]), bf_hi(a) * bf_hi(n4[j]));
+            y[i][2 * j] = bf_lo(b);
+            y[i][2 * j + 1] = bf_hi(b);
+            mx = fmaxf(mx, fmaxf(fabsf(y[i][2 * j]), fabsf(y[i][2 * j + 1])));
+        }
+    }
+    mx = wave_max(mx);
+    if (lane == 0) red[8 + wave] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(red[8], red[9]), fmaxf(red[10], red[11]));
+    return (float)act_scale_from_max(mx);
+}
+
+// codes of the NT-thread pieces into the tile layout, write-through (the in-launch hand-off)
+template <int PPT, int NT>
+__device__ __forceinline__ int quant_row_tiled_wt(const float (&y)[PPT][8], float sf, int npad, int8_t* base, int row,
+                                                  int nkb) {
+    const float inv = 1.0f / sf;
+    int asum = 0;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+        const int p = (int)threadIdx.x + NT * i;
+        const uint2 qv = quant8(y[i], sf, inv, asum);
+        if (p < npad) {
+            st_sc1(reinterpret_cast<uint32_t*>(base + tile_code_pos(row, 8 * p, nkb)), qv.x);
+            st_sc1(reinterpret_cast<uint32_t*>(base + tile_code_pos(row, 8 * p + 4, nkb)), qv.y);
+        }
+    }
+    return asum;
+}
+
+// The input row r of the fused GEMM (PRO 1 / 2): codes, scale and code sum published write-through.
+template <int PRO, int PP, int NW>
+__device__ __forceinline__ void dec_row_prologue(const GemvArgs& a, int r, float* red, int* red_i) {
+    constexpr int NT = NW * 64;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, K = a.K, nkb = K >> 7;
+    int8_t* q8 = const_cast<int8_t*>(a.q8);
+    float sf;
+    int as;
+    if constexpr (NT == 512) {
+        NormRow<PP, 512> nr;
+        float y[PP][8];
+        if constexpr (PRO == 2) {
+            AttnRow<PP, 512, kAttnPartSplits> ar;
+            ar.issue(a.part_ml, a.part_o, r, a.Hq, 128);
+            nr.issue_w(a.nw, K);
+            ar.finish(a.Hq, 128, y);
+            sf = norm_core(nr, K, a.eps, y, red);
+        } else {
+            nr.issue(a.x + (int64_t)r * a.x_stride, a.nw, K);
+            sf = norm_row(nr, K, a.eps, y, red);
+        }
+        as = quant_row_tiled_wt<PP, 512>(y, sf, K / 8, q8, r, nkb);
+    } else {
+        static_assert(NT == 256 && PRO == 1, "4-wave blocks: rms_norm of x only");
+        constexpr int PP2 = 2 * PP;
+        NormRow<PP2, 256> nr;
+        nr.issue(a.x + (int64_t)r * a.x_stride, a.nw, K);
+        float y[PP2][8];
+        unpack_row(nr, K, y);
+        sf = norm_core_e512(nr, K, a.eps, y, red);
+        as = quant_row_tiled_wt<PP2, 256>(y, sf, K / 8, q8, r, nkb);
+    }
+    as = wave_sum_i(as);
+    if (lane == 0) red_i[wave] = as;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) t += red_i[i];
+        st_sc1(const_cast<int*>(a.act_sum) + r, t);
+        st_sc1(const_cast<float*>(a.act_sf) + r, sf);
+    }
+}
+
+template <int TMT, int TNT, int NB, int MODE, int NW = kDgWaves, int PRO = 0, int PP = 1>
+__global__ __launch_bounds__(NW * 64, 2) void k_dec_gemm_t(GemvArgs a) {  // 2 waves / SIMD: 4-wave blocks 2 per CU
     constexpr int EPT = TMT * TNT / NW;  // epilogue tiles per wave
     static_assert(EPT * NW == TMT * TNT, "whole epilogue tiles per wave");
     __shared__ v4i_t red[NW][TMT * TNT][64];
@@ -651,11 +772,20 @@ __global__ __launch_bounds__(NW * 64) void k_dec_gemm_t(GemvArgs a) {
         for (int j = 0; j < TNT; ++j) acc[i][j] = v4i_t{0, 0, 0, 0};
     uint4 fa[NB][TMT][2];
     uint2 fw[NB][TNT];
-    auto load = [&](uint4 (&la)[TMT][2], uint2 (&lw)[TNT], int kb) {
+    // PRO: the codes were written in this launch -> sc1 loads (buffer offsets: the code tensor < 2 GB)
+    const __amdgpu_buffer_rsrc_t rq = make_rsrc(a.q8);
+    auto load_a = [&](uint4 (&la)[TMT][2], int kb) {
 #pragma unroll
         for (int i = 0; i < TMT; ++i)
 #pragma unroll
-            for (int h = 0; h < 2; ++h) la[i][h] = *reinterpret_cast<const uint4*>(ap[i] + ((int64_t)kb << 11) + (h << 10));
+            for (int h = 0; h < 2; ++h) {
+                if constexpr (PRO != 0)
+                    la[i][h] = ld16_sc1(rq, (int)(ap[i] - a.q8) + (kb << 11) + (h << 10));
+                else
+                    la[i][h] = *reinterpret_cast<const uint4*>(ap[i] + ((int64_t)kb << 11) + (h << 10));
+            }
+    };
+    auto load_w = [&](uint2 (&lw)[TNT], int kb) {
 #pragma unroll
         for (int j = 0; j < TNT; ++j) lw[j] = *reinterpret_cast<const uint2*>(wp[j] + ((int64_t)kb << 9));
     };
@@ -688,11 +818,55 @@ __global__ __launch_bounds__(NW * 64) void k_dec_gemm_t(GemvArgs a) {
         const int tile = wave * EPT + x;
         er0[x] = (rt0 + tile / TNT) * 16;
         ec0[x] = (ct0 + tile % TNT) * 16;
-        e.load(er0[x], ec0[x], l16, q, ein[x]);
     }
+    if constexpr (PRO != 0) {
+        __shared__ float s_red[16];
+        __shared__ int s_red_i[NW];
+        const int ty = blockIdx.y, rows = min(32, a.B - 32 * ty);
+        unsigned* arrive = a.seam + ty;
+        const bool producer = (int)blockIdx.x < rows;
+        // blocks that only wait start their weight stream now; a producing block first normalises its
+        // row (its loads must not queue behind the weights: loads return in order) and publishes
+        // (the drain before the arrival waits for every load in flight, weights included)
+        // wave 0 polls: its loads return in order, so it issues its own weights only after the wait
+        if (producer) {
+            dec_row_prologue<PRO, PP, NW>(a, 32 * ty + blockIdx.x, s_red, s_red_i);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's sc1 stores are done
+            __syncthreads();
+            if (threadIdx.x == 0) __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (wave != 0) {
 #pragma unroll
-    for (int b = 0; b < NB; ++b)
-        if (b < cnt) load(fa[b], fw[b], wave + NW * b);
+            for (int b = 0; b < NB; ++b)
+                if (b < cnt) load_w(fw[b], wave + NW * b);
+        }
+        WF_STAMP(14);
+        if (threadIdx.x == 0) {
+            unsigned spins = 0;
+            while (ld_sc1(arrive) < (unsigned)rows && ++spins < kSeamSpin) __builtin_amdgcn_s_sleep(1);
+        }
+        __syncthreads();
+        if (wave == 0) {
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+                if (b < cnt) load_w(fw[b], wave + NW * b);
+        }
+        WF_STAMP(15);
+#pragma unroll
+        for (int x = 0; x < EPT; ++x) e.template load<true>(er0[x], ec0[x], l16, q, ein[x]);
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+            if (b < cnt) load_a(fa[b], wave + NW * b);
+    } else {
+#pragma unroll
+        for (int x = 0; x < EPT; ++x) e.load(er0[x], ec0[x], l16, q, ein[x]);
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+            if (b < cnt) {
+                load_a(fa[b], wave + NW * b);
+                load_w(fw[b], wave + NW * b);
+            }
+    }
 #pragma unroll
     for (int x = 0; x < EPT; ++x) e.load_rope(ec0[x], l16, ein[x]);
     WF_STAMP(1);
@@ -703,7 +877,10 @@ __global__ __launch_bounds__(NW * 64) void k_dec_gemm_t(GemvArgs a) {
             if (t < cnt) {
                 mma(fa[b], fw[b]);
                 if (t == 0) WF_STAMP(2);
-                if (t + NB < cnt) load(fa[b], fw[b], wave + NW * (t + NB));
+                if (t + NB < cnt) {
+                    load_a(fa[b], wave + NW * (t + NB));
+                    load_w(fw[b], wave + NW * (t + NB));
+                }
             }
         }
     }
@@ -721,6 +898,19 @@ __global__ __launch_bounds__(NW * 64) void k_dec_gemm_t(GemvArgs a) {
 #pragma unroll
         for (int w = 1; w < NW; ++w) sum += red[w][tile][lane];
         e.apply(er0[x], ec0[x], sum, l16, q, ein[x]);
+    }
+    if constexpr (PRO != 0) {
+        // re-arm: every block of the tile is past its wait once all have counted in here (the add is
+        // at the end so its return does not hold this block's loads)
+        if (threadIdx.x == 0) {
+            unsigned* arrive = a.seam + blockIdx.y;
+            unsigned* passed = a.seam + kSeamTiles + blockIdx.y;
+            const unsigned old = __hip_atomic_fetch_add(passed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (old == gridDim.x - 1u) {
+                st_sc1(arrive, 0u);
+                st_sc1(passed, 0u);
+            }
+        }
     }
     WF_STAMP(5);
     WF_STAMP_DRAIN(6);
@@ -1547,6 +1737,8 @@ struct wf_model {
     float* act_sf = nullptr;
     int* act_sum = nullptr;
     unsigned* tickets = nullptr;
+    unsigned* seam = nullptr;  // fused row-norm hand-off words (k_dec_gemm_t PRO), zero between launches
+    int fuse[4] = {0, 0, 0, 0};  // per GEMM op (QKV, O, GU, DN): row norm fused into the GEMM launch
     uint2* am_part = nullptr;
     int lm_blocks = 0;
     int64_t q8_stride = 0;
@@ -1610,21 +1802,56 @@ int dec_split(int N, int K, int* steps_per_split) {
     return (steps + sps - 1) / sps;
 }
 
+// The batched tile-layout GEMM's kernel for a shape, with or without the fused row norm (PRO: 0 none,
+// else the op's input kind; PP = 8-element pieces per thread of the norm). One function so the
+// launch and the host occupancy check name the same instantiation.
+template <int MODE, int PRO, int PP>
+const void* dec_gemm_kernel(int N, int K, int* threads) {
+    if (N >= 8192) {  // wide layers (gate|up): 128-column tiles halve the code re-reads
+        // 4 waves per block (64 KiB of LDS, two blocks per CU): the 108 x 4 blocks of the 2B
+        // gate|up at batch 128 are resident in one round (8 waves + 128 KiB took two rounds)
+        *threads = 4 * 64;
+        if constexpr (PRO == 2) return nullptr;  // the attention input is never this wide
+        else return reinterpret_cast<const void*>(&k_dec_gemm_t<2, 8, 3, MODE, 4, PRO, PP>);
+    }
+    *threads = kDgWaves * 64;
+    if (K <= 3 * 128 * kDgWaves)  // the whole K in flight at once
+        return reinterpret_cast<const void*>(&k_dec_gemm_t<2, 4, 3, MODE, kDgWaves, PRO, PP>);
+    return reinterpret_cast<const void*>(&k_dec_gemm_t<2, 4, 2, MODE, kDgWaves, PRO, PP>);
+}
+dim3 dec_gemm_grid(int N, int B) {
+    return N >= 8192 ? dim3((N + 127) / 128, (B + 31) / 32) : dim3(N / 64 + ((N & 63) ? 1 : 0), (B + 31) / 32);
+}
+template <int MODE>
+const void* dec_gemm_kernel_pro(int pro, int K, int N, int* threads) {
+    if (pro == 0) return dec_gemm_kernel<MODE, 0, 1>(N, K, threads);
+#ifndef WF_FUSED_NORM
+    return nullptr;  // the fused row norm is a study build (-DWF_FUSED_NORM)
+#else
+    const bool big = norm_ppt(K) != 1;
+    if constexpr (MODE == MODE_O) {
+        return big ? dec_gemm_kernel<MODE, 2, 2>(N, K, threads) : dec_gemm_kernel<MODE, 2, 1>(N, K, threads);
+    } else {
+        return big ? dec_gemm_kernel<MODE, 1, 2>(N, K, threads) : dec_gemm_kernel<MODE, 1, 1>(N, K, threads);
+    }
+#endif
+}
+
 template <int MODE, int LPR>
-int launch_gemv_fmt(int fmt, const GemvArgs& ga, hipStream_t st) {
+int launch_gemv_fmt(int fmt, const GemvArgs& ga, hipStream_t st, int pro = 0) {
     if (fmt == WF_FMT_I2S_MFMA) {  // batched decode on the matrix-core tile layouts
-        if (ga.N >= 8192) {  // wide layers (gate|up): 128-column tiles halve the code re-reads
-            // 4 waves per block (64 KiB of LDS, two blocks per CU): the 108 x 4 blocks of the 2B
-            // gate|up at batch 128 are resident in one round (8 waves + 128 KiB took two rounds)
-            const dim3 grid((ga.N + 127) / 128, (ga.B + 31) / 32);
-            hipLaunchKernelGGL((k_dec_gemm_t<2, 8, 3, MODE, 4>), grid, dim3(4 * 64), 0, st, ga);
-            return check_launch("dec_gemm_t");
+        int threads = 0;
+        const void* fn = dec_gemm_kernel_pro<MODE>(pro, ga.K, ga.N, &threads);
+        if (!fn) {
+            set_error("dec_gemm_t: no fused kernel for this shape");
+            return WF_EINVAL;
         }
-        const dim3 grid(ga.N / 64 + ((ga.N & 63) ? 1 : 0), (ga.B + 31) / 32);
-        if (ga.K <= 3 * 128 * kDgWaves)  // the whole K in flight at once
-            hipLaunchKernelGGL((k_dec_gemm_t<2, 4, 3, MODE>), grid, dim3(kDgWaves * 64), 0, st, ga);
-        else
-            hipLaunchKernelGGL((k_dec_gemm_t<2, 4, 2, MODE>), grid, dim3(kDgWaves * 64), 0, st, ga);
+        void* args[] = {const_cast<GemvArgs*>(&ga)};
+        const hipError_t e = hipLaunchKernel(fn, dec_gemm_grid(ga.N, ga.B), dim3(threads), args, 0, st);
+        if (e != hipSuccess) {
+            set_error("dec_gemm_t launch: %s", hipGetErrorString(e));
+            return WF_EHIP;
+        }
         return check_launch("dec_gemm_t");
     }
     if (fmt == WF_FMT_I2S && ga.B >= kDecMfmaMinB) {  // batched decode on the matrix cores, split-K
@@ -1679,6 +1906,56 @@ void launch_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, const uint
 #undef WF_RN
 }
 
+// Which batched GEMMs take their row norm inside the launch (k_dec_gemm_t PRO). The hand-off needs
+// every block of the grid resident at once (blocks of a 32-sequence tile wait for the tile's rows,
+// which blocks 0..31 of that tile produce) and >= 32 column blocks: checked per op against the
+// occupancy of the exact instantiation (the API's count, cross-checked with the block's registers,
+// LDS and threads: the API can read one block per CU high, MI355X_MICROARCH.md). Otherwise the op
+// keeps the k_rownorm launch.
+//
+// Measured and NOT the product (round 3, same-box bench at batch 128, ctx 1024): 31.5-32.5k ->
+// 27.4k tok/s. In-graph stamps: producers publish their rows ~3.5-4.5 us after entry, but the tile's
+// rows are seen ready only at 8-11 us -- the one polling lane's loads queue behind its CU's weight
+// stream (MI355X_MICROARCH.md price table, handoff-flag under load) and the norm overlaps nothing,
+// while the boundary it removes costs ~2 us. So only the study build -DWF_FUSED_NORM plans it.
+void fused_norm_plan(wf_model* m) {
+    const wf_model_desc& d = m->d;
+    for (int& f : m->fuse) f = 0;
+#ifdef WF_FUSED_NORM
+    if (d.wfmt != WF_FMT_I2S_MFMA || d.batch < kDecMfmaMinB || d.batch > 32 * kSeamTiles) return;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return;
+    const int shapes[4][2] = {{m->qkv_rows, d.hidden}, {d.hidden, d.hidden}, {2 * d.inter, d.hidden}, {d.hidden, d.inter}};
+    for (int op = 0; op < 4; ++op) {
+        const int N = shapes[op][0], K = shapes[op][1];
+        int threads = 0;
+        const void* fn = nullptr;
+        switch (op) {
+            case 0: fn = dec_gemm_kernel_pro<MODE_QKV>(1, K, N, &threads); break;
+            case 1: fn = dec_gemm_kernel_pro<MODE_O>(2, K, N, &threads); break;
+            case 2: fn = dec_gemm_kernel_pro<MODE_GU>(1, K, N, &threads); break;
+            default: fn = dec_gemm_kernel_pro<MODE_DN>(1, K, N, &threads); break;
+        }
+        if (!fn) continue;
+        const dim3 g = dec_gemm_grid(N, d.batch);
+        int per_cu = 0;
+        hipFuncAttributes fa{};
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0) != hipSuccess ||
+            hipFuncGetAttributes(&fa, fn) != hipSuccess)
+            continue;
+        // cross-check the API with the block's own limits (512 registers per SIMD lane, 4 SIMDs,
+        // 160 KiB of LDS, 2048 threads per CU): the smaller count is the one relied on
+        const int regs = std::max(8, (fa.numRegs + 7) / 8 * 8), waves_per_simd = threads / 64 / 4;
+        const int by_regs = (512 / regs) / std::max(1, waves_per_simd);
+        const int by_lds = fa.sharedSizeBytes ? (int)((160 * 1024) / fa.sharedSizeBytes) : 64;
+        const int sure = std::min({per_cu, by_regs, by_lds, 2048 / threads});
+        m->fuse[op] = (g.x >= 32 && (int64_t)sure * cus >= (int64_t)g.x * g.y) ? 1 : 0;
+    }
+    (void)hipGetLastError();
+#endif
+}
+
 GemvArgs base_args(const wf_model* m, int l) {
     const wf_model_desc& d = m->d;
     GemvArgs a{};
@@ -1711,7 +1988,15 @@ GemvArgs base_args(const wf_model* m, int l) {
     a.v_inv = d.kv_fp8 ? 1.0f / m->kv_scale[2 * l + 1] : 1.0f;
     a.kv_b_stride = (int64_t)d.n_kv_heads * d.max_seq * d.head_dim;
     a.kv_t = m->kv_tiled;
+    a.seam = m->seam;
     return a;
+}
+
+// input rows + norm weight of a GEMM whose launch normalises them itself (k_dec_gemm_t PRO 1)
+void fused_input(GemvArgs& a, const uint16_t* x, int64_t xs, const uint16_t* nw) {
+    a.x = x;
+    a.x_stride = xs;
+    a.nw = nw;
 }
 
 // input row + norm weight of a GEMV; batch > 1 normalises them in a k_rownorm launch first
@@ -1742,6 +2027,7 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             a.w = d.w_qkv + (int64_t)l * m->qkv_rows * wrow_bytes(d.wfmt, H);
             a.N = m->qkv_rows; a.K = H; a.ws0 = wsh[0]; a.ws1 = wsh[1]; a.ws2 = wsh[2];
             a.out = m->qbuf; a.out_stride = (int64_t)d.n_heads * D;
+            if (m->fuse[0]) return fused_input(a, m->h_a, H, d.ln_in + (int64_t)l * H), launch_gemv_fmt<MODE_QKV, kLprQKV>(d.wfmt, a, st, 1);
             if ((rc = gemv_input(m, a, m->h_a, H, d.ln_in + (int64_t)l * H, st))) return rc;
             return launch_gemv_fmt<MODE_QKV, kLprQKV>(d.wfmt, a, st);
         case WF_OP_ATTN:  // split partials; merged by the O projection's input stage
@@ -1760,6 +2046,7 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             a.nw = d.attn_sub + (int64_t)l * H;
             a.part_ml = m->part_ml;
             a.part_o = m->part_o;
+            if (m->fuse[1]) return launch_gemv_fmt<MODE_O, kLprO>(d.wfmt, a, st, 2);
             if (B > 1) {
 // the records of decode_attention_partials: kAttnPartSplits1 per head below batch 16, else kAttnPartSplits
 #define WF_RA(PPTV, TL, NS)                                                                                                 \
@@ -1780,11 +2067,13 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
         case WF_OP_GATE_UP:  // act = relu(gate)^2 * up of rms_norm(post_attention_layernorm)(h_b)
             a.w = d.w_gu + (int64_t)l * 2 * I * wrow_bytes(d.wfmt, H); a.N = 2 * I; a.K = H;
             a.ws0 = wsh[4]; a.ws1 = wsh[5]; a.out = m->act; a.out_stride = I;
+            if (m->fuse[2]) return fused_input(a, m->h_b, H, d.ln_post + (int64_t)l * H), launch_gemv_fmt<MODE_GU, kLprGU>(d.wfmt, a, st, 1);
             if ((rc = gemv_input(m, a, m->h_b, H, d.ln_post + (int64_t)l * H, st))) return rc;
             return launch_gemv_fmt<MODE_GU, kLprGU>(d.wfmt, a, st);
         case WF_OP_DOWN:  // h_a = h_b + down(rms_norm(ffn_sub_norm)(act))
             a.w = d.w_d + (int64_t)l * H * wrow_bytes(d.wfmt, I); a.N = H; a.K = I; a.ws0 = wsh[6];
             a.resid = m->h_b; a.out = m->h_a; a.out_stride = H;
+            if (m->fuse[3]) return fused_input(a, m->act, I, d.ffn_sub + (int64_t)l * I), launch_gemv_fmt<MODE_DN, kLprDN>(d.wfmt, a, st, 1);
             if ((rc = gemv_input(m, a, m->act, I, d.ffn_sub + (int64_t)l * I, st))) return rc;
             return launch_gemv_fmt<MODE_DN, kLprDN>(d.wfmt, a, st);
         case WF_OP_LM_HEAD: {  // final norm -> hn, logits = hn @ embed^T, greedy token
@@ -1913,10 +2202,13 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_ALLOC(m->act_sf, sizeof(float) * B);
     WF_ALLOC(m->act_sum, sizeof(int) * B);
     WF_ALLOC(m->tickets, sizeof(unsigned) * kTicketWords * TK_COUNT);
+    WF_ALLOC(m->seam, sizeof(unsigned) * 2 * kSeamTiles);
     WF_ALLOC(m->am_part, sizeof(uint2) * B * m->lm_blocks);
 #undef WF_ALLOC
     // tickets start at zero; every launch re-arms the ones it uses
     if ((e = hipMemset(m->tickets, 0, sizeof(unsigned) * kTicketWords * TK_COUNT)) != hipSuccess) return fail(e);
+    if ((e = hipMemset(m->seam, 0, sizeof(unsigned) * 2 * kSeamTiles)) != hipSuccess) return fail(e);
+    fused_norm_plan(m);
     if ((e = hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking)) != hipSuccess) return fail(e);
     *out = m;
     return WF_OK;
@@ -1928,7 +2220,7 @@ int wf_model_destroy(wf_model* m) {
     if (m->graph) (void)hipGraphDestroy(m->graph);
     if (m->cap) (void)hipStreamDestroy(m->cap);
     void* ptrs[] = {m->seq_lens, m->h_a, m->h_b, m->qbuf, m->part_ml, m->part_o, m->hn, m->act, m->q8, m->dec_ws,
-                    m->act_sf, m->act_sum, m->tickets, m->am_part, m->embed_t, m->pf_h_a, m->pf_h_b, m->pf_q,
+                    m->act_sf, m->act_sum, m->tickets, m->seam, m->am_part, m->embed_t, m->pf_h_a, m->pf_h_b, m->pf_q,
                     m->pf_attn, m->pf_act, m->pf_q8, m->pf_sf, m->pf_asum, m->pf_seq};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -1947,6 +2239,12 @@ int wf_model_launch_op(wf_model* m, int layer, int op, void* stream) {
     WF_REQUIRE(m, "model_launch_op: null model");
     WF_REQUIRE(layer >= 0 && layer < m->d.layers, "model_launch_op: layer %d out of range", layer);
     return run_op(m, layer, op, as_stream(stream));
+}
+
+int wf_model_fused_norm(const wf_model* m, int* flags4) {
+    WF_REQUIRE(m && flags4, "model_fused_norm: null argument");
+    for (int i = 0; i < 4; ++i) flags4[i] = m->fuse[i];
+    return WF_OK;
 }
 
 int wf_model_attn_view(const wf_model* m, wf_attn_records* out) {

@@ -97,10 +97,10 @@ __global__ __launch_bounds__(256) void k_ternary_gemm(const uint8_t* __restrict_
 // ---------------------------------------------------------------------------------------------
 // Standalone GEMV (M = 1; sgl_kernel bitnet_gemv, scripts/benchmark_kernels.py:40-66): a memory-
 // latency problem -- 0.4-4.5 MB per call, i.e. 1.6-17 KB per CU -- so every byte of the matrix is
-// in flight at once and as many CUs as possible take part. Block = 256 threads = 4 waves; a row is
-// split over W waves (W = 1, 2 or 4, chosen per shape so the grid has >= ~1024 blocks: k/v's 640
-// rows take W = 4), wave kp of a row takes its contiguous 1/W of the row's 16-byte chunks, lane l
-// chunk c0 + l + 64 j. Issue order: the activation pieces (L2-resident), then every weight chunk of
+// in flight at once and as many CUs as possible take part. Block = 256 threads = 4 waves; the kernel
+// can split a row over W waves (wave kp takes its contiguous 1/W of the row's 16-byte chunks, lane l
+// chunk c0 + l + 64 j), but the launcher uses W = 1 (one wave per row) at every shape: fewer,
+// fuller blocks won over >= 1024 split-row blocks. Issue order: the activation pieces (L2-resident), then every weight chunk of
 // the lane (nt), then the activation image goes to LDS (conflict-free stripes, wf_device.h) behind
 // one barrier that the weight latency hides. Each wave sums its lanes with DPP; the W wave partials
 // of a row meet in LDS in wave order. Integer sums: bit-exact with any split.
@@ -159,11 +159,14 @@ __global__ __launch_bounds__(256) void k_gemv_rows(const uint8_t* __restrict__ W
     }
 }
 
+
 template <class F>
 static int launch_gemv_rows(const uint8_t* w, const int8_t* a, float scale, int N, int K, float* y, hipStream_t st) {
     const int C = F::chunks(K);
-    int W = 1;
-    while (W < 4 && (int64_t)N * W / 4 < 1024 && (C + 2 * W - 1) / (2 * W) >= 8) W *= 2;
+    // one wave per row at every shape: splitting k/v's and q/o's rows over 2-4 waves to reach >= 1024
+    // blocks was slower (same-box graph replay, tools/gemv_bench.py: q/o 2.91 -> 2.49 us, k/v 2.56 ->
+    // 2.18 us, down 3.27 -> 3.17 us with one wave per row; gate/up already was)
+    const int W = 1;
     const int cw = (C + W - 1) / W;
     const int J = (cw + 63) / 64;
     const int img = lds_image_bytes<F>(K);
@@ -172,9 +175,7 @@ static int launch_gemv_rows(const uint8_t* w, const int8_t* a, float scale, int 
 #define WF_GRJ(WV)            \
     if (J == 1) WF_GR(WV, 1); \
     else WF_GR(WV, 2);
-    if (W == 1) { WF_GRJ(1) }
-    else if (W == 2) { WF_GRJ(2) }
-    else { WF_GRJ(4) }
+    WF_GRJ(1)
 #undef WF_GRJ
 #undef WF_GR
     return check_launch("gemv_rows");

@@ -482,6 +482,25 @@ class BitNetDecoder:
         return q, ml, o
 
     @property
+    def fused_norm(self) -> tuple:
+        """(QKV, O, gate|up, down): which batched GEMMs normalise their input rows inside the GEMM
+        launch (include/wf_bitnet.h wf_model_fused_norm)."""
+        f = (C.c_int * 4)()
+        call("wf_model_fused_norm", self._h, C.addressof(f))
+        return tuple(bool(x) for x in f)
+
+    def load_attention_q(self, q: torch.Tensor) -> None:
+        """Overwrite the q hand-off of the last WF_OP_QKV with q [B, Hq, D] bf16 (kernel-level checks:
+        the next WF_OP_ATTN reads it)."""
+        v = _lib.WFAttnView()
+        call("wf_model_attn_view", self._h, C.addressof(v))
+        cfg, B = self.cfg, self.batch
+        if tuple(q.shape) != (B, cfg.n_heads, cfg.head_dim) or q.dtype != torch.bfloat16 or not q.is_cuda:
+            raise ValueError("q must be [batch, n_heads, head_dim] bf16 on the decoder's device")
+        q = q.contiguous()
+        ops.device_copy(v.q, q.data_ptr(), q.numel() * 2)
+
+    @property
     def weight_bytes(self) -> int:
         return sum(t.numel() for t in (self.w_qkv, self.w_o, self.w_gu, self.w_d)) + self.embed.numel() * 2
 
