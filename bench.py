@@ -51,8 +51,9 @@ def parse():
                          "config 4), on paged KV")
     ap.add_argument("--paged", action="store_true", help="paged KV (32-token pages; batch >= 16)")
     ap.add_argument("--no-gemv", action="store_true", help="skip the standalone GEMV benchmark")
-    ap.add_argument("--kv", choices=["bf16", "fp8"], default="bf16",
-                    help="K/V cache element type (fp8 = OCP e4m3fn, batch >= 16; scale 1.0)")
+    ap.add_argument("--kv", choices=["bf16", "fp8", "int8"], default="bf16",
+                    help="K/V cache element type (batch >= 16): fp8 = OCP e4m3fn, scale 1.0; int8 = the "
+                         "reference's INT8 KVCacheDtype, scale 4/127 (unit-variance synthetic K/V)")
     return ap.parse_args()
 
 
@@ -224,7 +225,7 @@ def main():
     num_pages = int(sum((c + total + 1 + 31) // 32 for c in ctxs)) if paged else 0
     w = synthetic_weights(cfg, seed=0, device="cuda")
     dec = BitNetDecoder(cfg, w, batch=B, wfmt=wfmt, num_pages=num_pages, page_seed=0 if paged else None,
-                        kv_dtype=args.kv)
+                        kv_dtype=args.kv, kv_scale=(4.0 / 127, 4.0 / 127) if args.kv == "int8" else None)
     del w
     torch.cuda.empty_cache()
     if paged:
@@ -257,7 +258,7 @@ def main():
         roof = {"bound": "hbm", "achieved": dom["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom_name,
                 "bytes_per_launch": dom["bytes"], "us_per_launch": dom["us"]}
-    kv_esz = 1 if args.kv == "fp8" else 2
+    kv_esz = 1 if args.kv in ("fp8", "int8") else 2
     step_bytes = cfg.weight_bytes_per_token(wfmt) + B * cfg.kv_bytes_per_token(ctx + total // 2) * kv_esz // 2
     gemv = None if (args.no_gemv or B != 1) else gemv_bench()
     if cpu:

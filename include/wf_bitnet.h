@@ -36,6 +36,8 @@ extern "C" {
 
 enum { WF_F32 = 0, WF_BF16 = 1, WF_F16 = 2, WF_I8 = 3, WF_U8 = 4 };
 enum { WF_FMT_I2S = 0, WF_FMT_TQ = 1, WF_FMT_I2S_MFMA = 2 };
+/* K/V cache element types (wf_model_desc.kv_quant) */
+enum { WF_KV_BF16 = 0, WF_KV_FP8 = 1, WF_KV_INT8 = 2 };
 
 /* ---- library ------------------------------------------------------------------------------ */
 const char* wf_last_error(void);
@@ -190,13 +192,17 @@ typedef struct {
      * page_table == NULL keeps the dense layout. */
     const int32_t* page_table;
     int num_pages;
-    /* FP8 K/V (optional; same decoders as paged KV): kv_fp8 = 1 stores K and V as OCP e4m3fn bytes,
-     * code = e4m3(clamp(v / scale, +-448)) (RNE), in the same tile layouts / pages with one byte per
-     * element -- half the attention bytes. kv_scale: HOST [layers][2] (K, V) scales (NULL = 1.0),
-     * copied at create; the attention widens codes to bf16 exactly and folds the scales into the
-     * score scale and the partial sums. The reference's INT8/"FP8" KVCache option
-     * (kv_cache/kv_cache.py:159-218) is the analogue; quality bar cosine >= 0.998 vs bf16 K/V. */
-    int kv_fp8;
+    /* One-byte K/V (optional; same decoders as paged KV), kv_quant:
+     *   WF_KV_BF16 (0) bf16 K/V;
+     *   WF_KV_FP8  (1) OCP e4m3fn bytes, code = e4m3(clamp(v / scale, +-448)) (RNE);
+     *   WF_KV_INT8 (2) int8, code = clamp(rne(v / scale), -127, 127) -- the reference's default
+     *                  KVCacheDtype.INT8 (kv_cache/kv_cache.py:30-37, 159-218) with a static
+     *                  per-layer scale instead of its per-update absmax (one scale per layer there too).
+     * Same tile layouts / pages with one byte per element -- half the attention bytes. kv_scale: HOST
+     * [layers][2] (K, V) scales (NULL = 1.0), copied at create; the attention widens codes to bf16
+     * exactly and folds the scales into the score scale and the partial sums. Quality bar (reference
+     * docs/research/notebook.md:690-700): attention-output cosine >= 0.998 vs bf16 K/V. */
+    int kv_quant;
     const float* kv_scale;
 } wf_model_desc;
 

@@ -240,6 +240,13 @@ def e4m3_decode_table() -> np.ndarray:
     return np.array([lib().orc_e4m3_to_f32(c) for c in range(256)], dtype=np.float32)
 
 
+def int8_codes_to_bf16(codes: np.ndarray, scale: float) -> np.ndarray:
+    """bf16 bits of int8 code * scale (what the oracle's int8 K/V rows hold); codes as int8 or their
+    uint8 bytes."""
+    v = np.asarray(codes).astype(np.uint8).view(np.int8).astype(np.float32) * np.float32(scale)
+    return f32_to_bf16(v.astype(np.float32))
+
+
 def fp8_codes_to_bf16(codes: np.ndarray, scale: float) -> np.ndarray:
     """bf16 bits of e4m3 code * scale (what the oracle's FP8 K/V rows hold)."""
     v = e4m3_decode_table()[np.asarray(codes, dtype=np.uint8)] * np.float32(scale)
@@ -259,7 +266,8 @@ class DecodeModel:
     """Holds a model's host arrays (dict of numpy arrays in the tests/golden/decode.npz layout) for
     orc_decode_step. K/V caches are [layers, n_kv_heads, max_seq, head_dim] bf16 bits."""
 
-    def __init__(self, arrays: dict, libname: str = "liborc.so", kv_fp8: bool = False, kv_scale=None):
+    def __init__(self, arrays: dict, libname: str = "liborc.so", kv_fp8=False, kv_scale=None):
+        """kv_fp8: False / 0 bf16 K/V rows, True / 1 e4m3 rows, 2 int8 rows (orc_model.kv_fp8)."""
         H, L, HQ, HKV, D, I, V, S = (int(x) for x in arrays["cfg"])
         self.cfg = (H, L, HQ, HKV, D, I, V, S)
         self.a = {k: np.ascontiguousarray(v) for k, v in arrays.items()}

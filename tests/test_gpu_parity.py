@@ -684,16 +684,19 @@ def _cos_rows(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return torch.nn.functional.cosine_similarity(a.float(), b.float(), dim=-1)
 
 
-def test_fp8_kv_codes_and_decode_quality():
-    """FP8 (e4m3fn) K/V for the batched decode step: (1) the K/V codes a step writes equal torch's
-    float8_e4m3fn rounding of the bf16 values a bf16-KV decoder writes, divided by the per-layer
-    scale (bit-exact, layer 0 where both see the same input); (2) decoding over ragged contexts
+@pytest.mark.parametrize("kvd", ["fp8", "int8"])
+def test_fp8_kv_codes_and_decode_quality(kvd):
+    """One-byte K/V for the batched decode step (FP8 e4m3fn; int8 = the reference's INT8
+    KVCacheDtype): (1) the K/V codes a step writes equal torch's e4m3fn / int8 rounding
+    (wfamd.model.to_fp8_codes / to_int8_codes) of the bf16 values a bf16-KV decoder writes, divided
+    by the per-layer scale (bit-exact, layer 0 where both see the same input); (2) decoding over ragged contexts
     with FP8 K/V keeps the logits close to bf16 K/V. The reference's quantized-KV bar is cosine >=
     0.998 on one attention output (docs/research/notebook.md:690-700); here it is the logits after
     two layers of a random-init model and the LM head, measured at mean ~0.997 (e4m3 keeps 3
     mantissa bits), so the bar is mean >= 0.995, floor 0.99, and >= 80 % equal greedy tokens;
     (3) paged FP8 == dense FP8 bit for bit."""
-    from wfamd.model import BitNetConfig, BitNetDecoder, from_kv_tiles, synthetic_weights, to_fp8_codes
+    from wfamd.model import KV_CODES, BitNetConfig, BitNetDecoder, from_kv_tiles, synthetic_weights
+    enc = KV_CODES[kvd][0]
     cfg = BitNetConfig(hidden=512, layers=2, n_heads=4, n_kv_heads=1, head_dim=128, inter=768, vocab=1024,
                        max_seq=2048)
     w = synthetic_weights(cfg, seed=31)
@@ -701,10 +704,10 @@ def test_fp8_kv_codes_and_decode_quality():
     # random-init scales give |scores| ~ 30: one-hot softmax where any rounding flips the winner)
     w["wscale"][:, :3] = 0.05
     B = 20
-    scale = [(0.5, 0.25), (1.0, 0.5)]
+    scale = [(0.5, 0.25), (1.0, 0.5)] if kvd == "fp8" else [(1 / 16, 1 / 32), (1 / 8, 1 / 16)]
     bf = BitNetDecoder(cfg, w, batch=B)
-    f8 = BitNetDecoder(cfg, w, batch=B, kv_dtype="fp8", kv_scale=scale)
-    f8p = BitNetDecoder(cfg, w, batch=B, kv_dtype="fp8", kv_scale=scale, num_pages=B * 64, page_seed=4)
+    f8 = BitNetDecoder(cfg, w, batch=B, kv_dtype=kvd, kv_scale=scale)
+    f8p = BitNetDecoder(cfg, w, batch=B, kv_dtype=kvd, kv_scale=scale, num_pages=B * 64, page_seed=4)
     gen = torch.Generator(device="cuda").manual_seed(5)
     ctx = 1500
     pos = [0, 1, 5, 31, 32, 33, 127, 128, 129, 255, 256, 300, 511, 777, 1000, 1023, 1024, 1300, 1499, 1400]
@@ -725,16 +728,17 @@ def test_fp8_kv_codes_and_decode_quality():
     k8, v8 = from_kv_tiles(f8.k_cache[0], f8.v_cache[0])
     for b in range(B):
         p = pos[b]
-        assert torch.equal(k8[b, :, p], to_fp8_codes(kb[b, :, p], scale[0][0])), b
-        assert torch.equal(v8[b, :, p], to_fp8_codes(vb[b, :, p], scale[0][1])), b
+        assert torch.equal(k8[b, :, p], enc(kb[b, :, p], scale[0][0])), b
+        assert torch.equal(v8[b, :, p], enc(vb[b, :, p], scale[0][1])), b
     assert torch.equal(f8.logits.view(torch.int16), f8p.logits.view(torch.int16))
     cos = _cos_rows(f8.logits, bf.logits)
     assert cos.mean().item() >= 0.995 and cos.min().item() >= 0.99, cos
     assert (f8.tokens == bf.tokens).float().mean().item() >= 0.8
 
 
-def test_fp8_kv_prefill():
-    """Prefill into FP8 K/V: paged == dense bit-exact, and the next step's logits stay within the
+@pytest.mark.parametrize("kvd", ["fp8", "int8"])
+def test_fp8_kv_prefill(kvd):
+    """Prefill into one-byte K/V (FP8 / int8): paged == dense bit-exact, and the next step's logits stay within the
     FP8 bar of test_fp8_kv_codes_and_decode_quality (mean cosine >= 0.995, floor 0.99) of the same
     prefill + step on bf16 K/V."""
     from wfamd.model import BitNetConfig, BitNetDecoder, synthetic_weights
@@ -745,8 +749,9 @@ def test_fp8_kv_prefill():
     B = 16
     rng = np.random.default_rng(6)
     prompts = {b: rng.integers(0, cfg.vocab, size=int(n)).tolist() for b, n in zip(range(0, B, 2), (40, 3, 150, 64, 97, 200, 17, 33))}
-    decs = [BitNetDecoder(cfg, w, batch=B), BitNetDecoder(cfg, w, batch=B, kv_dtype="fp8", kv_scale=(0.5, 0.5)),
-            BitNetDecoder(cfg, w, batch=B, kv_dtype="fp8", kv_scale=(0.5, 0.5), num_pages=B * 16, page_seed=9)]
+    sc = (0.5, 0.5) if kvd == "fp8" else (1 / 16, 1 / 16)
+    decs = [BitNetDecoder(cfg, w, batch=B), BitNetDecoder(cfg, w, batch=B, kv_dtype=kvd, kv_scale=sc),
+            BitNetDecoder(cfg, w, batch=B, kv_dtype=kvd, kv_scale=sc, num_pages=B * 16, page_seed=9)]
     for dec in decs:
         for b, p in prompts.items():
             dec.admit(b, p)
@@ -773,6 +778,10 @@ def test_prefill_fp8_paged_argument_errors():
         d1.prefill([(0, [1, 2, 3], 0)])
     with pytest.raises(ValueError):
         BitNetDecoder(cfg, w, batch=4, kv_dtype="fp8")
+    with pytest.raises(ValueError):
+        BitNetDecoder(cfg, w, batch=4, kv_dtype="int8")
+    with pytest.raises(ValueError):
+        BitNetDecoder(cfg, w, batch=16, kv_dtype="int4")
     with pytest.raises(ValueError):
         BitNetDecoder(cfg, w, batch=4, num_pages=64)
     with pytest.raises(ValueError):

@@ -499,7 +499,20 @@ __device__ __forceinline__ uint4 fp8x8_to_bf16(uint2 r) {
     return make_uint4(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, c),
                       __builtin_bit_cast(uint32_t, d));
 }
-template <bool KV8>
+// int8 K/V caches (the reference's default KVCacheDtype.INT8, kv_cache/kv_cache.py:159-218, with a
+// static per-layer scale): a fragment is 8 signed codes (8 bytes per lane), widened exactly -- each
+// byte biased to unsigned (xor 0x80), v_cvt_f32_ubyteN, -128 (packed), then bf16 (|code| <= 127 is
+// exact in bf16). Scales folded like FP8's.
+__device__ __forceinline__ uint32_t i8x2_to_bf16(uint32_t u, int sh) {
+    const float lo = (float)((u >> sh) & 0xffu) - 128.0f, hi = (float)((u >> (sh + 8)) & 0xffu) - 128.0f;
+    return pk_bf16(lo, hi);
+}
+__device__ __forceinline__ uint4 i8x8_to_bf16(uint2 r) {
+    const uint32_t x = r.x ^ 0x80808080u, y = r.y ^ 0x80808080u;
+    return make_uint4(i8x2_to_bf16(x, 0), i8x2_to_bf16(x, 16), i8x2_to_bf16(y, 0), i8x2_to_bf16(y, 16));
+}
+// KVQ: K/V cache element type -- 0 bf16, 1 OCP e4m3fn, 2 int8 (include/wf_bitnet.h WF_KV_*)
+template <int KVQ>
 struct KvFrag {
     using T = uint4;  // 8 bf16
     __device__ static __forceinline__ T ld(const uint16_t* base, int64_t elem) {
@@ -515,24 +528,31 @@ struct KvFrag {
         return make_uint4(t.x & vm[0], t.y & vm[1], t.z & vm[2], t.w & vm[3]);
     }
 };
-template <>
-struct KvFrag<true> {
-    using T = uint2;  // 8 fp8
+template <int KVQ>
+struct KvFrag8 {
+    using T = uint2;  // 8 one-byte codes
     __device__ static __forceinline__ T ld(const uint16_t* base, int64_t elem) {
         return *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(base) + elem);
     }
-    __device__ static __forceinline__ uint4 bf(const T& t) { return fp8x8_to_bf16(t); }
+    __device__ static __forceinline__ uint4 bf(const T& t) {
+        if constexpr (KVQ == 2) return i8x8_to_bf16(t);
+        else return fp8x8_to_bf16(t);
+    }
     __device__ static __forceinline__ T mask(const T& t, int lim) {
         if (lim >= 8) return t;
         const uint64_t m = lim <= 0 ? 0ull : (~0ull >> (8 * (8 - lim)));
-        return make_uint2(t.x & (uint32_t)m, t.y & (uint32_t)(m >> 32));
+        return make_uint2(t.x & (uint32_t)m, t.y & (uint32_t)(m >> 32));  // zero bytes: 0 in both codes
     }
 };
+template <>
+struct KvFrag<1> : KvFrag8<1> {};
+template <>
+struct KvFrag<2> : KvFrag8<2> {};
 
 // PAIR: records of 2 waves -- grid.x = kAttnPartSplits / 2, the 16 waves of (b, g) take the
 // tiles round-robin and each block merges its wave pairs (0, 1) and (2, 3) into 2 records: half the
 // per-tile block overheads of the 4-wave records, twice the waves per sequence of WREC.
-template <bool DB, bool RR, bool WREC = false, bool KV8 = false, bool PAIR = false>
+template <bool DB, bool RR, bool WREC = false, int KV8 = 0, bool PAIR = false>
 __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* __restrict__ q, int64_t q_sb,
                                                    const uint16_t* __restrict__ K, const uint16_t* __restrict__ Vt,
                                                    int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv, int S,
@@ -662,7 +682,7 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
     WF_STAMP(1);
     l_run += __shfl_xor(l_run, 16, 64);
     l_run += __shfl_xor(l_run, 32, 64);
-    if constexpr (KV8) {  // o = v_scale * sum p v8 (the partial records carry the V scale)
+    if constexpr (KV8 != 0) {  // o = v_scale * sum p v8 (the partial records carry the V scale)
 #pragma unroll
         for (int n = 0; n < 8; ++n)
 #pragma unroll
@@ -742,7 +762,7 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
 // position are zeroed (stale pages). Each wave streams its whole key
 // range and writes the normalised output rows bf16(o / l) (no split partials).
 // ---------------------------------------------------------------------------------------------
-template <int CG, int OCC, bool KV8 = false>
+template <int CG, int OCC, int KV8 = 0>
 __global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __restrict__ q, int64_t q_rs,
                                                          const uint16_t* __restrict__ K, const uint16_t* __restrict__ Vt,
                                                          int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv,
@@ -861,7 +881,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __res
                 acc[u][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl[u], vf[n], acc[u][n], 0, 0, 0);
             }
     }
-    if constexpr (KV8) {
+    if constexpr (KV8 != 0) {
 #pragma unroll
         for (int u = 0; u < CG; ++u)
 #pragma unroll
@@ -1169,8 +1189,12 @@ int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const 
         const float sl2 = sm_scale * 1.4426950408889634f;
         hipLaunchKernelGGL(k_attn_prefill_fa, grid, dim3(256), 0, st, q, q_rs, k, v, kv_sb, kv_sh, row_pos, row_slot, M,
                            sl2, pt, pps, npages, kv_pgs, out, o_rs, xchunk);
-    } else if (kv8)
-        hipLaunchKernelGGL((k_attn_prefill<1, 2, true>), dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v, kv_sb,
+    } else if (kv8 == 2)
+        hipLaunchKernelGGL((k_attn_prefill<1, 2, 2>), dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v, kv_sb,
+                           kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale * k_scale, pt, pps, npages, kv_pgs, out, o_rs,
+                           v_scale);
+    else if (kv8)
+        hipLaunchKernelGGL((k_attn_prefill<1, 2, 1>), dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v, kv_sb,
                            kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale * k_scale, pt, pps, npages, kv_pgs, out, o_rs,
                            v_scale);
     else
@@ -1203,8 +1227,11 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
             set_error("decode_attention_partials: tiled K/V need S %% 32 == 0 (S=%d)", S);
             return WF_EINVAL;
         }
-        if (kv8)  // FP8 caches: K scale folded into the score scale; one tile in flight per wave, 4 waves per SIMD
-            hipLaunchKernelGGL((k_attn_mfma<false, false, false, true>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
+        if (kv8 == 2)  // int8 caches: as FP8, a wider in-register decode
+            hipLaunchKernelGGL((k_attn_mfma<false, false, false, 2>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
+                               kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale, ml, o, pt, pps, npages, kv_pgs, v_scale);
+        else if (kv8)  // FP8 caches: K scale folded into the score scale; one tile in flight per wave, 4 waves per SIMD
+            hipLaunchKernelGGL((k_attn_mfma<false, false, false, 1>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
                                kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale, ml, o, pt, pps, npages, kv_pgs, v_scale);
         else  // bf16: double-buffered tiles, 2 waves per SIMD (at 4 splits a wave takes >= 2 tiles at ctx >= 1024)
             hipLaunchKernelGGL((k_attn_mfma<true, false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv,

@@ -94,6 +94,12 @@ __device__ __forceinline__ uint8_t to_fp8(float y) {
     const float c = fminf(fmaxf(y, -448.f), 448.f);
     return (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(c, c, 0, false) & 0xffu);
 }
+// one-byte K/V code of y (already divided by the layer's scale): kvq 1 = OCP e4m3fn (RNE, saturating),
+// 2 = int8 (the reference's INT8 KVCacheDtype: clamp(rne(y), -127, 127), kv_cache/kv_cache.py:159-185)
+__device__ __forceinline__ uint8_t to_kv8(float y, int kvq) {
+    if (kvq == 2) return (uint8_t)(int8_t)(int)fminf(fmaxf(__builtin_rintf(y), -127.f), 127.f);
+    return to_fp8(y);
+}
 
 // Reference correction (direct_inference_full.py:201-208) for one output:
 // raw = fl32(S * f(ws)); c = f(ws * act_sum); out = fl32(fl32(raw - c) * f(s))
@@ -473,7 +479,7 @@ struct EpiDec {
                     } else {
                         const int kvh = head - g.Hq - (proj == 2 ? g.Hkv : 0);
                         const int slot = g.row_slot ? g.row_slot[m] : m;
-                        if (g.kv8) {  // FP8 tile-layout cache (element offsets are byte offsets)
+                        if (g.kv8) {  // FP8 / int8 tile-layout cache (element offsets are byte offsets)
                             uint8_t* c8 = reinterpret_cast<uint8_t*>(proj == 1 ? g.kc : g.vc);
                             int64_t off;
                             if (g.pt) {
@@ -483,7 +489,7 @@ struct EpiDec {
                                 off = (int64_t)slot * g.kv_b_stride + (int64_t)kvh * g.S * 128 +
                                       (proj == 1 ? k_tile_off(pos, d) : v_tile_off(pos, d));
                             }
-                            c8[off] = to_fp8(y * (proj == 1 ? g.k_inv : g.v_inv));
+                            c8[off] = to_kv8(y * (proj == 1 ? g.k_inv : g.v_inv), g.kv8);
                             continue;
                         }
                         if (g.pt) {  // paged: block pos >> 5 lives in page pt[slot][pos >> 5]
@@ -1006,8 +1012,8 @@ __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int b
             uint32_t b1[2] = {0u, 0u}, b2[2] = {0u, 0u};
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                b1[e >> 2] |= (uint32_t)to_fp8(y1[e] * g.k_inv) << (8 * (e & 3));
-                b2[e >> 2] |= (uint32_t)to_fp8(y2[e] * g.k_inv) << (8 * (e & 3));
+                b1[e >> 2] |= (uint32_t)to_kv8(y1[e] * g.k_inv, kv8) << (8 * (e & 3));
+                b2[e >> 2] |= (uint32_t)to_kv8(y2[e] * g.k_inv, kv8) << (8 * (e & 3));
             }
             *reinterpret_cast<uint2*>(c8 + o1) = make_uint2(b1[0], b1[1]);
             *reinterpret_cast<uint2*>(c8 + o2) = make_uint2(b2[0], b2[1]);
@@ -1039,7 +1045,7 @@ __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int b
             if (kv8) {
                 uint32_t b[2] = {0u, 0u};
 #pragma unroll
-                for (int e = 0; e < 8; ++e) b[e >> 2] |= (uint32_t)to_fp8(bf2f(vv[e]) * g.v_inv) << (8 * (e & 3));
+                for (int e = 0; e < 8; ++e) b[e >> 2] |= (uint32_t)to_kv8(bf2f(vv[e]) * g.v_inv, kv8) << (8 * (e & 3));
                 *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(g.vc) + off) = make_uint2(b[0], b[1]);
             } else {
                 *reinterpret_cast<uint4*>(g.vc + off) = make_uint4(vv[0] | (uint32_t)vv[1] << 16, vv[2] | (uint32_t)vv[3] << 16,
@@ -1054,7 +1060,7 @@ __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int b
             const int64_t base = g.pt ? (int64_t)s_pg[rl] * g.kv_pgs + (int64_t)kvh * 4096
                                       : (int64_t)s_slot[rl] * g.kv_b_stride + (int64_t)kvh * g.S * 128;
             const int64_t off = base + v_tile_off(g.pt ? (pos & 31) : pos, d);
-            if (kv8) reinterpret_cast<uint8_t*>(g.vc)[off] = to_fp8(bf2f(vv[e]) * g.v_inv);
+            if (kv8) reinterpret_cast<uint8_t*>(g.vc)[off] = to_kv8(bf2f(vv[e]) * g.v_inv, kv8);
             else g.vc[off] = vv[e];
         }
     }
@@ -1919,9 +1925,9 @@ void launch_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, const uint
 // stream (MI355X_MICROARCH.md price table, handoff-flag under load) and the norm overlaps nothing,
 // while the boundary it removes costs ~2 us. So only the study build -DWF_FUSED_NORM plans it.
 void fused_norm_plan(wf_model* m) {
-    const wf_model_desc& d = m->d;
     for (int& f : m->fuse) f = 0;
 #ifdef WF_FUSED_NORM
+    const wf_model_desc& d = m->d;
     if (d.wfmt != WF_FMT_I2S_MFMA || d.batch < kDecMfmaMinB || d.batch > 32 * kSeamTiles) return;
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -1980,12 +1986,12 @@ GemvArgs base_args(const wf_model* m, int l) {
     a.npages = d.num_pages;
     a.kv_pgs = (int64_t)d.n_kv_heads * 32 * d.head_dim;
     // FP8 caches hold one byte per element: the layer offset is in bytes, the kernels index bytes
-    const int64_t esz = d.kv_fp8 ? 1 : 2;
+    const int64_t esz = d.kv_quant ? 1 : 2;
     a.kc = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(m->k_cache) + l * kvl * esz);
     a.vc = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(m->v_cache) + l * kvl * esz);
-    a.kv8 = d.kv_fp8;
-    a.k_inv = d.kv_fp8 ? 1.0f / m->kv_scale[2 * l] : 1.0f;
-    a.v_inv = d.kv_fp8 ? 1.0f / m->kv_scale[2 * l + 1] : 1.0f;
+    a.kv8 = d.kv_quant;
+    a.k_inv = d.kv_quant ? 1.0f / m->kv_scale[2 * l] : 1.0f;
+    a.v_inv = d.kv_quant ? 1.0f / m->kv_scale[2 * l + 1] : 1.0f;
     a.kv_b_stride = (int64_t)d.n_kv_heads * d.max_seq * d.head_dim;
     a.kv_t = m->kv_tiled;
     a.seam = m->seam;
@@ -2034,12 +2040,12 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             if (a.pt)  // paged pool: kv head stride 32 * D inside a page
                 return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, 0, 32 * D, B, d.n_heads,
                                                  d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D), m->part_ml,
-                                                 m->part_o, st, true, a.pt, a.pps, a.npages, a.kv_pgs, d.kv_fp8,
+                                                 m->part_o, st, true, a.pt, a.pps, a.npages, a.kv_pgs, d.kv_quant,
                                                  m->kv_scale[2 * l], m->kv_scale[2 * l + 1]);
             return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, a.kv_b_stride, (int64_t)S * D,
                                              B, d.n_heads, d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D),
-                                             m->part_ml, m->part_o, st, m->kv_tiled != 0, nullptr, 0, 0, 0, d.kv_fp8,
-                                             d.kv_fp8 ? m->kv_scale[2 * l] : 1.f, d.kv_fp8 ? m->kv_scale[2 * l + 1] : 1.f);
+                                             m->part_ml, m->part_o, st, m->kv_tiled != 0, nullptr, 0, 0, 0, d.kv_quant,
+                                             d.kv_quant ? m->kv_scale[2 * l] : 1.f, d.kv_quant ? m->kv_scale[2 * l + 1] : 1.f);
         case WF_OP_O:  // h_b = h_a + o_proj(rms_norm(attn_sub_norm)(attn))
             a.w = d.w_o + (int64_t)l * H * wrow_bytes(d.wfmt, H); a.N = H; a.K = H; a.ws0 = wsh[3];
             a.resid = m->h_a; a.out = m->h_b; a.out_stride = H;
@@ -2163,16 +2169,21 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_ALLOC(m->qbuf, 2 * (size_t)B * d.hidden);
     m->kv_tiled = (B >= kDecMfmaMinB && (d.wfmt == WF_FMT_I2S || d.wfmt == WF_FMT_I2S_MFMA) && d.max_seq % 32 == 0) ? 1 : 0;
     m->kv_scale = new float[2 * d.layers];
-    for (int i = 0; i < 2 * d.layers; ++i) m->kv_scale[i] = (d.kv_fp8 && d.kv_scale) ? d.kv_scale[i] : 1.0f;
-    if (d.kv_fp8 && !(m->kv_tiled && d.head_dim == 128)) {
-        set_error("model_create: FP8 K/V needs the batched matrix-core decoder (batch >= %d, I2_S, head_dim 128, "
+    for (int i = 0; i < 2 * d.layers; ++i) m->kv_scale[i] = (d.kv_quant && d.kv_scale) ? d.kv_scale[i] : 1.0f;
+    if (d.kv_quant < WF_KV_BF16 || d.kv_quant > WF_KV_INT8) {
+        set_error("model_create: kv_quant must be WF_KV_BF16, WF_KV_FP8 or WF_KV_INT8 (got %d)", d.kv_quant);
+        wf_model_destroy(m);
+        return WF_EINVAL;
+    }
+    if (d.kv_quant && !(m->kv_tiled && d.head_dim == 128)) {
+        set_error("model_create: FP8 / int8 K/V need the batched matrix-core decoder (batch >= %d, I2_S, head_dim 128, "
                   "max_seq %% 32 == 0)", kDecMfmaMinB);
         wf_model_destroy(m);
         return WF_EINVAL;
     }
     for (int i = 0; i < 2 * d.layers; ++i)
         if (!(m->kv_scale[i] > 0.f) || !std::isfinite(m->kv_scale[i])) {
-            set_error("model_create: FP8 K/V scales must be positive and finite");
+            set_error("model_create: K/V scales must be positive and finite");
             wf_model_destroy(m);
             return WF_EINVAL;
         }
@@ -2386,8 +2397,8 @@ int wf_model_prefill(wf_model* m, const int32_t* tokens, const int32_t* row_slot
         const bool paged = d.page_table != nullptr;
         if ((rc = prefill_attention(m->pf_q, H, a.kc, a.vc, paged ? 0 : a.kv_b_stride, paged ? 32 * D : (int64_t)d.max_seq * D,
                                     d.n_heads, d.n_kv_heads, row_pos, row_slot, rows, 1.0f / sqrtf((float)D), a.pt,
-                                    a.pps, a.npages, a.kv_pgs, m->pf_attn, H, st, d.kv_fp8,
-                                    d.kv_fp8 ? m->kv_scale[2 * l] : 1.f, d.kv_fp8 ? m->kv_scale[2 * l + 1] : 1.f)))
+                                    a.pps, a.npages, a.kv_pgs, m->pf_attn, H, st, d.kv_quant,
+                                    d.kv_quant ? m->kv_scale[2 * l] : 1.f, d.kv_quant ? m->kv_scale[2 * l + 1] : 1.f)))
             return rc;
         // O (+ residual)
         prefill_rownorm(m, m->pf_attn, H, d.attn_sub + (int64_t)l * H, H, rows, st);

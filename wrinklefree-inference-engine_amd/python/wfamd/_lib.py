@@ -17,6 +17,7 @@ LIB_PATH = Path(os.environ.get("WF_BITNET_LIB", PKG_ROOT / "lib" / "libwfbitnet.
 WF_OK, WF_EINVAL, WF_EHIP, WF_ENOTSUP = 0, 1, 2, 3
 WF_F32, WF_BF16, WF_F16, WF_I8, WF_U8 = 0, 1, 2, 3, 4
 WF_FMT_I2S, WF_FMT_TQ, WF_FMT_I2S_MFMA = 0, 1, 2
+WF_KV_BF16, WF_KV_FP8, WF_KV_INT8 = 0, 1, 2  # wf_model_desc.kv_quant
 WF_PREFILL_ROW_GROUP = 32  # include/wf_bitnet.h
 (WF_OP_EMBED, WF_OP_QKV, WF_OP_ATTN, WF_OP_O, WF_OP_GATE_UP, WF_OP_DOWN, WF_OP_LM_HEAD) = range(7)
 
@@ -77,7 +78,7 @@ class WFModelDesc(C.Structure):
                                           "attn_sub", "ffn_sub", "w_qkv", "w_o", "w_gu", "w_d", "wscale",
                                           "tokens", "positions", "logits", "k_cache", "v_cache")] + \
                [("debug_flags", C.c_int), ("page_table", C.c_void_p), ("num_pages", C.c_int),
-                ("kv_fp8", C.c_int), ("kv_scale", C.c_void_p)]
+                ("kv_quant", C.c_int), ("kv_scale", C.c_void_p)]
 
 
 class WFAttnView(C.Structure):

@@ -200,6 +200,21 @@ def from_fp8_codes(c: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
     return c.view(torch.float8_e4m3fn).float() * scale
 
 
+def to_int8_codes(x: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+    """bf16/fp32 values -> int8 codes clamp(rne(x / scale), -127, 127) (stored as uint8 bytes): what
+    the decode step's cache epilogue stores for an int8 K/V cache (the reference's KVCacheDtype.INT8,
+    kv_cache/kv_cache.py:159-185, with a static scale)."""
+    y = torch.round(x.float() / scale).clamp(-127.0, 127.0)
+    return y.to(torch.int8).view(torch.uint8)
+
+
+def from_int8_codes(c: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+    return c.view(torch.int8).float() * scale
+
+
+KV_CODES = {"fp8": (to_fp8_codes, from_fp8_codes), "int8": (to_int8_codes, from_int8_codes)}
+
+
 def pack_prefill_rows(seqs, group: int = _lib.WF_PREFILL_ROW_GROUP):
     """(slot, tokens, start) triples -> the row arrays of wf_model_prefill (tokens, slots,
     positions): each slot's tokens at positions start, start + 1, ..., padded to a multiple of
@@ -289,12 +304,14 @@ class BitNetDecoder:
             self.page_table = torch.zeros((B, cfg.max_seq // 32), dtype=torch.int32, device=self.dev)
         else:
             kv_shape = (L, B, cfg.n_kv_heads, cfg.max_seq, cfg.head_dim)
-        if kv_dtype not in ("bf16", "fp8"):
-            raise ValueError(f"kv_dtype must be 'bf16' or 'fp8', got {kv_dtype!r}")
-        self.kv_fp8 = kv_dtype == "fp8"
+        if kv_dtype not in ("bf16", "fp8", "int8"):
+            raise ValueError(f"kv_dtype must be 'bf16', 'fp8' or 'int8', got {kv_dtype!r}")
+        self.kv_dtype = kv_dtype
+        self.kv_quant = {"bf16": _lib.WF_KV_BF16, "fp8": _lib.WF_KV_FP8, "int8": _lib.WF_KV_INT8}[kv_dtype]
+        self.kv_fp8 = self.kv_quant != _lib.WF_KV_BF16  # one-byte codes (e4m3 or int8)
         if self.kv_fp8 and not self.kv_tiled:
-            raise ValueError("FP8 K/V needs the batched matrix-core decoder (batch >= 16, I2_S, max_seq % 32 == 0)")
-        # FP8: OCP e4m3fn codes as uint8, per-layer (K, V) scales (include/wf_bitnet.h kv_fp8)
+            raise ValueError("FP8 / int8 K/V need the batched matrix-core decoder (batch >= 16, I2_S, max_seq % 32 == 0)")
+        # one-byte codes as uint8 storage, per-layer (K, V) scales (include/wf_bitnet.h kv_quant)
         sc = np.ones((L, 2), dtype=np.float32) if kv_scale is None else np.broadcast_to(
             np.asarray(kv_scale, dtype=np.float32), (L, 2)).copy()
         self.kv_scale = torch.from_numpy(np.ascontiguousarray(sc))
@@ -317,7 +334,7 @@ class BitNetDecoder:
         if self.paged:
             d.page_table, d.num_pages = self.page_table.data_ptr(), int(num_pages)
         if self.kv_fp8:
-            d.kv_fp8, d.kv_scale = 1, self.kv_scale.data_ptr()
+            d.kv_quant, d.kv_scale = self.kv_quant, self.kv_scale.data_ptr()
         self._desc = d
         h = C.c_void_p()
         call("wf_model_create", C.addressof(d), C.addressof(h))
@@ -401,11 +418,11 @@ class BitNetDecoder:
         order; in the tile layouts whole 32-key blocks)."""
         g = torch.Generator(device=self.dev).manual_seed(seed)
         D = self.cfg.head_dim
-        if self.kv_fp8:  # random finite e4m3 codes (the whole store: stale rows are never read)
+        if self.kv_fp8:  # random finite codes (the whole store: stale rows are never read)
+            enc = KV_CODES[self.kv_dtype][0]
             for l in range(self.cfg.layers):
-                for c in (self.k_cache, self.v_cache):
-                    c[l].copy_(torch.randn(c[l].shape, generator=g, device=self.dev).to(torch.float8_e4m3fn)
-                               .view(torch.uint8))
+                for j, c in enumerate((self.k_cache, self.v_cache)):
+                    c[l].copy_(enc(torch.randn(c[l].shape, generator=g, device=self.dev), float(self.kv_scale[l, j])))
             return
         for l in range(self.cfg.layers):
             for c in (self.k_cache, self.v_cache):
@@ -421,10 +438,11 @@ class BitNetDecoder:
         """Write logical K/V [B, Hkv, n, D] into positions [0, n) of a layer (any storage layout).
         Paged: only the first lengths[b] (default n) positions of sequence b, on pages reserved for them."""
         n = k.shape[2]
-        if self.kv_fp8:  # the stored codes: e4m3(clamp(x / scale)), as the step's cache epilogue writes
+        if self.kv_fp8:  # the stored codes, as the step's cache epilogue writes them
             ks, vs = (float(x) for x in self.kv_scale[layer])
-            k = to_fp8_codes(k, ks)
-            v = to_fp8_codes(v, vs)
+            enc = KV_CODES[self.kv_dtype][0]
+            k = enc(k, ks)
+            v = enc(v, vs)
         if self.paged:
             B, H, _, D = k.shape
             nblk = (n + 31) // 32
