@@ -377,13 +377,14 @@ def test_int8_kv_attention_cosine_reference_bar(orc, ctx):
 
 @pytest.mark.parametrize("ctx", [1024, 4096])
 def test_fp8_kv_attention_cosine(orc, ctx):
-    """True OCP e4m3 K/V (the FP8 option) under the same check. The kernels add nothing to the format's
-    own error; e4m3 (3 mantissa bits, any scale) itself gives min 0.9974-0.9980 on these inputs,
-    below the reference's 0.998 -- which its "FP8" option meets only because it stores int8 codes
-    with an absmax scale (kv_cache/kv_cache.py:159-185), i.e. the int8 option above."""
+    """True OCP e4m3 K/V (the FP8 option, scale 1) under the same reference protocol and bar (>= 0.998;
+    measured min 0.9991 at both contexts, int8 0.9998). The kernels add nothing to the format's own
+    error. (With the step's own projected K row in the cache -- |k| far above the N(0, 1) history --
+    e4m3 measured min 0.9974-0.9980: the format's 3 mantissa bits, not the kernels.)"""
     kern16, kern8, fmt, got = _kv_quality(orc, ctx, "fp8")
     assert kern16.min() > 0.99999 and kern8.min() > 0.99999, (kern16.min(), kern8.min())
-    assert abs(got.min() - fmt.min()) < 1e-5 and fmt.min() > 0.997, (got.min(), fmt.min())
+    assert abs(got.min() - fmt.min()) < 1e-5, (got.min(), fmt.min())
+    assert got.min() >= 0.998, (got.min(), got.mean())
 
 
 # ------------------------------------------------------------------------------------------------

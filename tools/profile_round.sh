@@ -31,6 +31,14 @@ timeout -k 10 600 python bench.py --batch 128 --steps 100 --warmup 10 --no-cpu-b
 tail -1 "$O/bench_b128_fp8.log" | cut -c1-200
 timeout -k 10 600 python bench.py --batch 128 --steps 100 --warmup 10 --no-cpu-baseline --kv fp8 --ctx-dist uniform > "$O/bench_b128u_fp8.log" 2>&1 || exit $?
 tail -1 "$O/bench_b128u_fp8.log" | cut -c1-200
+step bench-b128-int8
+timeout -k 10 600 python bench.py --batch 128 --steps 100 --warmup 10 --no-cpu-baseline --kv int8 > "$O/bench_b128_int8.log" 2>&1 || exit $?
+tail -1 "$O/bench_b128_int8.log" | cut -c1-200
+timeout -k 10 600 python bench.py --batch 128 --steps 100 --warmup 10 --no-cpu-baseline --kv int8 --ctx-dist uniform > "$O/bench_b128u_int8.log" 2>&1 || exit $?
+tail -1 "$O/bench_b128u_int8.log" | cut -c1-200
+step kv-quality
+timeout -k 10 600 python -m pytest tests/test_gpu_configs.py -q -s -p no:cacheprovider -k "kv_attention_cosine" > "$O/kv_quality.log" 2>&1 || exit $?
+grep "K/V ctx" "$O/kv_quality.log"
 step bench-b1-tq
 timeout -k 10 600 python bench.py --steps 200 --warmup 10 --no-cpu-baseline --no-gemv --wfmt tq > "$O/bench_b1_tq.log" 2>&1 || exit $?
 tail -1 "$O/bench_b1_tq.log" | cut -c1-200
