@@ -21,7 +21,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 PKG = ROOT / "wrinklefree-inference-engine_amd"
-os.environ["WF_BITNET_LIB"] = str(PKG / "lib" / "libwfbitnet_stamps.so")
+os.environ["WF_BITNET_LIB"] = os.environ.get("WF_STAMPS_LIB", str(PKG / "lib" / "libwfbitnet_stamps.so"))
 sys.path.insert(0, str(PKG / "python"))
 
 import numpy as np  # noqa: E402

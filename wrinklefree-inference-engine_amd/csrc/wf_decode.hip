@@ -94,6 +94,16 @@ __device__ __forceinline__ uint8_t to_fp8(float y) {
     const float c = fminf(fmaxf(y, -448.f), 448.f);
     return (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(c, c, 0, false) & 0xffu);
 }
+// A decode step's K/V cache element store, write-through (sc1). A new key's row lands in the tile
+// layouts as 16 (K) and 128 (V) scattered 2-byte pieces, each dirtying its own cache line: plain
+// stores left ~12 MB of partly dirty lines for the launch boundary to write back (batch 128; the
+// attention launch then started 3.9 us after the QKV launch ended). Write-through: QKV op 13.3 ->
+// 12.5 us, step 4.00 -> 3.96 ms (same-box A/B, round 3).
+template <class T>
+__device__ __forceinline__ void kv_store(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // one-byte K/V code of y (already divided by the layer's scale): kvq 1 = OCP e4m3fn (RNE, saturating),
 // 2 = int8 (the reference's INT8 KVCacheDtype: clamp(rne(y), -127, 127), kv_cache/kv_cache.py:159-185)
 __device__ __forceinline__ uint8_t to_kv8(float y, int kvq) {
@@ -489,17 +499,17 @@ struct EpiDec {
                                 off = (int64_t)slot * g.kv_b_stride + (int64_t)kvh * g.S * 128 +
                                       (proj == 1 ? k_tile_off(pos, d) : v_tile_off(pos, d));
                             }
-                            c8[off] = to_kv8(y * (proj == 1 ? g.k_inv : g.v_inv), g.kv8);
+                            kv_store(c8 + off, to_kv8(y * (proj == 1 ? g.k_inv : g.v_inv), g.kv8));
                             continue;
                         }
                         if (g.pt) {  // paged: block pos >> 5 lives in page pt[slot][pos >> 5]
                             const int pg = min(max(g.pt[(int64_t)slot * g.pps + (pos >> 5)], 0), g.npages - 1);
                             uint16_t* cache = (proj == 1 ? g.kc : g.vc) + pg * g.kv_pgs + (int64_t)kvh * 4096;
-                            cache[proj == 1 ? k_tile_off(pos & 31, d) : v_tile_off(pos & 31, d)] = f2bf(y);
+                            kv_store(cache + (proj == 1 ? k_tile_off(pos & 31, d) : v_tile_off(pos & 31, d)), f2bf(y));
                             continue;
                         }
                         uint16_t* cache = (proj == 1 ? g.kc : g.vc) + (int64_t)slot * g.kv_b_stride + (int64_t)kvh * g.S * 128;
-                        if (g.kv_t) cache[proj == 1 ? k_tile_off(pos, d) : v_tile_off(pos, d)] = f2bf(y);
+                        if (g.kv_t) kv_store(cache + (proj == 1 ? k_tile_off(pos, d) : v_tile_off(pos, d)), f2bf(y));
                         else cache[(int64_t)pos * 128 + d] = f2bf(y);
                     }
                 }

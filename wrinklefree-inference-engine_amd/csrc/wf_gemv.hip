@@ -9,6 +9,7 @@
 
 #include "wf_common.h"
 #include "wf_device.h"
+#include "wf_norm.h"  // stamps (diagnostic build)
 
 namespace wf {
 
@@ -97,38 +98,36 @@ __global__ __launch_bounds__(256) void k_ternary_gemm(const uint8_t* __restrict_
 // ---------------------------------------------------------------------------------------------
 // Standalone GEMV (M = 1; sgl_kernel bitnet_gemv, scripts/benchmark_kernels.py:40-66): a memory-
 // latency problem -- 0.4-4.5 MB per call, i.e. 1.6-17 KB per CU -- so every byte of the matrix is
-// in flight at once and as many CUs as possible take part. Block = 256 threads = 4 waves; the kernel
-// can split a row over W waves (wave kp takes its contiguous 1/W of the row's 16-byte chunks, lane l
-// chunk c0 + l + 64 j), but the launcher uses W = 1 (one wave per row) at every shape: fewer,
-// fuller blocks won over >= 1024 split-row blocks. Issue order: the activation pieces (L2-resident), then every weight chunk of
+// in flight at once and as many CUs as possible take part. One wave per weight row (lane l takes
+// chunks l + 64 j), NW waves per block. Issue order: the activation pieces (L2-resident), then every weight chunk of
 // the lane (nt), then the activation image goes to LDS (conflict-free stripes, wf_device.h) behind
 // one barrier that the weight latency hides. Each wave sums its lanes with DPP; the W wave partials
 // of a row meet in LDS in wave order. Integer sums: bit-exact with any split.
 // ---------------------------------------------------------------------------------------------
 constexpr int kGemvMaxPieces = 2;  // 16-byte activation pieces per thread: K_pad <= 8192
-template <class F, int W, int J>
-__global__ __launch_bounds__(256) void k_gemv_rows(const uint8_t* __restrict__ Wt, const int8_t* __restrict__ A,
-                                                   float scale, int N, int K, float* __restrict__ Y) {
+template <class F, int NW, int J>
+__global__ __launch_bounds__(NW * 64) void k_gemv_rows(const uint8_t* __restrict__ Wt, const int8_t* __restrict__ A,
+                                                       float scale, int N, int K, float* __restrict__ Y) {
     extern __shared__ __attribute__((aligned(16))) int8_t smem[];
-    __shared__ int part[4];
-    constexpr int R = 4 / W;
+    constexpr int NT = NW * 64, MAXP = (8192 / 16 + NT - 1) / NT;  // activation pieces per thread
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int row = blockIdx.x * R + wave / W, kp = wave % W;
-    const int C = F::chunks(K), cw = (C + W - 1) / W, c0 = kp * cw, c1 = min(C, c0 + cw);
+    WF_STAMP(0);
+    const int row = blockIdx.x * NW + wave;
+    const int C = F::chunks(K);
     const int pieces = F::k_pad(K) / 16;
-    uint4 apre[kGemvMaxPieces];
+    uint4 apre[MAXP];
 #pragma unroll
-    for (int i = 0; i < kGemvMaxPieces; ++i) {
-        const int p = min((int)threadIdx.x + 256 * i, pieces - 1), pk = min(p, K / 16 - 1);
+    for (int i = 0; i < MAXP; ++i) {
+        const int p = min((int)threadIdx.x + NT * i, pieces - 1), pk = min(p, K / 16 - 1);
         apre[i] = *reinterpret_cast<const uint4*>(A + 16 * pk);  // pieces >= K/16: zeroed below
     }
     const uint8_t* wr = Wt + (int64_t)min(row, N - 1) * F::row_bytes(K);
     uint4 wv[J];
 #pragma unroll
-    for (int j = 0; j < J; ++j) wv[j] = ldg_nt(wr + (int64_t)min(c0 + lane + 64 * j, C - 1) * 16);
+    for (int j = 0; j < J; ++j) wv[j] = ldg_nt(wr + (int64_t)min(lane + 64 * j, C - 1) * 16);
 #pragma unroll
-    for (int i = 0; i < kGemvMaxPieces; ++i) {
-        const int p = (int)threadIdx.x + 256 * i;
+    for (int i = 0; i < MAXP; ++i) {
+        const int p = (int)threadIdx.x + NT * i;
         if (p < pieces)
             *reinterpret_cast<uint4*>(smem + F::lds_off(16 * p)) = 16 * p < K ? apre[i] : make_uint4(0, 0, 0, 0);
     }
@@ -136,46 +135,42 @@ __global__ __launch_bounds__(256) void k_gemv_rows(const uint8_t* __restrict__ W
     DotAcc<F> dacc;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-        const int c = c0 + lane + 64 * j;
-        if (c < c1) {
+        const int c = lane + 64 * j;
+        if (c < C) {
             Decoded<F> d;
             d.load(wv[j]);
             chunk_dot<F>(d, smem + ((c >> 4) * F::kGroups) * 256 + (c & 15) * 16, dacc);
         }
     }
     const int acc = wave_sum_i(dacc.total());
-    if constexpr (W == 1) {
-        if (lane == 0 && row < N) Y[row] = (float)acc * scale;
-    } else {
-        if (lane == 0) part[wave] = acc;
-        __syncthreads();
-        if (threadIdx.x < R) {
-            const int r = blockIdx.x * R + threadIdx.x;
-            int s = 0;
-#pragma unroll
-            for (int i = 0; i < W; ++i) s += part[threadIdx.x * W + i];
-            if (r < N) Y[r] = (float)s * scale;
-        }
-    }
+    if (lane == 0 && row < N) Y[row] = (float)acc * scale;
+#ifdef WF_STAMPS
+    __syncthreads();  // stamps build: waves 0-3 stamp, so the exit is taken once every wave is done
+#endif
+    WF_STAMP(1);
 }
 
 
 template <class F>
 static int launch_gemv_rows(const uint8_t* w, const int8_t* a, float scale, int N, int K, float* y, hipStream_t st) {
-    const int C = F::chunks(K);
-    // one wave per row at every shape: splitting k/v's and q/o's rows over 2-4 waves to reach >= 1024
-    // blocks was slower (same-box graph replay, tools/gemv_bench.py: q/o 2.91 -> 2.49 us, k/v 2.56 ->
-    // 2.18 us, down 3.27 -> 3.17 us with one wave per row; gate/up already was)
-    const int W = 1;
-    const int cw = (C + W - 1) / W;
-    const int J = (cw + 63) / 64;
+    // one wave per row; NW rows (waves) per block share one LDS activation image. Measured (graph
+    // replay, tools/gemv_bench.py): splitting rows over 2-4 waves to reach >= 1024 blocks was slower
+    // (q/o 2.91 -> 2.49 us, k/v 2.56 -> 2.18, down 3.27 -> 3.17 with one wave per row)
+#ifdef WF_GEMV_WAVES
+    const int NW = WF_GEMV_WAVES;
+#else
+    const int NW = N >= 4096 ? 16 : (N >= 2048 ? 8 : 4);
+#endif
+    const int J = (F::chunks(K) + 63) / 64;
     const int img = lds_image_bytes<F>(K);
-#define WF_GR(WV, JV) \
-    hipLaunchKernelGGL((k_gemv_rows<F, WV, JV>), dim3((N * WV + 3) / 4), dim3(256), (size_t)img, st, w, a, scale, N, K, y)
-#define WF_GRJ(WV)            \
-    if (J == 1) WF_GR(WV, 1); \
-    else WF_GR(WV, 2);
-    WF_GRJ(1)
+    const dim3 grid((N + NW - 1) / NW);
+#define WF_GR(NWV, JV) hipLaunchKernelGGL((k_gemv_rows<F, NWV, JV>), grid, dim3(NWV * 64), (size_t)img, st, w, a, scale, N, K, y)
+#define WF_GRJ(NWV)            \
+    if (J == 1) WF_GR(NWV, 1); \
+    else WF_GR(NWV, 2);
+    if (NW == 16) { WF_GRJ(16) }
+    else if (NW == 8) { WF_GRJ(8) }
+    else { WF_GRJ(4) }
 #undef WF_GRJ
 #undef WF_GR
     return check_launch("gemv_rows");
@@ -407,6 +402,8 @@ static inline int grid_for(int64_t n, int per = 256, int cap = 4096) {
 }
 
 }  // namespace wf
+
+WF_STAMP_READER(wf_debug_stamps_gemv)
 
 using namespace wf;
 
