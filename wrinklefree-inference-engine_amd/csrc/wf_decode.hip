@@ -1825,7 +1825,10 @@ template <int MODE, int PRO, int PP>
 const void* dec_gemm_kernel(int N, int K, int* threads) {
     if (N >= 8192) {  // wide layers (gate|up): 128-column tiles halve the code re-reads
         // 4 waves per block (64 KiB of LDS, two blocks per CU): the 108 x 4 blocks of the 2B
-        // gate|up at batch 128 are resident in one round (8 waves + 128 KiB took two rounds)
+        // gate|up at batch 128 are resident in one round (8 waves + 128 KiB took two rounds).
+        // Measured and not kept (round 3): 32 x 224 tiles, one 4-wave block per CU (248 blocks,
+        // 220 KB of fragments each instead of 2 x 160 KB on 176 CUs): gate|up 16.3 -> 20.2 us per
+        // op -- one wave per SIMD cannot hide its own 28-tile MFMA + decode stream.
         *threads = 4 * 64;
         if constexpr (PRO == 2) return nullptr;  // the attention input is never this wide
         else return reinterpret_cast<const void*>(&k_dec_gemm_t<2, 8, 3, MODE, 4, PRO, PP>);
