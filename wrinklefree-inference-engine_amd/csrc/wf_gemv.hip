@@ -154,22 +154,23 @@ __global__ __launch_bounds__(NW * 64) void k_gemv_rows(const uint8_t* __restrict
 template <class F>
 static int launch_gemv_rows(const uint8_t* w, const int8_t* a, float scale, int N, int K, float* y, hipStream_t st) {
     // one wave per row; NW rows (waves) per block share one LDS activation image. Measured (graph
-    // replay, tools/gemv_bench.py): splitting rows over 2-4 waves to reach >= 1024 blocks was slower
-    // (q/o 2.91 -> 2.49 us, k/v 2.56 -> 2.18, down 3.27 -> 3.17 with one wave per row)
+    // replay, same box, tools/gemv_bench.py, profiles/gemv_ab_r03.txt): splitting rows over 2-4 waves
+    // to reach >= 1024 blocks was slower (q/o 2.91 -> 2.49 us, k/v 2.56 -> 2.18, down 3.27 -> 3.17
+    // with one wave per row); 8 rows per block helps only q/o (2.48 -> 2.43 us); 16 rows for gate|up
+    // (3.08 -> 3.20) and 2 rows for k/v (2.18 -> 2.40) lost.
+    const int J = (F::chunks(K) + 63) / 64;
 #ifdef WF_GEMV_WAVES
     const int NW = WF_GEMV_WAVES;
 #else
-    const int NW = N >= 4096 ? 16 : (N >= 2048 ? 8 : 4);
+    const int NW = (N >= 2048 && N < 4096 && J == 1) ? 8 : 4;
 #endif
-    const int J = (F::chunks(K) + 63) / 64;
     const int img = lds_image_bytes<F>(K);
     const dim3 grid((N + NW - 1) / NW);
 #define WF_GR(NWV, JV) hipLaunchKernelGGL((k_gemv_rows<F, NWV, JV>), grid, dim3(NWV * 64), (size_t)img, st, w, a, scale, N, K, y)
 #define WF_GRJ(NWV)            \
     if (J == 1) WF_GR(NWV, 1); \
     else WF_GR(NWV, 2);
-    if (NW == 16) { WF_GRJ(16) }
-    else if (NW == 8) { WF_GRJ(8) }
+    if (NW == 8) { WF_GRJ(8) }
     else { WF_GRJ(4) }
 #undef WF_GRJ
 #undef WF_GR
