@@ -232,8 +232,10 @@ def test_decode_batch128_paged_full_width_vs_oracle(orc, kv, B):
     # and that row's later layers move by ~1e-2 (tools/diag_ragged_batch.py: batch 40, row 23 at
     # context 12, the same in graph / eager / dense / paged runs; the batch-1 path shows them at ~1.6 %
     # of positions, test_prefill_8x2048_full_width_vs_oracle)
+    # a flip stays in that row's cache (its later steps read the moved K/V): count first flips per row
+    events = len({b for _, b, _, _, _ in flips})
     print(f"batch {B} paged {kv}: worst logits rel-L2 {worst:.2e} over rows {rows}; isolated flips {flips}")
-    assert len(flips) <= max(1, checks // 10), flips
+    assert events <= max(1, checks // 10), flips
 
 
 # ------------------------------------------------------------------------------------------------
