@@ -1637,13 +1637,12 @@ __global__ __launch_bounds__(256) void k_lm_head(const uint16_t* __restrict__ E,
 #pragma unroll
     for (int m = 0; m < MB; ++m) acc[m] = 0.f;
     for (int c0 = 0; c0 < C; c0 += 64) {
-        // the next 64 chunks are in flight while these are consumed (one HBM round trip per row
-        // instead of one per 64 chunks)
-        uint4 wn[4];
+        if (c0 > 0) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int c = c0 + 64 + 16 * u + sub;
-            wn[u] = (c < C) ? ldg_nt(reinterpret_cast<const uint8_t*>(er + 8 * c)) : make_uint4(0, 0, 0, 0);
+            for (int u = 0; u < 4; ++u) {
+                const int c = c0 + 16 * u + sub;
+                w[u] = (c < C) ? ldg_nt(reinterpret_cast<const uint8_t*>(er + 8 * c)) : make_uint4(0, 0, 0, 0);
+            }
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -1662,8 +1661,6 @@ __global__ __launch_bounds__(256) void k_lm_head(const uint16_t* __restrict__ E,
                 }
             }
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) w[u] = wn[u];
     }
     WF_STAMP(2);
 #pragma unroll
