@@ -424,10 +424,12 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
                 }
             }
         };
+        // block-uniform guards: only chunks that hold keys are loaded (a dead load still costs its
+        // latency where its destination registers are next written)
         for (int c0 = t0; c0 < t1; c0 += 2 * CH) {
-            load(kB, vB, c0 + CH);  // next chunk in flight while this one is computed
+            if (c0 + CH < t1) load(kB, vB, c0 + CH);  // next chunk in flight while this one is computed
             compute(kA, vA, c0);
-            load(kA, vA, c0 + 2 * CH);
+            if (c0 + 2 * CH < t1) load(kA, vA, c0 + 2 * CH);
             if (c0 + CH < t1) compute(kB, vB, c0 + CH);
         }
     }
