@@ -67,6 +67,18 @@ int wf_bitnet_gemm_ex(int fmt, const uint8_t* w, const int8_t* a, int64_t lda, f
 int64_t wf_bitnet_linear_ws_bytes(int M, int K);
 int wf_bitnet_linear(int fmt, const uint8_t* w, const uint16_t* x, int64_t ldx, float ws, int M, int N, int K,
                      uint16_t* y, int64_t ldy, void* workspace, void* stream);
+/* Fused projections with ONE shared activation quantization ("shared quantize
+ * across fused QKV / gate-up"; the reference's attempted bitnet_qkv_forward_cpu / bitnet_mlp_forward_cpu,
+ * docs/research/sglang_optimization_plan.md:326-331, and the q|k|v / gate|up projections of
+ * scripts/direct_inference_full.py:212-214,254-256 that quantize the same input 3x / 2x). The nseg
+ * (1..3) layers' packed weights are row-concatenated in w (segment s = the next n[s] rows, same format
+ * and K), each with its own weight scale ws[s] and bf16 output y[s] (device pointer, row stride
+ * ldy[s]); n, ws, y, ldy are host arrays of nseg entries. y[s] equals wf_bitnet_linear on segment s
+ * bit for bit. M < 16: one launch for all segments; M >= 16 (I2_S): one row quantization and one
+ * int8-MFMA GEMM over all segments (workspace of wf_bitnet_linear_ws_bytes(M, K) bytes). */
+int wf_bitnet_linear_fused(int fmt, const uint8_t* w, int nseg, const int* n, const float* ws, const uint16_t* x,
+                           int64_t ldx, int M, int K, uint16_t* const* y, const int64_t* ldy, void* workspace,
+                           void* stream);
 /* kernels/native.py:27-65 (wrinklefree_inference.kernels.native gemv/gemm): signed (bits-1) dot
  * on the LSB-interleaved layout byte[j] = w[4j] | w[4j+1]<<2 | ..., float(sum) * scale. */
 int wf_bitnet_gemm_lsb(const uint8_t* w, const int8_t* a, float scale, int M, int N, int K, float* y, void* stream);

@@ -461,6 +461,43 @@ def test_bitnet_linear_rows_vs_oracle(orc, m, n, k):
         assert np.array_equal(out[r], ref), r
 
 
+@pytest.mark.parametrize("m,k,rows,fmt", [(1, 2560, (2560, 640, 640), 0), (5, 2560, (6912, 6912), 0),
+                                           (1, 2560, (2560, 640, 640), 1), (3, 6912, (2560,), 1),
+                                           (16, 2560, (2560, 640, 640), 0), (130, 2560, (6912, 6912), 0),
+                                           (40, 640, (136, 40, 8), 0)])
+def test_bitnet_linear_fused_vs_oracle(orc, m, k, rows, fmt):
+    """wf_bitnet_linear_fused (q|k|v, gate|up: one shared activation quantization):
+    every segment bf16 bit-exact with the oracle's per-row linear on that segment's weights and
+    scale, and with ops.bitnet_linear on the segment alone; M < 16 (one GEMV launch, I2_S and TQ),
+    M >= 16 (one row quantizer + one int8-MFMA GEMM over all segments), ragged segments, strided rows."""
+    from wfamd import ops
+    from wfamd._lib import WF_FMT_TQ
+    from wfamd.linear import BitNetFusedLinear, BitNetLinear
+    rng = np.random.default_rng(m * 7 + k + sum(rows))
+    ws = [1.25 + 0.25 * i for i in range(len(rows))]
+    ps = [orc.pack_i2s(rng.integers(-1, 2, size=(n, k)).astype(np.float32)) for n in rows]
+    x = (rng.standard_normal((m, k + 32)) * rng.uniform(0.05, 3.0, size=(m, 1))).astype(np.float32)
+    xb = orc.f32_to_bf16(x)
+    xt = cu(xb.view(np.int16)).view(torch.bfloat16)[:, :k]  # row stride k + 32
+    packed = torch.cat([cu(p) for p in ps], dim=0)
+    if fmt == WF_FMT_TQ:
+        packed = torch.cat([ops.i2s_to_tq(cu(p)) for p in ps], dim=0)
+    outs = ops.bitnet_linear_fused(xt, packed, rows, ws, fmt, in_features=k)
+    layers = [BitNetLinear(k, n, ops.i2s_to_tq(cu(p)) if fmt == WF_FMT_TQ else cu(p), w, fmt)
+              for n, p, w in zip(rows, ps, ws)]
+    mod = BitNetFusedLinear(layers)(xt)
+    for s, (n, p, w) in enumerate(zip(rows, ps, ws)):
+        got = bits(outs[s])
+        assert got.shape == (m, n)
+        assert np.array_equal(got, bits(mod[s])), s
+        assert np.array_equal(got, bits(layers[s](xt))), s
+        for r in ([0, m - 1] if m > 16 else range(m)):
+            ref = orc.bitnet_linear_bf16(np.ascontiguousarray(xb[r, :k]), p, w)
+            assert np.array_equal(got[r], ref), (s, r)
+    with pytest.raises(ValueError):
+        ops.bitnet_linear_fused(xt, packed, [rows[0] + 16] + list(rows[1:]), ws, fmt, in_features=k)
+
+
 def test_bitnet_linear_module_and_errors():
     from wfamd import ops
     from wfamd._lib import WF_FMT_TQ

@@ -63,7 +63,9 @@ struct GemvArgs {
     const uint16_t* resid;     // O/DN residual input [B, out_stride]
     uint16_t* out;             // O/DN hidden out; GU act; QKV q
     int64_t out_stride;
-    // QKV extras
+    // QKV extras (MODE_LINEAR: row segments of wf_bitnet_linear_fused -- rows [0, Hq) scale ws0 ->
+    // out / out_stride, [Hq, Hq + Hkv) ws1 -> kc / kv_b_stride, [Hq + Hkv, N) ws2 -> vc / kv_pgs; see
+    // lin_seg())
     int Hq, Hkv, S;
     const int32_t* positions;
     int* ws;                   // batched decode: split-K int32 partials
@@ -109,6 +111,20 @@ __device__ __forceinline__ void kv_store(T* p, T v) {
 __device__ __forceinline__ uint8_t to_kv8(float y, int kvq) {
     if (kvq == 2) return (uint8_t)(int8_t)(int)fminf(fmaxf(__builtin_rintf(y), -127.f), 127.f);
     return to_fp8(y);
+}
+
+// MODE_LINEAR output n -> its row segment (wf_bitnet_linear_fused; one segment: Hq = N): the
+// segment's weight scale, output base, row stride and column within the segment
+struct LinSeg {
+    float ws;
+    uint16_t* out;
+    int64_t ld;
+    int col;
+};
+__device__ __forceinline__ LinSeg lin_seg(const GemvArgs& a, int n) {
+    if (n < a.Hq) return {a.ws0, a.out, a.out_stride, n};
+    if (n < a.Hq + a.Hkv) return {a.ws1, a.kc, a.kv_b_stride, n - a.Hq};
+    return {a.ws2, a.vc, a.kv_pgs, n - a.Hq - a.Hkv};
 }
 
 // Reference correction (direct_inference_full.py:201-208) for one output:
@@ -316,13 +332,16 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
         // BitNetLinear (direct_inference_full.py:186-208): y = bf16(fl32(fl32(raw - ws*sum(q)) * s))
         if (sub == 0) {
 #pragma unroll
-            for (int m = 0; m < MB; ++m) s_out[m][lrow] = corrected(acc[m], a.ws0, asum[m], sf[m]);
+            for (int m = 0; m < MB; ++m) s_out[m][lrow] = corrected(acc[m], lin_seg(a, row).ws, asum[m], sf[m]);
         }
         __syncthreads();
         if (threadIdx.x < MB * RPB) {
             const int m = threadIdx.x / RPB, i = threadIdx.x % RPB;
             const int n = blockIdx.x * RPB + i;
-            if (n < N) a.out[(int64_t)(b0 + m) * a.out_stride + n] = f2bf(s_out[m][i]);
+            if (n < N) {
+                const LinSeg g = lin_seg(a, n);
+                g.out[(int64_t)(b0 + m) * g.ld + g.col] = f2bf(s_out[m][i]);
+            }
         }
     } else {
         // O/DN: out[row] = bf16(resid + bf16(o)); GU: act[8t+i] = bf16(bf16(relu(g)^2) * u)
@@ -1226,10 +1245,11 @@ struct EpiLinear {
         const GemvArgs& g = *a;
         const int n = c0 + l16;
         if (n >= g.N) return;
+        const LinSeg sg = lin_seg(g, n);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int m = r0 + 4 * q + r;
-            if (m < g.B) g.out[(int64_t)m * g.out_stride + n] = f2bf(corrected(acc[r], g.ws0, g.act_sum[m], g.act_sf[m]));
+            if (m < g.B) sg.out[(int64_t)m * sg.ld + sg.col] = f2bf(corrected(acc[r], sg.ws, g.act_sum[m], g.act_sf[m]));
         }
     }
 };
@@ -2441,18 +2461,30 @@ int64_t wf_bitnet_linear_ws_bytes(int M, int K) {
 // BitNetLinear.forward (scripts/direct_inference_full.py:186-208): per-row int8 quantization of x,
 // ternary GEMM, the reference's correction, bf16 out. One launch for M < 16 (quantize in the GEMV
 // prologue), else a quantize launch + the int8-MFMA GEMM (I2_S).
-int wf_bitnet_linear(int fmt, const uint8_t* w, const uint16_t* x, int64_t ldx, float ws, int M, int N, int K,
-                     uint16_t* y, int64_t ldy, void* workspace, void* stream) {
-    WF_REQUIRE(w && x && y, "bitnet_linear: null pointer");
-    WF_REQUIRE(M > 0 && N > 0 && K > 0 && K % 128 == 0, "bitnet_linear: bad shape M=%d N=%d K=%d (K %% 128 == 0)", M, N, K);
+int wf_bitnet_linear_fused(int fmt, const uint8_t* w, int nseg, const int* n, const float* ws, const uint16_t* x,
+                           int64_t ldx, int M, int K, uint16_t* const* y, const int64_t* ldy, void* workspace,
+                           void* stream) {
+    WF_REQUIRE(w && x && n && ws && y && ldy, "bitnet_linear: null pointer");
+    WF_REQUIRE(nseg >= 1 && nseg <= 3, "bitnet_linear_fused: 1..3 segments (got %d)", nseg);
+    int N = 0;
+    for (int s = 0; s < nseg; ++s) {
+        WF_REQUIRE(n[s] > 0 && y[s] && ldy[s] >= n[s], "bitnet_linear_fused: segment %d: bad rows / output / stride", s);
+        N += n[s];
+    }
+    WF_REQUIRE(M > 0 && K > 0 && K % 128 == 0, "bitnet_linear: bad shape M=%d N=%d K=%d (K %% 128 == 0)", M, N, K);
     WF_REQUIRE(fmt == WF_FMT_I2S || fmt == WF_FMT_TQ, "bitnet_linear: unknown weight format %d", fmt);
     const int kp = fmt == WF_FMT_TQ ? FmtTQ::k_pad(K) : FmtI2S::k_pad(K);
     WF_REQUIRE(kp <= 8192, "bitnet_linear: K > 8192 not supported");
-    WF_REQUIRE(ldx >= K && ldx % 8 == 0 && ldy >= N && aligned16(x) && aligned16(w), "bitnet_linear: bad strides / alignment");
+    WF_REQUIRE(ldx >= K && ldx % 8 == 0 && aligned16(x) && aligned16(w), "bitnet_linear: bad strides / alignment");
     hipStream_t st = as_stream(stream);
     GemvArgs a{};
-    a.w = w; a.N = N; a.K = K; a.B = M; a.ws0 = ws; a.out = y; a.out_stride = ldy;
+    a.w = w; a.N = N; a.K = K; a.B = M;
     a.x = x; a.x_stride = ldx;
+    // row segments (lin_seg): [0, Hq) -> out, [Hq, Hq + Hkv) -> kc, the rest -> vc
+    a.Hq = n[0]; a.ws0 = ws[0]; a.out = y[0]; a.out_stride = ldy[0];
+    a.Hkv = nseg > 1 ? n[1] : 0;
+    if (nseg > 1) { a.ws1 = ws[1]; a.kc = y[1]; a.kv_b_stride = ldy[1]; }
+    if (nseg > 2) { a.ws2 = ws[2]; a.vc = y[2]; a.kv_pgs = ldy[2]; }
     if (M < kDecMfmaMinB || fmt != WF_FMT_I2S) {
         constexpr int LPR = 32, RPB = kNT / LPR;
         const dim3 grid((N + RPB - 1) / RPB, M);
@@ -2472,6 +2504,14 @@ int wf_bitnet_linear(int fmt, const uint8_t* w, const uint16_t* x, int64_t ldx, 
     a.q8 = q8; a.q8_stride = q8s; a.act_sf = sf; a.act_sum = asum;
     hipLaunchKernelGGL(k_linear_mfma, dim3((N + 127) / 128, (M + 127) / 128), dim3(256), 0, st, a);
     return check_launch("bitnet_linear");
+}
+
+int wf_bitnet_linear(int fmt, const uint8_t* w, const uint16_t* x, int64_t ldx, float ws, int M, int N, int K,
+                     uint16_t* y, int64_t ldy, void* workspace, void* stream) {
+    WF_REQUIRE(N > 0, "bitnet_linear: bad shape M=%d N=%d K=%d (K %% 128 == 0)", M, N, K);
+    uint16_t* const ys[1] = {y};
+    const int64_t lds[1] = {ldy};
+    return wf_bitnet_linear_fused(fmt, w, 1, &N, &ws, x, ldx, M, K, ys, lds, workspace, stream);
 }
 
 int wf_model_graph_launch(wf_model* m, void* stream) {

@@ -50,3 +50,30 @@ class BitNetLinear(nn.Module):
     def extra_repr(self) -> str:
         fmt = "i2s" if self.fmt == WF_FMT_I2S else "tq"
         return f"in_features={self.in_features}, out_features={self.out_features}, fmt={fmt}"
+
+
+class BitNetFusedLinear(nn.Module):
+    """Two or three BitNetLinear layers that read the same input (q|k|v, gate|up) as ONE op with one
+    shared activation quantization (include/wf_bitnet.h wf_bitnet_linear_fused).
+    forward returns a tuple with one bf16 tensor per layer, each bit-identical to that layer alone."""
+
+    def __init__(self, layers: "list[BitNetLinear]"):
+        super().__init__()
+        if not 1 <= len(layers) <= 3:
+            raise ValueError("BitNetFusedLinear takes 1..3 layers")
+        k, fmt = layers[0].in_features, layers[0].fmt
+        if any(l.in_features != k or l.fmt != fmt for l in layers):
+            raise ValueError("fused layers must share in_features and the weight format")
+        self.in_features = k
+        self.fmt = fmt
+        self.rows = [l.out_features for l in layers]
+        self.weight_scales = [l.weight_scale for l in layers]
+        self.register_buffer("packed_weight", torch.cat([l.packed_weight for l in layers], dim=0).contiguous())
+
+    def forward(self, x: torch.Tensor):
+        return tuple(ops.bitnet_linear_fused(x, self.packed_weight, self.rows, self.weight_scales, self.fmt,
+                                             self.in_features))
+
+    def extra_repr(self) -> str:
+        return f"in_features={self.in_features}, rows={self.rows}, fmt={'i2s' if self.fmt == WF_FMT_I2S else 'tq'}"
+

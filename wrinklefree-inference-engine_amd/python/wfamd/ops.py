@@ -8,8 +8,9 @@ RuntimeError (KernelError) for HIP failures.
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
-from typing import Optional, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 
@@ -159,6 +160,44 @@ def bitnet_linear(x: torch.Tensor, packed: torch.Tensor, weight_scale: float, fm
              y.data_ptr(), n, _ptr(ws), _stream())
     out = y.reshape(*x.shape[:-1], n)
     return out.cpu() if host else out
+
+
+def bitnet_linear_fused(x: torch.Tensor, packed: torch.Tensor, rows: Sequence[int], weight_scales: Sequence[float],
+                        fmt: int = WF_FMT_I2S, in_features: Optional[int] = None) -> List[torch.Tensor]:
+    """Several BitNetLinear layers on the same input with one shared activation quantization
+    (include/wf_bitnet.h wf_bitnet_linear_fused; SURVEY §8f rank 1: fused q|k|v, gate|up).
+    `packed` holds the layers' packed weights row-concatenated ([sum(rows), row bytes]); returns one
+    bf16 tensor [..., rows[s]] per layer, each bit-identical to bitnet_linear on that layer."""
+    if x.dtype != torch.bfloat16:
+        raise ValueError(f"bitnet_linear_fused expects bf16 activations, got {x.dtype}")
+    rows = [int(r) for r in rows]
+    if not 1 <= len(rows) <= 3 or len(weight_scales) != len(rows) or min(rows) <= 0:
+        raise ValueError("bitnet_linear_fused: 1..3 layers, one positive row count and one scale each")
+    k = x.shape[-1] if in_features is None else in_features
+    _check_packed(packed, k, fmt)
+    if packed.shape[0] != sum(rows):
+        raise ValueError(f"packed weights have {packed.shape[0]} rows, the layers {sum(rows)}")
+    if x.shape[-1] != k:
+        raise ValueError(f"activations have {x.shape[-1]} features, weights expect {k}")
+    host = not (packed.is_cuda and x.is_cuda)
+    w = _on_device(packed)
+    x2 = _on_device(x.reshape(-1, k))
+    if x2.stride(1) != 1 or x2.stride(0) % 8 != 0 or x2.data_ptr() % 16 != 0:
+        x2 = x2.contiguous()
+    m = x2.shape[0]
+    ys = [torch.empty((m, r), dtype=torch.bfloat16, device=w.device) for r in rows]
+    if m > 0:
+        ns = len(rows)
+        nws = int(_lib.load().wf_bitnet_linear_ws_bytes(m, k))
+        ws = torch.empty(nws, dtype=torch.uint8, device=w.device) if m >= 16 else None
+        c_n = (C.c_int * ns)(*rows)
+        c_s = (C.c_float * ns)(*[float(v) for v in weight_scales])
+        c_y = (C.c_void_p * ns)(*[y.data_ptr() for y in ys])
+        c_l = (C.c_int64 * ns)(*rows)
+        call("wf_bitnet_linear_fused", fmt, w.data_ptr(), ns, C.addressof(c_n), C.addressof(c_s), x2.data_ptr(),
+             x2.stride(0), m, k, C.addressof(c_y), C.addressof(c_l), _ptr(ws), _stream())
+    outs = [y.reshape(*x.shape[:-1], y.shape[1]) for y in ys]
+    return [o.cpu() for o in outs] if host else outs
 
 
 # ---------------------------------------------------------------------------------------------
