@@ -79,6 +79,17 @@ int wf_bitnet_linear(int fmt, const uint8_t* w, const uint16_t* x, int64_t ldx, 
 int wf_bitnet_linear_fused(int fmt, const uint8_t* w, int nseg, const int* n, const float* ws, const uint16_t* x,
                            int64_t ldx, int M, int K, uint16_t* const* y, const int64_t* ldy, void* workspace,
                            void* stream);
+/* BitNet MLP (scripts/direct_inference_full.py:252-265; the reference's attempted
+ * bitnet_mlp_forward_cpu, docs/research/sglang_optimization_plan.md:326-331): for each row of x
+ * (bf16 [M, H], the post-attention-normed hidden state), y = down(rms_norm(relu(gate(x))^2 * up(x),
+ * ffn_sub_norm)) with BitNetLinear gate / up / down (gate|up: one shared quantization, weights
+ * row-concatenated [gate; up] as wf_bitnet_linear_fused), bf16 between ops as the reference. y bf16
+ * [M, H] (row stride ldy); H, I multiples of 128, I <= 8192; workspace of wf_bitnet_mlp_ws_bytes(M, H, I)
+ * bytes, 256-byte aligned. Four launches below 16 rows, six above. */
+int64_t wf_bitnet_mlp_ws_bytes(int M, int H, int I);
+int wf_bitnet_mlp(int fmt, const uint8_t* w_gate_up, const uint8_t* w_down, float ws_gate, float ws_up,
+                  float ws_down, const uint16_t* ffn_sub_norm, float eps, const uint16_t* x, int64_t ldx, int M, int H,
+                  int I, uint16_t* y, int64_t ldy, void* workspace, void* stream);
 /* kernels/native.py:27-65 (wrinklefree_inference.kernels.native gemv/gemm): signed (bits-1) dot
  * on the LSB-interleaved layout byte[j] = w[4j] | w[4j+1]<<2 | ..., float(sum) * scale. */
 int wf_bitnet_gemm_lsb(const uint8_t* w, const int8_t* a, float scale, int M, int N, int K, float* y, void* stream);

@@ -48,6 +48,7 @@ def _load(path: Path):
     L = C.CDLL(str(path))
     vp, i32, i64, f32 = C.c_void_p, C.c_int, C.c_int64, C.c_float
     sig = {
+        "orc_rmsnorm_bf16": [vp, vp, i32, f32, vp],
         "orc_pack_i2s": [vp, i32, i32, vp], "orc_unpack_i2s": [vp, i32, i32, vp],
         "orc_unpack_hf": [vp, i32, i32, vp], "orc_pack_lsb": [vp, i32, i32, vp],
         "orc_unpack_lsb": [vp, i32, i32, vp], "orc_pack_tq": [vp, i32, i32, vp],
@@ -206,6 +207,15 @@ def bitnet_linear_bf16(x_bits: np.ndarray, p: np.ndarray, ws: float) -> np.ndarr
     p = np.ascontiguousarray(p, dtype=np.uint8)
     y = np.zeros(p.shape[0], np.uint16)
     _ck(lib().orc_bitnet_linear_bf16(_p(x_bits), _p(p), float(ws), p.shape[0], x_bits.shape[0], _p(y)), "linear")
+    return y
+
+
+def rms_norm_bf16(x_bits: np.ndarray, w_bits: np.ndarray, eps: float) -> np.ndarray:
+    """rms_norm of one bf16 row (scripts/direct_inference_full.py:181-184; the decode step's norm)."""
+    x_bits = np.ascontiguousarray(x_bits, dtype=np.uint16)
+    w_bits = np.ascontiguousarray(w_bits, dtype=np.uint16)
+    y = np.zeros(x_bits.shape[0], np.uint16)
+    _ck(lib().orc_rmsnorm_bf16(_p(x_bits), _p(w_bits), x_bits.shape[0], float(eps), _p(y)), "rmsnorm")
     return y
 
 

@@ -498,6 +498,42 @@ def test_bitnet_linear_fused_vs_oracle(orc, m, k, rows, fmt):
         ops.bitnet_linear_fused(xt, packed, [rows[0] + 16] + list(rows[1:]), ws, fmt, in_features=k)
 
 
+@pytest.mark.parametrize("m,h,i,fmt", [(1, 2560, 6912, 0), (3, 512, 1536, 1), (20, 512, 1536, 0), (1, 2560, 6912, 1)])
+def test_bitnet_mlp_vs_oracle(orc, m, h, i, fmt):
+    """wf_bitnet_mlp (BitNetMLP) against the reference's mlp() (scripts/direct_inference_full.py:252-265)
+    composed from the oracle: per row gate / up = BitNetLinear (bit-exact pieces), act =
+    bf16(bf16(relu(gate)^2) * up), rms_norm(ffn_sub_norm) (oracle orc_rmsnorm_bf16, double sum), down.
+    The GPU's fp32 norm sum can move one activation across a bf16 / int8 rounding boundary, so the bar
+    is rel-L2 <= 2e-3 per row (the decode step's 1e-3 at the logits), most rows bit-exact."""
+    from wfamd import ops
+    from wfamd._lib import WF_FMT_TQ
+    from wfamd.linear import BitNetLinear, BitNetMLP
+    rng = np.random.default_rng(m + h + i + fmt)
+    ws = (1.6, 1.8, 1.7)
+    pg, pu = (orc.pack_i2s(rng.integers(-1, 2, size=(i, h)).astype(np.float32)) for _ in range(2))
+    pd = orc.pack_i2s(rng.integers(-1, 2, size=(h, i)).astype(np.float32))
+    fw = orc.f32_to_bf16(rng.uniform(0.5, 1.5, size=i).astype(np.float32))
+    xb = orc.f32_to_bf16(rng.standard_normal((m, h)).astype(np.float32))
+    dev = lambda p: ops.i2s_to_tq(cu(p)) if fmt == WF_FMT_TQ else cu(p)  # noqa: E731
+    layers = [BitNetLinear(h, i, dev(pg), ws[0], fmt), BitNetLinear(h, i, dev(pu), ws[1], fmt),
+              BitNetLinear(i, h, dev(pd), ws[2], fmt)]
+    mlp = BitNetMLP(*layers, cu(fw.view(np.int16)).view(torch.bfloat16), eps=1e-5)
+    xt = cu(xb.view(np.int16)).view(torch.bfloat16)
+    got = bits(mlp(xt))
+    exact = 0
+    for r in range(m):
+        g = orc.bf16_to_f32(orc.bitnet_linear_bf16(xb[r], pg, ws[0]))
+        u = orc.bf16_to_f32(orc.bitnet_linear_bf16(xb[r], pu, ws[1]))
+        sq = orc.bf16_to_f32(orc.f32_to_bf16(np.maximum(g, 0) * np.maximum(g, 0)))
+        act = orc.f32_to_bf16(sq * u)
+        ref = orc.bitnet_linear_bf16(orc.rms_norm_bf16(act, fw, 1e-5), pd, ws[2])
+        a, b = orc.bf16_to_f32(got[r]), orc.bf16_to_f32(ref)
+        e = float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+        assert e <= 2e-3, (r, e)
+        exact += int(np.array_equal(got[r], ref))
+    assert exact >= (m + 1) // 2, (exact, m)
+
+
 def test_bitnet_linear_module_and_errors():
     from wfamd import ops
     from wfamd._lib import WF_FMT_TQ

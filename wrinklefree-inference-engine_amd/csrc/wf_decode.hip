@@ -1259,6 +1259,22 @@ __global__ __launch_bounds__(256) void k_linear_mfma(GemvArgs a) {
     tgemm_tile<2, kTgStagesWide>(a.w, a.q8, a.q8_stride, a.B, a.N, a.K, blockIdx.y * 128, blockIdx.x * 128, lds, e);
 }
 // per-row activation quantizer of BitNetLinear: codes, float scale, code sum
+// BitNet MLP activation (direct_inference_full.py:258): g <- bf16(bf16(relu(g)^2) * u), 8 elements per
+// thread (n % 8 == 0, 16-byte aligned rows)
+__global__ __launch_bounds__(256) void k_relu2_mul(uint16_t* __restrict__ g, const uint16_t* __restrict__ u, int64_t n8) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n8) return;
+    const uint4 gv = reinterpret_cast<const uint4*>(g)[i], uv = reinterpret_cast<const uint4*>(u)[i];
+    const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w}, uw[4] = {uv.x, uv.y, uv.z, uv.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float g0 = fmaxf(bf_lo(gw[j]), 0.f), g1 = fmaxf(bf_hi(gw[j]), 0.f);
+        o[j] = pk_bf16(rbf(rbf(g0 * g0) * bf_lo(uw[j])), rbf(rbf(g1 * g1) * bf_hi(uw[j])));
+    }
+    reinterpret_cast<uint4*>(g)[i] = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 template <int PPT>
 __global__ __launch_bounds__(kNT) void k_quant_rows_lin(const uint16_t* __restrict__ x, int64_t xs, int K,
                                                         int8_t* __restrict__ q8, int64_t q8s, float* __restrict__ sf,
@@ -2512,6 +2528,46 @@ int wf_bitnet_linear(int fmt, const uint8_t* w, const uint16_t* x, int64_t ldx, 
     uint16_t* const ys[1] = {y};
     const int64_t lds[1] = {ldy};
     return wf_bitnet_linear_fused(fmt, w, 1, &N, &ws, x, ldx, M, K, ys, lds, workspace, stream);
+}
+
+int64_t wf_bitnet_mlp_ws_bytes(int M, int H, int I) {
+    if (M <= 0 || H <= 0 || I <= 0) return 0;
+    const int64_t act = ((int64_t)M * I * 2 + 255) / 256 * 256;
+    return 2 * act + std::max(wf_bitnet_linear_ws_bytes(M, H), wf_bitnet_linear_ws_bytes(M, I));
+}
+
+// BitNet MLP (direct_inference_full.py:252-265): gate|up with one shared quantization, relu(g)^2 * u,
+// rms_norm(ffn_sub_norm), down -- the reference's attempted bitnet_mlp_forward_cpu as one call.
+int wf_bitnet_mlp(int fmt, const uint8_t* w_gate_up, const uint8_t* w_down, float ws_gate, float ws_up,
+                  float ws_down, const uint16_t* ffn_sub_norm, float eps, const uint16_t* x, int64_t ldx, int M, int H,
+                  int I, uint16_t* y, int64_t ldy, void* workspace, void* stream) {
+    WF_REQUIRE(w_gate_up && w_down && ffn_sub_norm && x && y && workspace, "bitnet_mlp: null pointer");
+    WF_REQUIRE(((uintptr_t)workspace & 255) == 0, "bitnet_mlp: workspace of wf_bitnet_mlp_ws_bytes() bytes, 256-byte aligned");
+    WF_REQUIRE(M > 0 && H > 0 && I > 0 && H % 128 == 0 && I % 128 == 0 && I <= 8192,
+               "bitnet_mlp: bad shape M=%d H=%d I=%d (multiples of 128, I <= 8192)", M, H, I);
+    WF_REQUIRE(aligned16(ffn_sub_norm), "bitnet_mlp: ffn_sub_norm must be 16-byte aligned");
+    hipStream_t st = as_stream(stream);
+    const int64_t act = ((int64_t)M * I * 2 + 255) / 256 * 256;
+    uint16_t* g = reinterpret_cast<uint16_t*>(workspace);
+    uint16_t* u = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(workspace) + act);
+    void* lin_ws = reinterpret_cast<uint8_t*>(workspace) + 2 * act;
+    const int n[2] = {I, I};
+    const float ws[2] = {ws_gate, ws_up};
+    uint16_t* const ys[2] = {g, u};
+    const int64_t lds[2] = {I, I};
+    int rc = wf_bitnet_linear_fused(fmt, w_gate_up, 2, n, ws, x, ldx, M, H, ys, lds, lin_ws, stream);
+    if (rc) return rc;
+    const int64_t n8 = (int64_t)M * I / 8;
+    hipLaunchKernelGGL(k_relu2_mul, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, st, g, u, n8);
+    // rms_norm(ffn_sub_norm) of the activation rows (the decode step's row norm) -> u
+    if (norm_ppt(I) == 1)
+        hipLaunchKernelGGL((k_rownorm<1, true, false>), dim3(M), dim3(kNT), 0, st, g, (int64_t)I, ffn_sub_norm, I, eps,
+                           nullptr, (int64_t)0, nullptr, nullptr, u, (int64_t)I);
+    else
+        hipLaunchKernelGGL((k_rownorm<2, true, false>), dim3(M), dim3(kNT), 0, st, g, (int64_t)I, ffn_sub_norm, I, eps,
+                           nullptr, (int64_t)0, nullptr, nullptr, u, (int64_t)I);
+    if ((rc = check_launch("bitnet_mlp"))) return rc;
+    return wf_bitnet_linear(fmt, w_down, u, I, ws_down, M, H, I, y, ldy, lin_ws, stream);
 }
 
 int wf_model_graph_launch(wf_model* m, void* stream) {

@@ -35,6 +35,8 @@ SIGNATURES = {
     "wf_bitnet_linear_ws_bytes": (i64, [i32, i32]),
     "wf_bitnet_linear": (i32, [i32, vp, vp, i64, f32, i32, i32, i32, vp, i64, vp, vp]),
     "wf_bitnet_linear_fused": (i32, [i32, vp, i32, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp]),
+    "wf_bitnet_mlp_ws_bytes": (i64, [i32, i32, i32]),
+    "wf_bitnet_mlp": (i32, [i32, vp, vp, f32, f32, f32, vp, f32, vp, i64, i32, i32, i32, vp, i64, vp, vp]),
     "wf_quantize_i8": (i32, [vp, i32, i64, vp, vp, vp]),
     "wf_quantize_i8_rows": (i32, [vp, i32, i32, i32, vp, vp, vp]),
     "wf_quantize_i8_trunc": (i32, [vp, i32, i64, vp, vp, vp]),

@@ -77,3 +77,24 @@ class BitNetFusedLinear(nn.Module):
     def extra_repr(self) -> str:
         return f"in_features={self.in_features}, rows={self.rows}, fmt={'i2s' if self.fmt == WF_FMT_I2S else 'tq'}"
 
+
+class BitNetMLP(nn.Module):
+    """The BitNet MLP block (scripts/direct_inference_full.py:252-265) as one op (wf_bitnet_mlp):
+    down(rms_norm(relu(gate(x))^2 * up(x), ffn_sub_norm)), gate|up sharing one quantization."""
+
+    def __init__(self, gate: BitNetLinear, up: BitNetLinear, down: BitNetLinear, ffn_sub_norm: torch.Tensor,
+                 eps: float = 1e-5):
+        super().__init__()
+        if not (gate.in_features == up.in_features == down.out_features and gate.out_features == up.out_features
+                == down.in_features and gate.fmt == up.fmt == down.fmt):
+            raise ValueError("gate / up / down shapes or formats do not form an MLP")
+        self.hidden, self.inter, self.fmt, self.eps = gate.in_features, gate.out_features, gate.fmt, float(eps)
+        self.scales = (gate.weight_scale, up.weight_scale, down.weight_scale)
+        self.register_buffer("packed_gate_up", torch.cat([gate.packed_weight, up.packed_weight], 0).contiguous())
+        self.register_buffer("packed_down", down.packed_weight)
+        self.register_buffer("ffn_sub_norm", ffn_sub_norm.to(torch.bfloat16).contiguous())
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return ops.bitnet_mlp(x, self.packed_gate_up, self.packed_down, *self.scales, self.ffn_sub_norm, self.eps,
+                              self.fmt)
+

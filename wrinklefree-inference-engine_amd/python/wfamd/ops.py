@@ -200,6 +200,36 @@ def bitnet_linear_fused(x: torch.Tensor, packed: torch.Tensor, rows: Sequence[in
     return [o.cpu() for o in outs] if host else outs
 
 
+def bitnet_mlp(x: torch.Tensor, packed_gate_up: torch.Tensor, packed_down: torch.Tensor, ws_gate: float, ws_up: float,
+               ws_down: float, ffn_sub_norm: torch.Tensor, eps: float = 1e-5, fmt: int = WF_FMT_I2S) -> torch.Tensor:
+    """BitNet MLP in one call (include/wf_bitnet.h wf_bitnet_mlp; scripts/direct_inference_full.py:252-265):
+    bf16 x [..., H] -> down(rms_norm(relu(gate(x))^2 * up(x), ffn_sub_norm)) bf16 [..., H]; gate|up
+    row-concatenated with one shared activation quantization."""
+    if x.dtype != torch.bfloat16 or ffn_sub_norm.dtype != torch.bfloat16:
+        raise ValueError("bitnet_mlp expects bf16 activations and norm weight")
+    h, i = x.shape[-1], ffn_sub_norm.shape[-1]
+    _check_packed(packed_gate_up, h, fmt)
+    _check_packed(packed_down, i, fmt)
+    if packed_gate_up.shape[0] != 2 * i or packed_down.shape[0] != h:
+        raise ValueError(f"gate|up must have {2 * i} rows and down {h} rows")
+    if not (x.is_cuda and packed_gate_up.is_cuda and packed_down.is_cuda and ffn_sub_norm.is_cuda):
+        raise ValueError("bitnet_mlp: device tensors only")
+    x2 = x.reshape(-1, h)
+    if x2.stride(1) != 1 or x2.stride(0) % 8 != 0 or x2.data_ptr() % 16 != 0:
+        x2 = x2.contiguous()
+    m = x2.shape[0]
+    y = torch.empty((m, h), dtype=torch.bfloat16, device=x.device)
+    if m > 0:
+        nws = int(_lib.load().wf_bitnet_mlp_ws_bytes(m, h, i))
+        ws = torch.empty(nws + 256, dtype=torch.uint8, device=x.device)
+        base = (ws.data_ptr() + 255) // 256 * 256
+        nw = ffn_sub_norm.contiguous()
+        call("wf_bitnet_mlp", fmt, packed_gate_up.data_ptr(), packed_down.data_ptr(), float(ws_gate), float(ws_up),
+             float(ws_down), nw.data_ptr(), float(eps), x2.data_ptr(), x2.stride(0), m, h, i, y.data_ptr(), h, base,
+             _stream())
+    return y.reshape(*x.shape[:-1], h)
+
+
 # ---------------------------------------------------------------------------------------------
 # a3: activation quantizers
 # ---------------------------------------------------------------------------------------------
