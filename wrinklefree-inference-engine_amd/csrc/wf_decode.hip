@@ -1635,6 +1635,10 @@ __global__ __launch_bounds__(kNT) void k_rownorm_attn(const float2* __restrict__
     WF_STAMP(2);
 }
 
+#ifndef WF_LM_U  // study builds only (tools/build_variant.sh): 16-byte chunks in flight per lane
+#define WF_LM_U 4
+#endif
+constexpr int kLmU = WF_LM_U;
 // logits[b, v] = bf16(sum_k hn[b,k] * E[v,k]) (F.linear, fp32 accumulation); 16 lanes per vocab
 // row, 16 rows per block. Each block publishes its (max, first index) per row (sc1); the last
 // block reduces them: greedy token (direct_inference_full.py:306-307; first index on ties), and
@@ -1657,9 +1661,10 @@ __global__ __launch_bounds__(256) void k_lm_head(const uint16_t* __restrict__ E,
     const uint16_t* er = E + (int64_t)min(row, V - 1) * H;
     WF_STAMP_BASE(4096u);
     WF_STAMP(0);
-    uint4 w[4];
+    constexpr int U = kLmU;
+    uint4 w[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {  // first weight chunks in flight before the activation staging
+    for (int u = 0; u < U; ++u) {  // first weight chunks in flight before the activation staging
         const int c = 16 * u + sub;
         w[u] = (c < C) ? ldg_nt(reinterpret_cast<const uint8_t*>(er + 8 * c)) : make_uint4(0, 0, 0, 0);
     }
@@ -1672,16 +1677,16 @@ __global__ __launch_bounds__(256) void k_lm_head(const uint16_t* __restrict__ E,
     float acc[MB];
 #pragma unroll
     for (int m = 0; m < MB; ++m) acc[m] = 0.f;
-    for (int c0 = 0; c0 < C; c0 += 64) {
+    for (int c0 = 0; c0 < C; c0 += 16 * U) {
         if (c0 > 0) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < U; ++u) {
                 const int c = c0 + 16 * u + sub;
                 w[u] = (c < C) ? ldg_nt(reinterpret_cast<const uint8_t*>(er + 8 * c)) : make_uint4(0, 0, 0, 0);
             }
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int c = c0 + 16 * u + sub;
             if (c < C) {
                 const uint32_t wd[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
