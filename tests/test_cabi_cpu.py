@@ -219,3 +219,35 @@ def test_sglang_backend_surface():
     assert not r["valid"] and r["errors"]
     meth = bq.BitNetLinearMethod()
     assert meth.compute_dtype == torch.bfloat16 and meth.get_sparsity_stats() == {"enabled": False}
+
+
+def test_fused_projection_and_mlp_argument_errors():
+    """wf_bitnet_linear_fused / wf_bitnet_mlp validate their arguments on the host before any HIP
+    call (WF_EINVAL + wf_last_error), so the boundary's error behaviour is checkable without a GPU;
+    workspace sizes are host arithmetic."""
+    import ctypes as C
+    from wfamd import _lib
+    lib = _lib.load()
+    x = (C.c_uint16 * 4096)()
+    w = (C.c_uint8 * 4096)()
+    y0, y1 = (C.c_uint16 * 4096)(), (C.c_uint16 * 4096)()
+    ys = (C.c_void_p * 2)(C.addressof(y0), C.addressof(y1))
+    n = (C.c_int * 2)(256, 256)
+    ws = (C.c_float * 2)(1.0, 1.0)
+    ld = (C.c_int64 * 2)(256, 256)
+
+    def fused(nseg, K=256, nn=n, ldy=ld):
+        return lib.wf_bitnet_linear_fused(0, C.addressof(w), nseg, C.addressof(nn), C.addressof(ws), C.addressof(x),
+                                          K, 1, K, C.addressof(ys), C.addressof(ldy), None, None)
+    assert fused(0) == _lib.WF_EINVAL and b"segments" in lib.wf_last_error()
+    assert fused(4) == _lib.WF_EINVAL
+    assert fused(2, K=200) == _lib.WF_EINVAL and b"K % 128" in lib.wf_last_error()
+    bad_n = (C.c_int * 2)(256, 0)
+    assert fused(2, nn=bad_n) == _lib.WF_EINVAL and b"segment 1" in lib.wf_last_error()
+    bad_ld = (C.c_int64 * 2)(256, 100)
+    assert fused(2, ldy=bad_ld) == _lib.WF_EINVAL and b"segment 1" in lib.wf_last_error()
+    assert lib.wf_bitnet_mlp(0, C.addressof(w), C.addressof(w), 1.0, 1.0, 1.0, C.addressof(x), 1e-5, C.addressof(x),
+                             256, 1, 256, 200, C.addressof(y0), 256, None, None) == _lib.WF_EINVAL
+    assert lib.wf_bitnet_mlp_ws_bytes(0, 2560, 6912) == 0
+    ws_b = lib.wf_bitnet_mlp_ws_bytes(4, 2560, 6912)
+    assert ws_b >= 2 * 4 * 6912 * 2 + lib.wf_bitnet_linear_ws_bytes(4, 6912)
