@@ -91,6 +91,9 @@ struct GemvArgs {
     unsigned* seam;
 };
 constexpr int kSeamTiles = 8;  // 32-sequence tiles: batch <= 256 (kDecGemmMaxB)
+// one 128-byte line per seam word: memory-side atomics and polls on one line serialise (the batch-1
+// QKV + attention study measured ~5 us per hand-off with 20 counters sharing a line)
+constexpr int kSeamLine = 32;
 
 __device__ __forceinline__ uint8_t to_fp8(float y) {
     const float c = fminf(fmaxf(y, -448.f), 448.f);
@@ -858,7 +861,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_dec_gemm_t(GemvArgs a) {  // 2 w
         __shared__ float s_red[16];
         __shared__ int s_red_i[NW];
         const int ty = blockIdx.y, rows = min(32, a.B - 32 * ty);
-        unsigned* arrive = a.seam + ty;
+        unsigned* arrive = a.seam + ty * kSeamLine;
         const bool producer = (int)blockIdx.x < rows;
         // blocks that only wait start their weight stream now; a producing block first normalises its
         // row (its loads must not queue behind the weights: loads return in order) and publishes
@@ -938,8 +941,8 @@ __global__ __launch_bounds__(NW * 64, 2) void k_dec_gemm_t(GemvArgs a) {  // 2 w
         // re-arm: every block of the tile is past its wait once all have counted in here (the add is
         // at the end so its return does not hold this block's loads)
         if (threadIdx.x == 0) {
-            unsigned* arrive = a.seam + blockIdx.y;
-            unsigned* passed = a.seam + kSeamTiles + blockIdx.y;
+            unsigned* arrive = a.seam + blockIdx.y * kSeamLine;
+            unsigned* passed = a.seam + (kSeamTiles + blockIdx.y) * kSeamLine;
             const unsigned old = __hip_atomic_fetch_add(passed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (old == gridDim.x - 1u) {
                 st_sc1(arrive, 0u);
@@ -2267,12 +2270,12 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_ALLOC(m->act_sf, sizeof(float) * B);
     WF_ALLOC(m->act_sum, sizeof(int) * B);
     WF_ALLOC(m->tickets, sizeof(unsigned) * kTicketWords * TK_COUNT);
-    WF_ALLOC(m->seam, sizeof(unsigned) * 2 * kSeamTiles);
+    WF_ALLOC(m->seam, sizeof(unsigned) * 2 * kSeamTiles * kSeamLine);
     WF_ALLOC(m->am_part, sizeof(uint2) * B * m->lm_blocks);
 #undef WF_ALLOC
     // tickets start at zero; every launch re-arms the ones it uses
     if ((e = hipMemset(m->tickets, 0, sizeof(unsigned) * kTicketWords * TK_COUNT)) != hipSuccess) return fail(e);
-    if ((e = hipMemset(m->seam, 0, sizeof(unsigned) * 2 * kSeamTiles)) != hipSuccess) return fail(e);
+    if ((e = hipMemset(m->seam, 0, sizeof(unsigned) * 2 * kSeamTiles * kSeamLine)) != hipSuccess) return fail(e);
     fused_norm_plan(m);
     if ((e = hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking)) != hipSuccess) return fail(e);
     *out = m;
