@@ -327,19 +327,25 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
 // fixed number of records, so it needs no sequence length and issues every load before its
 // weight stream.
 // ---------------------------------------------------------------------------------------------
-#ifndef WF_AP_THREADS  // study builds only (tools/build_variant.sh): threads per block, keys per lane group and chunk
+#ifndef WF_AP_THREADS  // study builds only (tools/build_variant.sh): threads per block
 #define WF_AP_THREADS 256
-#define WF_AP_U 8
 #endif
 constexpr int kAttnPartThreads = WF_AP_THREADS;
-template <int G, int NS>
-__global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* __restrict__ q, int64_t q_sb,
-                                                                const uint16_t* __restrict__ K,
-                                                                const uint16_t* __restrict__ V, int64_t kv_sb,
-                                                                int64_t kv_sh, int Hq, int Hkv, int S,
-                                                                const int32_t* __restrict__ seq_lens, float sm_scale,
-                                                                float2* __restrict__ ml_out, float* __restrict__ o_out) {
-    constexpr int D = 128, LP = D / 8, NG = kAttnPartThreads / LP, U = WF_AP_U, CH = U * NG;  // 128 keys per chunk
+// keys per lane group per chunk (chunk = 16 U keys at 256 threads): a split that one 160-key chunk
+// covers (contexts <= 1280 at 8 splits) takes U = 10 -- one load round; longer splits the
+// double-buffered 128-key chunks (same-box, batch 1: U 10 vs 8 at ctx 1024 attention 5.59 -> 4.85 us,
+// 1080 -> 1104 tok/s; at ctx 4000 U 10 alone lost 10.3 -> 11.3 us). -DWF_AP_U=n: one U everywhere.
+#ifdef WF_AP_U
+constexpr int kApUShort = WF_AP_U, kApULong = WF_AP_U;
+#else
+constexpr int kApUShort = 10, kApULong = 8;
+#endif
+template <int G, int NS, int U>
+__device__ __forceinline__ void attn_part_body(const uint16_t* __restrict__ q, int64_t q_sb, const uint16_t* __restrict__ K,
+                                               const uint16_t* __restrict__ V, int64_t kv_sb, int64_t kv_sh, int Hq,
+                                               int Hkv, int S, const int32_t* __restrict__ seq_lens, float sm_scale,
+                                               float2* __restrict__ ml_out, float* __restrict__ o_out) {
+    constexpr int D = 128, LP = D / 8, NG = kAttnPartThreads / LP, CH = U * NG;
     // block (s, y, b): query heads hq0 .. hq0 + G - 1 (G = whole GQA group, or 1: one block per query
     // head, 4x the blocks for a group of 4 -- the K/V re-reads hit the caches)
     const int s = blockIdx.x, b = blockIdx.z;
@@ -464,6 +470,24 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
         if (d == 0) ml_out[rec] = make_float2(mx, ls);
     }
     WF_STAMP(2);
+}
+
+template <int G, int NS>
+__global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* __restrict__ q, int64_t q_sb,
+                                                                const uint16_t* __restrict__ K,
+                                                                const uint16_t* __restrict__ V, int64_t kv_sb,
+                                                                int64_t kv_sh, int Hq, int Hkv, int S,
+                                                                const int32_t* __restrict__ seq_lens, float sm_scale,
+                                                                float2* __restrict__ ml_out, float* __restrict__ o_out) {
+    constexpr int NG = kAttnPartThreads / 16;
+    const int Sb = min(seq_lens[blockIdx.z], S);
+    const int T = ((Sb + NS - 1) / NS + 15) / 16 * 16;  // the body's split length
+    // (the batched untiled fallback, G > 1, keeps one body: two would double its LDS)
+    if (G == 1 && T <= kApUShort * NG)  // block-uniform
+        attn_part_body<G, NS, G == 1 ? kApUShort : kApULong>(q, q_sb, K, V, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale,
+                                                             ml_out, o_out);
+    else
+        attn_part_body<G, NS, kApULong>(q, q_sb, K, V, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, ml_out, o_out);
 }
 
 // ---------------------------------------------------------------------------------------------
