@@ -389,9 +389,7 @@ def gen_msb():
             yb = meth.apply(pl, sl, x, 192, 1024, bias=bias)
             out[f"lin_y{m}_{tag}"] = y.view(torch.int16).numpy().view(np.uint16)
             out[f"lin_yb{m}_{tag}"] = yb.view(torch.int16).numpy().view(np.uint16)
-    # activation sparsity (float32 activations, 4 tokens). Round 3: sparsity is out of scope (SURVEY
-    # §2 row 4b); only sp_x is still read (the disabled default is the identity), the masks stay in
-    # the committed fixture unchecked.
+    # activation sparsity (float32 activations, 4 tokens; checked in tests/test_oracle_golden.py)
     xs = torch.randn(4, 256, generator=g) * torch.linspace(0.2, 3.0, 4).unsqueeze(1)
     out["sp_x"] = xs.numpy()
     out["sp_topk"], out["sp_topk_r"] = rsp.apply_top_k_sparsity(xs, 0.4)[0].numpy(), np.array(0.6)

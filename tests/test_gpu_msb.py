@@ -117,11 +117,20 @@ def test_reference_accuracy_bar(size, m):
         assert rel < max(0.05, 1.25 * rel_t), (dtype, rel, rel_t)
 
 
-def test_fp32_compute():
+def test_sparsity_on_device_and_fp32_compute():
+    from wrinklefree_inference.sglang_backend import activation_sparsity as sp
     from wrinklefree_inference.sglang_backend import bitnet_quantization as bq
     g = load_golden("msb")
+    xs = torch.from_numpy(g["sp_x"]).cuda()
+    y, _ = sp.apply_top_k_sparsity(xs, 0.4)
+    assert np.array_equal(y.cpu().numpy(), g["sp_topk"])
     packed, scale = torch.from_numpy(g["lin_packed"]).cuda(), float(g["lin_scale"])
     x = torch.from_numpy(g["lin_x3"]).cuda()
+    meth = bq.BitNetLinearMethod(compute_dtype=torch.bfloat16, sparsity_config=sp.get_qsparse_config())
+    y = meth.apply(packed, scale, x, 192, 1024)
+    xk, _ = sp.apply_top_k_sparsity(x.to(torch.bfloat16), 0.4)
+    y2 = bq.BitNetLinearMethod(compute_dtype=torch.bfloat16).apply(packed, scale, xk, 192, 1024)
+    assert torch.equal(y, y2) and meth.get_last_sparsity() == pytest.approx(0.6)
     y32 = bq.BitNetLinearMethod(compute_dtype=torch.float32).apply(packed, scale, x, 192, 1024)
     ref = x @ bq.dequantize_bitnet(packed, scale, 192, 1024).T
     assert torch.allclose(y32, ref, rtol=1e-5, atol=1e-4)

@@ -207,14 +207,23 @@ class TestMsbLinearMethod:
 
 
 class TestActivationSparsity:
-    """Activation sparsity is out of scope: the linear method's config surface
-    keeps the reference's disabled default as the identity, and an enabled mode fails loudly."""
+    """Our device-op restatement of sglang_backend/activation_sparsity.py (host logic, runs on CPU
+    tensors too) against the reference's outputs (threshold :83-99, top-k :102-133, adaptive
+    :136-195; disabled by default :240-242)."""
 
-    def test_default_is_identity_enabled_raises(self):
+    def test_masks_match_reference(self):
         import torch
         from wrinklefree_inference.sglang_backend import activation_sparsity as sp
-        x = torch.from_numpy(load_golden("msb")["sp_x"])
+        g = load_golden("msb")
+        x = torch.from_numpy(g["sp_x"])
+        y, r = sp.apply_top_k_sparsity(x, 0.4)
+        assert np.array_equal(y.numpy(), g["sp_topk"]) and r == pytest.approx(float(g["sp_topk_r"]))
+        y, r = sp.apply_threshold_sparsity(x, 0.5)
+        assert np.array_equal(y.numpy(), g["sp_thr"]) and r == pytest.approx(float(g["sp_thr_r"]))
+        y, r = sp.apply_adaptive_sparsity(x, 0.3, 0.7)
+        assert np.array_equal(y.numpy(), g["sp_adapt"]) and r == pytest.approx(float(g["sp_adapt_r"]))
+        cfg = sp.get_qsparse_config()
+        y, r = sp.apply_sparsity(x, cfg)
+        assert np.array_equal(y.numpy(), g["sp_topk"]) and cfg.get_average_sparsity() == pytest.approx(0.6)
         y, r = sp.apply_sparsity(x, sp.get_default_config())
         assert y is x and r == 0.0
-        with pytest.raises(NotImplementedError):
-            sp.apply_sparsity(x, sp.ActivationSparsityConfig(enabled=True, mode=sp.SparsityMode.TOP_K))
