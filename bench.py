@@ -153,16 +153,15 @@ def gemv_bench(rotate_bytes: float = 1.2e9, reps: int = 3):
 def cpu_baseline(ctx: int, seconds: float, pin_cores: int = 8):
     """The CPU baseline on this host (oracle/cpu_baseline.py, run as a child process so its core
     affinity and OpenMP pool are its own): the oracle's full decode step of the 2B model shape and the
-    standalone GEMV shapes, AVX512-VNNI build where the host has it, timed (1) on every core of this
-    process's affinity mask with the environment's OMP_NUM_THREADS and (2) pinned to `pin_cores`
-    cores with as many threads (the reference's server pin, scripts/launch_sglang_bitnet.sh:61).
-    Bounded samples of `seconds` each; random weights (timing only)."""
+    standalone GEMV shapes, AVX512-VNNI build where the host has it, timed (1) on the process's whole
+    CPU share (every physical core of its affinity mask, capped by the cgroup CPU quota) and (2)
+    pinned to `pin_cores` physical cores (the reference's server pin,
+    scripts/launch_sglang_bitnet.sh:61); one OpenMP thread per core, OMP_PROC_BIND=close,
+    OMP_PLACES=cores. Bounded samples of `seconds` each; random weights (timing only)."""
     import subprocess
     runs = {}
     for name, cores in (("all", 0), (f"pin{pin_cores}", pin_cores)):
         env = dict(os.environ)
-        if cores:
-            env["OMP_NUM_THREADS"] = str(cores)
         cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--ctx", str(ctx), "--seconds", str(seconds),
                "--gemv-seconds", "1.0", "--cores", str(cores)]
         r = subprocess.run(cmd, cwd=str(ROOT), env=env, capture_output=True, text=True, timeout=600)
@@ -176,10 +175,48 @@ def cpu_baseline(ctx: int, seconds: float, pin_cores: int = 8):
                       f"batch 1, ctx {ctx}, {a['decode']['tokens']} tokens in {a['decode']['seconds']}s (random weights)",
             "ms_per_token": a["decode"]["ms_per_token"], "cpu_model": a["cpu_model"], "isa": a["isa"],
             "omp_threads": a["threads"], "affinity_cpus": a["affinity_cpus"],
-            "logical_cpus_total": a["logical_cpus_total"],
+            "logical_cpus_total": a["logical_cpus_total"], "core_choice": a["core_choice"],
+            "omp_proc_bind": a["omp_proc_bind"], "omp_places": a["omp_places"],
             f"pinned_{pin_cores}_cores": {"value": p["decode"]["tokens_per_s"], "omp_threads": p["threads"],
                                           "ms_per_token": p["decode"]["ms_per_token"], "gemv": p["gemv"]},
             "gemv": a["gemv"]}
+
+
+def _profile_json(name: str):
+    f = ROOT / "profiles" / name
+    try:
+        return json.loads(f.read_text()) if f.exists() else None
+    except Exception:
+        return None
+
+
+def roofline(kern: dict, B: int, args, step_gbs: float) -> dict:
+    """The `roofline` object. The dominant kernel is fixed by the committed rocprofv3 profile of this
+    workload (profiles/rocprof_ops*.json, `_dominant` = the op with the largest TOTAL kernel time,
+    tools/rocprof_ops.py), so the choice does not flip between near-equal ops on the live timing's
+    noise; its achieved GB/s is measured live (HIP events over graph replays of its launches).
+    `traffic` = PMC HBM bytes per launch (profiles/pmc_traffic*.json, FETCH_SIZE x 2 + WRITE_SIZE).
+    `ops` carries every op's live fraction and its PMC traffic / algorithmic-bytes ratio; `step_frac`
+    is the whole step's (weights + KV) bytes per step over the step time, against the same peak."""
+    fixed_ctx = args.ctx_dist == "fixed" and args.kv == "bf16"  # the profiled workload
+    suffix = "" if B < 16 else f"_b{B}"
+    prof = _profile_json(f"rocprof_ops{suffix}.json") if fixed_ctx else None
+    pmc = (_profile_json(f"pmc_traffic{suffix}.json") or {}) if fixed_ctx else {}
+    if prof and prof.get("_dominant") in kern:
+        dom_name, how = prof["_dominant"], f"largest total rocprofv3 time in profiles/{prof.get('_source')}"
+    else:
+        dom_name, how = max(kern, key=lambda k: kern[k]["us_per_step"]), "largest live us per step (no profile)"
+    ops = {}
+    for name, k in kern.items():
+        t = pmc.get(name, {}).get("hbm_bytes_per_launch")
+        ops[name] = {"us": k["us"], "gbs": k["gbs"], "frac": round(k["gbs"] / HBM_PEAK_GBS, 4),
+                     "traffic": t, "traffic_ratio": round(t / k["bytes"], 3) if t else None,
+                     "rocprof_avg_us": (prof or {}).get(name, {}).get("avg_us")}
+    dom = kern[dom_name]
+    return {"bound": "hbm", "achieved": dom["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": ops[dom_name]["traffic"],
+            "kernel": dom_name, "dominant_by": how, "bytes_per_launch": dom["bytes"], "us_per_launch": dom["us"],
+            "step_gbs": round(step_gbs, 1), "step_frac": round(step_gbs / HBM_PEAK_GBS, 4), "ops": ops}
 
 
 def main():
@@ -243,23 +280,10 @@ def main():
     ms_step = 1000.0 * el / args.steps
 
     kern = {} if args.no_op_timing else op_timing(dec, ctx + total // 2)
-    roof = None
-    if kern:
-        dom_name = max(kern, key=lambda k: kern[k]["us_per_step"])
-        dom = kern[dom_name]
-        traffic = None
-        pmc = ROOT / "profiles" / ("pmc_traffic.json" if B < 16 else f"pmc_traffic_b{B}.json")
-        # the PMC files are measured on the fixed-context workload (tools/profile_round.sh)
-        if pmc.exists() and args.ctx_dist == "fixed" and args.kv == "bf16":
-            try:
-                traffic = json.loads(pmc.read_text()).get(dom_name, {}).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        roof = {"bound": "hbm", "achieved": dom["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom_name,
-                "bytes_per_launch": dom["bytes"], "us_per_launch": dom["us"]}
     kv_esz = 1 if args.kv in ("fp8", "int8") else 2
     step_bytes = cfg.weight_bytes_per_token(wfmt) + B * cfg.kv_bytes_per_token(ctx + total // 2) * kv_esz // 2
+    step_gbs = step_bytes / (ms_step / 1000.0) / 1e9
+    roof = roofline(kern, B, args, step_gbs) if kern else None
     gemv = None if (args.no_gemv or B != 1) else gemv_bench()
     if cpu:
         cpu_gemv = cpu.pop("gemv")
@@ -282,7 +306,7 @@ def main():
                        "kv": args.kv + (", paged (32-token pages)" if paged else ""),
                        **({"ctx_mean": ctx, "ctx_min": int(ctxs.min()), "ctx_max": int(ctxs.max())}
                           if args.ctx_dist == "uniform" else {})},
-            "step_hbm_gbs": round(step_bytes / (ms_step / 1000.0) / 1e9, 1),
+            "step_hbm_gbs": round(step_gbs, 1),
             "gemv_hbm_gbs": kern.get("gate_up", {}).get("gbs") if kern else None,
             "gemv": gemv,
             "roofline": roof, "cpu_baseline": cpu, "kernels": kern,

@@ -9,6 +9,12 @@ the build's own AVX512-VNNI restatement of a1-a3), else the autovectorised scala
 (-march=native). Random weights of the full bitnet-b1.58-2B-4T shape, bounded samples.
 
     python -m oracle.cpu_baseline --ctx 1024 --seconds 6 [--cores 8]   -> one JSON line
+
+Threads and placement: --cores N pins to N distinct physical cores of the affinity mask (one
+logical CPU per core, SMT siblings skipped); --cores 0 uses the process's whole CPU share: the
+affinity mask capped by the cgroup CPU quota (a GPU box may show every CPU of the machine in its
+mask while its quota allows a slice of them). One OpenMP thread per chosen core with
+OMP_PROC_BIND=close and OMP_PLACES=cores, set before the OpenMP runtime loads.
 """
 from __future__ import annotations
 
@@ -39,6 +45,49 @@ def host_info() -> dict:
     isa = sorted(f for f in flags if f.startswith(("avx512", "amx")) or f in ("avx2", "avx_vnni", "fma"))
     return {"cpu_model": model, "isa": isa, "logical_cpus_total": os.cpu_count(),
             "affinity_cpus": len(os.sched_getaffinity(0)), "_flags": flags}
+
+
+def cgroup_cpu_quota() -> float | None:
+    """CPUs allowed by the cgroup (v2 cpu.max, or v1 cfs quota / period); None when unlimited."""
+    try:
+        q, p = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        return None if q == "max" else int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read_text())
+        p = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+        return None if q <= 0 else q / p
+    except (OSError, ValueError):
+        return None
+
+
+def physical_cores(cpus) -> list[int]:
+    """One logical CPU per physical core (first sibling), in CPU order."""
+    seen, out = set(), []
+    for c in sorted(cpus):
+        base = Path(f"/sys/devices/system/cpu/cpu{c}/topology")
+        try:
+            key = (base.joinpath("physical_package_id").read_text().strip(), base.joinpath("core_id").read_text().strip())
+        except OSError:
+            key = ("cpu", str(c))
+        if key not in seen:
+            seen.add(key)
+            out.append(c)
+    return out
+
+
+def choose_cores(n: int) -> tuple[list[int], str]:
+    """(cores to run on, how their count was chosen)."""
+    mask = sorted(os.sched_getaffinity(0))
+    phys = physical_cores(mask) or mask
+    if n > 0:
+        return phys[:n], f"pinned to {min(n, len(phys))} physical cores"
+    quota = cgroup_cpu_quota()
+    if quota is not None and int(quota) < len(phys):
+        k = max(1, int(quota))
+        return phys[:k], f"cgroup CPU quota {quota:g} of {len(mask)} CPUs in the affinity mask"
+    return phys, f"every physical core of the {len(mask)}-CPU affinity mask"
 
 
 def build_lib(flags) -> tuple[str, str]:
@@ -138,11 +187,15 @@ def main():
     ap.add_argument("--ctx", type=int, default=1024)
     ap.add_argument("--seconds", type=float, default=6.0)
     ap.add_argument("--gemv-seconds", type=float, default=1.0)
-    ap.add_argument("--cores", type=int, default=0, help="pin to the first N cores of the affinity mask")
+    ap.add_argument("--cores", type=int, default=0,
+                    help="pin to N physical cores of the affinity mask; 0 = the process's whole CPU share")
     args = ap.parse_args()
-    if args.cores:
-        os.sched_setaffinity(0, sorted(os.sched_getaffinity(0))[:args.cores])
-    info = host_info()
+    info = host_info()  # the mask as given, before pinning
+    cores, how = choose_cores(args.cores)
+    os.sched_setaffinity(0, cores)
+    # one OpenMP thread per chosen core, bound (read when the OpenMP runtime loads with the library)
+    os.environ.update(OMP_NUM_THREADS=str(len(cores)), OMP_PROC_BIND="close", OMP_PLACES="cores")
+    info.update(cores_used=len(cores), core_choice=how, omp_proc_bind="close", omp_places="cores")
     flags = info.pop("_flags")
     libname, kind = build_lib(flags)
     threads = orc.num_threads(libname)

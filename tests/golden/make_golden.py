@@ -351,6 +351,138 @@ def gen_decode():
     return save("decode", **out)
 
 
+def reference_decoder():
+    """(DirectBitNetInference instance with the full_inputs weights and history, cfg, weights, K, V,
+    the full_inputs module); see gen_decode_full."""
+    import types
+    sys.path.insert(0, str(OUT))
+    import full_inputs as fi
+    sys.path.insert(0, str(OUT.parents[1] / "wrinklefree-inference-engine_amd" / "python"))
+    cache = {}
+    orig_unpack = tbc._unpack_i2_to_ternary
+
+    def unpack_memo(p, n, k):
+        key = (p.data_ptr(), n, k)
+        if key not in cache:
+            cache[key] = orig_unpack(p, n, k)
+        return cache[key]
+
+    tbc._unpack_i2_to_ternary = unpack_memo
+    mods = {"sglang": types.ModuleType("sglang"), "sglang.srt": types.ModuleType("sglang.srt"),
+            "sglang.srt.models": types.ModuleType("sglang.srt.models"),
+            "sglang.srt.models.bitnet": types.ModuleType("sglang.srt.models.bitnet"),
+            "sgl_kernel": types.ModuleType("sgl_kernel"), "sgl_kernel.quantization": types.ModuleType("sgl_kernel.quantization"),
+            "sgl_kernel.quantization.bitnet": types.ModuleType("sgl_kernel.quantization.bitnet")}
+    mods["sglang.srt.models.bitnet"]._unpack_ternary_weights = tbc._unpack_ternary_weights
+    mods["sglang.srt.models.bitnet"]._pack_ternary_weights = tbc._pack_ternary_weights
+    mods["sgl_kernel.quantization.bitnet"].bitnet_gemv = tbc.bitnet_gemv_reference
+    mods["sgl_kernel.quantization.bitnet"].quantize_activations_i8 = tbc.quantize_activations_i8
+    saved = {k: sys.modules.get(k) for k in mods}
+    sys.modules.update(mods)
+    try:
+        dif = _load_by_path("ref_direct_inference_full", REF / "scripts/direct_inference_full.py")
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+        tbc._unpack_i2_to_ternary = orig_unpack
+    sys.modules["ref_direct_inference_full"] = dif
+    tbc._unpack_i2_to_ternary = unpack_memo
+    cfg = fi.config()
+    w = fi.weights(cfg)
+    kh, vh = fi.history(cfg)
+    L, H, HKV, D = cfg.layers, cfg.hidden, cfg.n_kv_heads, cfg.head_dim
+    bf = torch.bfloat16
+    m = object.__new__(dif.DirectBitNetInference)
+    m.device, m.dtype = "cpu", bf
+    m.hidden_dim, m.n_layers, m.n_heads, m.n_kv_heads = H, L, cfg.n_heads, HKV
+    m.head_dim, m.mlp_hidden, m.vocab_size, m.rms_eps, m.rope_theta = D, cfg.inter, cfg.vocab, cfg.eps, cfg.rope_theta
+    m.rope = dif.RotaryEmbedding(D, max_seq_len=cfg.max_seq, base=cfg.rope_theta)
+    m.embed_tokens = w["embed"]
+    m.lm_head = m.embed_tokens
+    m.final_norm = w["final_norm"]
+    ws = w["wscale"].numpy()
+    names = [("q_proj", "wq"), ("k_proj", "wk"), ("v_proj", "wv"), ("o_proj", "wo"), ("gate_proj", "wg"),
+             ("up_proj", "wu"), ("down_proj", "wd")]
+    m.layers = []
+    for li in range(L):
+        lay = {"input_layernorm": w["ln_in"][li], "post_attention_layernorm": w["ln_post"][li],
+               "attn_sub_norm": w["attn_sub"][li], "ffn_sub_norm": w["ffn_sub"][li]}
+        for j, (rn, wn) in enumerate(names):
+            lay[rn] = w[wn][li].contiguous()
+            lay[rn.replace("_proj", "_scale")] = float(ws[li, j])
+        m.layers.append(lay)
+    m.max_seq_len = cfg.max_seq
+    m.k_cache = torch.zeros(L, cfg.max_seq, HKV, D, dtype=bf)
+    m.v_cache = torch.zeros(L, cfg.max_seq, HKV, D, dtype=bf)
+    m.k_cache[:, :fi.CTX0] = kh.transpose(1, 2)
+    m.v_cache[:, :fi.CTX0] = vh.transpose(1, 2)
+    return m, cfg, w, kh, vh, fi, unpack_memo, orig_unpack
+
+
+def gen_decode_full(sdpa_fp32: bool = False):
+    """The reference's OWN decode loop at the 2B-4T geometry (2 layers, full width and vocabulary):
+    scripts/direct_inference_full.py's DirectBitNetInference.forward_layer / rms_norm / attention /
+    mlp / bitnet_linear and its RotaryEmbedding, run on an instance whose weights are set directly
+    (its __init__ reads a checkpoint from disk, :74-112). The script imports two un-vendored modules
+    (sglang.srt.models.bitnet, sgl_kernel.quantization.bitnet, :21-22); they are provided here by the
+    reference's own restatements of the same functions in tests/test_bitnet_core.py (the
+    _unpack/_pack_ternary_weights copies :21-106, quantize_activations_i8 :139-146 and
+    bitnet_gemv_reference :149-167, which `ref_linear` above uses too), with the unpacked weights
+    memoised per tensor (same values, fewer host loops). Inputs: tests/golden/full_inputs.py.
+    Stored: per position the hidden state after each layer, the K / V rows each layer appends, the
+    top-64 logits (indices + bf16 values) and the greedy token; sha256 of the regenerated inputs.
+
+    sdpa_fp32 (decode_full_f32attn.npz): the same loop with the one call whose CPU bf16 arithmetic
+    is not reproducible elsewhere -- torch's CPU flash SDPA on bf16 tensors, which rounds the
+    softmax probabilities to bf16 before P.V (measured: ~20-40 % of a 961-key output's elements
+    differ from the exactly rounded result by >= 1 bf16 ulp) -- evaluated on the same bf16 q / K /
+    V upcast to fp32 and rounded to bf16 once (the script's F.scaled_dot_product_attention call
+    :241 routed through an upcasting wrapper); every other op is the reference's own."""
+    m, cfg, w, kh, vh, fi, unpack_memo, orig_unpack = reference_decoder()
+    dif = sys.modules["ref_direct_inference_full"]
+    if sdpa_fp32:
+        class _F:  # the script's `F` module with the SDPA call upcast
+            def __getattr__(self, name):
+                return getattr(F, name)
+
+            @staticmethod
+            def scaled_dot_product_attention(q, k, v, **kw):
+                return F.scaled_dot_product_attention(q.float(), k.float(), v.float(), **kw).to(q.dtype)
+        dif.F = _F()
+    L = cfg.layers
+    tbc._unpack_i2_to_ternary = unpack_memo
+    tokens, nexts, hidden, krows, vrows, tidx, tval = [], [], [], [], [], [], []
+    tok = fi.FIRST_TOKEN
+    with torch.no_grad():
+        for i in range(fi.POSITIONS):
+            pos = fi.CTX0 + i
+            hid = m.embed_tokens[tok]  # DirectBitNetInference.forward (:285-300), one layer at a time
+            hs = []
+            for li in range(L):
+                hid = m.forward_layer(hid, li, pos)
+                hs.append(bf16_bits(hid))
+            logits = F.linear(m.rms_norm(hid, m.final_norm), m.lm_head)
+            nxt = int(logits.argmax().item())  # sample(temperature=0) (:304-306)
+            top = torch.topk(logits.float(), fi.TOPK)
+            tokens.append(tok)
+            nexts.append(nxt)
+            hidden.append(np.stack(hs))
+            krows.append(np.stack([bf16_bits(m.k_cache[li, pos].flatten()) for li in range(L)]))
+            vrows.append(np.stack([bf16_bits(m.v_cache[li, pos].flatten()) for li in range(L)]))
+            tidx.append(top.indices.numpy().astype(np.int32))
+            tval.append(bf16_bits(logits[top.indices]))
+            tok = nxt
+    tbc._unpack_i2_to_ternary = orig_unpack
+    dif.F = F
+    return save("decode_full_f32attn" if sdpa_fp32 else "decode_full", tokens=np.array(tokens, np.int64), next=np.array(nexts, np.int64),
+                hidden=np.stack(hidden), k_rows=np.stack(krows), v_rows=np.stack(vrows),
+                top_idx=np.stack(tidx), top_val=np.stack(tval), ctx0=np.int64(fi.CTX0),
+                input_sha256=np.array(fi.input_digest(w, kh, vh)))
+
+
 def gen_msb():
     """SGLang BitNet linear method: quantize_to_bitnet (bitnet_quantization.py:69-109),
     dequantize_bitnet (:211-252, LUT path: numba is absent), BitNetLinearMethod.apply (:366-409) in
@@ -402,7 +534,8 @@ def gen_msb():
 
 GENERATORS = {"packing": lambda: gen_packing(), "quant": lambda: gen_quant(), "gemv": lambda: gen_gemv(),
               "linear": lambda: gen_linear(), "kv": lambda: gen_kv(), "attention": lambda: gen_attention(),
-              "decode": lambda: gen_decode(), "msb": lambda: gen_msb()}
+              "decode": lambda: gen_decode(), "msb": lambda: gen_msb(), "decode_full": lambda: gen_decode_full(),
+              "decode_full_f32attn": lambda: gen_decode_full(sdpa_fp32=True)}
 
 
 def main():

@@ -1,0 +1,107 @@
+"""The oracle against the reference's OWN decode loop at the 2B-4T geometry (tests/golden/
+decode_full.npz, made by tests/golden/make_golden.py gen_decode_full from
+scripts/direct_inference_full.py's DirectBitNetInference methods): 2 full-width layers, vocab
+128256, a 960-position random K/V history, 64 teacher-forced decode positions.
+
+This pins the oracle where every batched / prefill / full-width GPU test uses it as the checker,
+and MEASURES the oracle-vs-reference flip rate those tests' allowances are derived from: a
+position "flips" when one bf16 element of an attention output lands on the other side of a
+rounding boundary between two implementations (the reference's bf16 SDPA vs the oracle's double
+attention) and the int8 requantisation of the next GEMV input turns it into whole code steps."""
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+GOLDEN = ROOT / "tests" / "golden"
+sys.path.insert(0, str(GOLDEN))
+sys.path.insert(0, str(ROOT / "wrinklefree-inference-engine_amd" / "python"))
+
+FLIP = 1e-3  # north_star's bf16 tolerance; a position above it in any compared quantity is a flip
+
+
+def rel_l2(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def load_fixture(name: str = "decode_full"):
+    with np.load(GOLDEN / f"{name}.npz", allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def regenerate(name: str = "decode_full"):
+    """(cfg, weights, K history, V history) on the CPU, checked against the fixture's input sha256."""
+    import full_inputs as fi
+    g = load_fixture(name)
+    cfg = fi.config()
+    w = fi.weights(cfg)
+    kh, vh = fi.history(cfg)
+    assert fi.input_digest(w, kh, vh) == str(g["input_sha256"]), "regenerated inputs differ from the fixture's"
+    return cfg, w, kh, vh, g
+
+
+def compare_position(g, i, krows, vrows, top_vals, layers):
+    """Per-layer K / V row rel-L2 and the top-64 logits' rel-L2 of position i (bf16 bits in)."""
+    from oracle.oracle import bf16_to_f32
+    ek = [rel_l2(bf16_to_f32(krows[l]), bf16_to_f32(g["k_rows"][i, l])) for l in range(layers)]
+    ev = [rel_l2(bf16_to_f32(vrows[l]), bf16_to_f32(g["v_rows"][i, l])) for l in range(layers)]
+    el = rel_l2(bf16_to_f32(top_vals), bf16_to_f32(g["top_val"][i]))
+    return ek, ev, el
+
+
+@pytest.mark.parametrize("fixture", ["decode_full", "decode_full_f32attn"])
+def test_oracle_full_width_vs_reference_decode_loop(orc, fixture):
+    """K / V rows of both layers and the top-64 logits of all 64 positions vs the reference, teacher
+    forced; layer 0's rows (computed from the token embedding alone) bit-exact; greedy token equal
+    wherever the reference's top-2 gap is clear. decode_full_f32attn (the reference's loop with its
+    SDPA evaluated in fp32): bit-exact everywhere. decode_full (its CPU bf16 SDPA): bounded drift
+    from layer 1 on, explained by the SDPA's bf16 probabilities (see the asserts)."""
+    cfg, w, kh, vh, g = regenerate(fixture)
+    import torch
+    from wfamd.model import rope_tables
+    cos, sin = rope_tables(cfg.head_dim, cfg.max_seq, cfg.rope_theta)
+    bits = lambda t: t.contiguous().view(torch.int16).numpy().view(np.uint16)
+    a = {"cfg": np.array([cfg.hidden, cfg.layers, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, cfg.inter, cfg.vocab,
+                          cfg.max_seq], dtype=np.int64),
+         "eps": np.float32(cfg.eps), "rope_cos": bits(cos), "rope_sin": bits(sin),
+         "wscale": w["wscale"].numpy().astype(np.float32)}
+    for n in ("wq", "wk", "wv", "wo", "wg", "wu", "wd"):
+        a[n] = w[n].numpy()
+    for n in ("embed", "final_norm", "ln_in", "ln_post", "attn_sub", "ffn_sub"):
+        a[n] = bits(w[n])
+    m = orc.DecodeModel(a)
+    ctx0 = int(g["ctx0"])
+    m.k_cache[:, :, :ctx0] = bits(kh)
+    m.v_cache[:, :, :ctx0] = bits(vh)
+    flips, worst = [], 0.0
+    P = len(g["tokens"])
+    for i in range(P):
+        pos = ctx0 + i
+        logits, nxt = m.step(int(g["tokens"][i]), pos)
+        kr = m.k_cache[:, :, pos].reshape(cfg.layers, -1)
+        vr = m.v_cache[:, :, pos].reshape(cfg.layers, -1)
+        ek, ev, el = compare_position(g, i, kr, vr, logits[g["top_idx"][i]], cfg.layers)
+        assert ek[0] == 0.0 and ev[0] == 0.0, (i, ek, ev)  # layer 0: bit-exact
+        if max(ek + ev + [el]) >= FLIP:
+            flips.append((i, [round(e, 4) for e in ek + ev], round(el, 4)))
+            continue
+        worst = max(worst, el)
+        ref = orc.bf16_to_f32(g["top_val"][i])
+        if ref[0] - ref[1] > 1e-2 * abs(ref[0]):
+            assert nxt == int(g["next"][i]), i
+    print(f"oracle vs reference ({fixture}), {P} positions: worst clean top-64 logits rel-L2 {worst:.2e}; "
+          f"flips {len(flips)}: {flips}")
+    if fixture == "decode_full_f32attn":
+        # the reference's loop with its SDPA evaluated in fp32 and rounded once: the oracle IS that
+        # computation -- every K / V row and every top-64 logit bit-identical, every greedy token equal
+        assert not flips and worst == 0.0, flips
+    else:
+        # the reference's CPU bf16 SDPA rounds the softmax probabilities to bf16 before P.V, so ~20-40 %
+        # of its attention-output elements sit >= 1 bf16 ulp from the exactly rounded value; that flips
+        # int8 codes of attn_sub_norm's quantization and the random-init model carries one code flip to
+        # ~2-4 % of the next layer's K / V (measured: 63 of 64 positions, layer-1 rows 2.2-4.2 %, top-64
+        # logits 1-2.6 %). Layer 0's rows (no attention upstream) stay bit-exact (asserted above).
+        assert all(e < 6e-2 for _, es, el in flips for e in es + [el]), flips

@@ -25,6 +25,9 @@ pytestmark = pytest.mark.gpu
 
 FULL = dict(hidden=2560, n_heads=20, n_kv_heads=5, head_dim=128, inter=6912)
 ATTN_S = [1, 31, 32, 33, 1024, 4096]
+# batch-1 attention body switch (wf_attn.hip: one 160-key chunk per split up to 1280 keys, the
+# double-buffered 128-key chunks above): a full one-chunk split, both sides of the switch, two chunks
+ATTN_S_B1 = ATTN_S + [1152, 1280, 1281, 2048]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -270,7 +273,7 @@ def test_step_attention_kernels_vs_oracle(orc, variant):
     rng = np.random.default_rng(5)
     S = np.array([ATTN_S[b] if b < len(ATTN_S) else int(rng.integers(1, 4097)) for b in range(B)])
     if B == 1:
-        cases = [np.array([s]) for s in ATTN_S]
+        cases = [np.array([s]) for s in ATTN_S_B1]
     else:
         cases = [S]
     worst = 0.0

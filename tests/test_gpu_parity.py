@@ -757,7 +757,7 @@ def _cos_rows(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return torch.nn.functional.cosine_similarity(a.float(), b.float(), dim=-1)
 
 
-@pytest.mark.parametrize("kvd", ["fp8", "int8"])
+@pytest.mark.parametrize("kvd", ["fp8", "int8", "int8-absmax"])
 def test_fp8_kv_codes_and_decode_quality(kvd):
     """One-byte K/V for the batched decode step (FP8 e4m3fn; int8 = the reference's INT8
     KVCacheDtype): (1) the K/V codes a step writes equal torch's e4m3fn / int8 rounding
@@ -767,8 +767,12 @@ def test_fp8_kv_codes_and_decode_quality(kvd):
     0.998 on one attention output (docs/research/notebook.md:690-700); here it is the logits after
     two layers of a random-init model and the LM head, measured at mean ~0.997 (e4m3 keeps 3
     mantissa bits), so the bar is mean >= 0.995, floor 0.99, and >= 80 % equal greedy tokens;
-    (3) paged FP8 == dense FP8 bit for bit."""
+    (3) paged FP8 == dense FP8 bit for bit. int8-absmax: int8 codes at non-power-of-two scales of the
+    reference's absmax / 127 form (kv_cache/kv_cache.py:159-185), where rne(y / s) and rne(y * (1 / s))
+    differ near ties: the device divides, as the header, the oracle and to_int8_codes do."""
     from wfamd.model import KV_CODES, BitNetConfig, BitNetDecoder, from_kv_tiles, synthetic_weights
+    absmax = kvd == "int8-absmax"
+    kvd = "int8" if absmax else kvd
     enc = KV_CODES[kvd][0]
     cfg = BitNetConfig(hidden=512, layers=2, n_heads=4, n_kv_heads=1, head_dim=128, inter=768, vocab=1024,
                        max_seq=2048)
@@ -778,6 +782,8 @@ def test_fp8_kv_codes_and_decode_quality(kvd):
     w["wscale"][:, :3] = 0.05
     B = 20
     scale = [(0.5, 0.25), (1.0, 0.5)] if kvd == "fp8" else [(1 / 16, 1 / 32), (1 / 8, 1 / 16)]
+    if absmax:
+        scale = [(4.37 / 127, 3.91 / 127), (5.03 / 127, 4.66 / 127)]
     bf = BitNetDecoder(cfg, w, batch=B)
     f8 = BitNetDecoder(cfg, w, batch=B, kv_dtype=kvd, kv_scale=scale)
     f8p = BitNetDecoder(cfg, w, batch=B, kv_dtype=kvd, kv_scale=scale, num_pages=B * 64, page_seed=4)

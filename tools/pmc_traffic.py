@@ -26,7 +26,7 @@ def op_name(kernel: str):
     m = re.search(r"k_gemv<wf::Fmt(\w+), (\d)", kernel)
     if m:
         return MODES[m.group(2)], m.group(1)
-    m = re.search(r"k_dec_gemm(?:_t)?<\d+, \d+, \d+, (\d)>", kernel)
+    m = re.search(r"k_dec_gemm(?:_t)?<\d+, \d+, \d+, (\d)[,>]", kernel)
     if m:  # batched matrix-core GEMMs (last template argument = mode)
         return MODES[m.group(1)], "I2S_MFMA" if "k_dec_gemm_t" in kernel else "I2S"
     if "k_attn_part" in kernel or "k_attn_mfma" in kernel:

@@ -85,7 +85,7 @@ struct GemvArgs {
     const int32_t* row_slot;
     // FP8 (e4m3fn) K/V cache: stored code = e4m3(clamp(y / scale, +-448)), RNE
     int kv8;
-    float k_inv, v_inv;
+    float k_div, v_div;  // K / V scales: code = rne(y / scale) exactly as the header, the oracle and the reference
     // batched decode with the row norm fused into the GEMM launch (k_dec_gemm_t PRO != 0): arrival
     // and pass words per 32-sequence tile ([kSeamTiles] each), zero between launches
     unsigned* seam;
@@ -521,7 +521,7 @@ struct EpiDec {
                                 off = (int64_t)slot * g.kv_b_stride + (int64_t)kvh * g.S * 128 +
                                       (proj == 1 ? k_tile_off(pos, d) : v_tile_off(pos, d));
                             }
-                            kv_store(c8 + off, to_kv8(y * (proj == 1 ? g.k_inv : g.v_inv), g.kv8));
+                            kv_store(c8 + off, to_kv8(y / (proj == 1 ? g.k_div : g.v_div), g.kv8));
                             continue;
                         }
                         if (g.pt) {  // paged: block pos >> 5 lives in page pt[slot][pos >> 5]
@@ -1044,8 +1044,8 @@ __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int b
             uint32_t b1[2] = {0u, 0u}, b2[2] = {0u, 0u};
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                b1[e >> 2] |= (uint32_t)to_kv8(y1[e] * g.k_inv, kv8) << (8 * (e & 3));
-                b2[e >> 2] |= (uint32_t)to_kv8(y2[e] * g.k_inv, kv8) << (8 * (e & 3));
+                b1[e >> 2] |= (uint32_t)to_kv8(y1[e] / g.k_div, kv8) << (8 * (e & 3));
+                b2[e >> 2] |= (uint32_t)to_kv8(y2[e] / g.k_div, kv8) << (8 * (e & 3));
             }
             *reinterpret_cast<uint2*>(c8 + o1) = make_uint2(b1[0], b1[1]);
             *reinterpret_cast<uint2*>(c8 + o2) = make_uint2(b2[0], b2[1]);
@@ -1077,7 +1077,7 @@ __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int b
             if (kv8) {
                 uint32_t b[2] = {0u, 0u};
 #pragma unroll
-                for (int e = 0; e < 8; ++e) b[e >> 2] |= (uint32_t)to_kv8(bf2f(vv[e]) * g.v_inv, kv8) << (8 * (e & 3));
+                for (int e = 0; e < 8; ++e) b[e >> 2] |= (uint32_t)to_kv8(bf2f(vv[e]) / g.v_div, kv8) << (8 * (e & 3));
                 *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(g.vc) + off) = make_uint2(b[0], b[1]);
             } else {
                 *reinterpret_cast<uint4*>(g.vc + off) = make_uint4(vv[0] | (uint32_t)vv[1] << 16, vv[2] | (uint32_t)vv[3] << 16,
@@ -1092,7 +1092,7 @@ __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int b
             const int64_t base = g.pt ? (int64_t)s_pg[rl] * g.kv_pgs + (int64_t)kvh * 4096
                                       : (int64_t)s_slot[rl] * g.kv_b_stride + (int64_t)kvh * g.S * 128;
             const int64_t off = base + v_tile_off(g.pt ? (pos & 31) : pos, d);
-            if (kv8) reinterpret_cast<uint8_t*>(g.vc)[off] = to_kv8(bf2f(vv[e]) * g.v_inv, kv8);
+            if (kv8) reinterpret_cast<uint8_t*>(g.vc)[off] = to_kv8(bf2f(vv[e]) / g.v_div, kv8);
             else g.vc[off] = vv[e];
         }
     }
@@ -2047,8 +2047,8 @@ GemvArgs base_args(const wf_model* m, int l) {
     a.kc = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(m->k_cache) + l * kvl * esz);
     a.vc = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(m->v_cache) + l * kvl * esz);
     a.kv8 = d.kv_quant;
-    a.k_inv = d.kv_quant ? 1.0f / m->kv_scale[2 * l] : 1.0f;
-    a.v_inv = d.kv_quant ? 1.0f / m->kv_scale[2 * l + 1] : 1.0f;
+    a.k_div = d.kv_quant ? m->kv_scale[2 * l] : 1.0f;
+    a.v_div = d.kv_quant ? m->kv_scale[2 * l + 1] : 1.0f;
     a.kv_b_stride = (int64_t)d.n_kv_heads * d.max_seq * d.head_dim;
     a.kv_t = m->kv_tiled;
     a.seam = m->seam;

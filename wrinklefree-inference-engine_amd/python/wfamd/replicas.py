@@ -11,7 +11,8 @@ timed region, on the host.
   elapsed time over ranks; `replica_rate` turns that into the whole-job rate.
 * `aggregate` sums per-replica results and reports the spread (BASELINE configs[4]).
 * `launch` starts N replica processes, process i with HIP_VISIBLE_DEVICES=i, and collects the one
-  JSON line each prints (tools/replica_node.py).
+  JSON line each prints (tools/replica_node.py); it hands them a host rendezvous (MASTER_ADDR
+  127.0.0.1 and a free MASTER_PORT) so they can bracket their timed windows with a gloo barrier.
 """
 from __future__ import annotations
 
@@ -96,14 +97,25 @@ def aggregate(results: List[Dict], key: str = "tokens_per_s") -> Dict:
             "per_replica": [round(v, 2) for v in vals]}
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def launch(n: int, argv: List[str], timeout_s: float = 900.0, env_extra: Optional[Dict[str, str]] = None,
            visible_devices: bool = True) -> List[Dict]:
     """Start n replica processes `python argv... --replica i --replicas n` (process i sees GPU i only
     when visible_devices), wait for all, and return the last JSON line each printed. Raises if a
-    replica fails (its stderr tail in the message). The parent never touches the GPU."""
+    replica fails (its stderr tail in the message). The parent never touches the GPU. Every child
+    gets MASTER_ADDR=127.0.0.1 / MASTER_PORT (one free port per launch), RANK and WORLD_SIZE for
+    an optional gloo rendezvous."""
     procs = []
+    port = str(free_port())
     for i in range(n):
         env = dict(os.environ, **(env_extra or {}))
+        env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port, RANK=str(i), WORLD_SIZE=str(n))
         if visible_devices:
             env["HIP_VISIBLE_DEVICES"] = str(i)
         cmd = [sys.executable] + list(argv) + ["--replica", str(i), "--replicas", str(n)]
