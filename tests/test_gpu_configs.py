@@ -232,13 +232,17 @@ def test_decode_batch128_paged_full_width_vs_oracle(orc, kv, B):
                 assert int(dec.tokens[b]) == onext, (i, b)
     # isolated flips: where one bf16 element of an attention output lands within the fp32-vs-double
     # rounding of a bf16 boundary, the int8 requantisation (attn_sub_norm) turns it into code steps
-    # and that row's later layers move by ~1e-2 (tools/diag_ragged_batch.py: batch 40, row 23 at
-    # context 12, the same in graph / eager / dense / paged runs; the batch-1 path shows them at ~1.6 %
-    # of positions, test_prefill_8x2048_full_width_vs_oracle)
-    # a flip stays in that row's cache (its later steps read the moved K/V): count first flips per row
+    # and that row's later layers move by 2-6 % (tools/diag_ragged_batch.py: batch 40, row 23 at
+    # context 12, the same in graph / eager / dense / paged runs). Allowance from the reference
+    # itself (tests/test_gpu_reference_golden.py vs the reference's own decode loop, where the oracle
+    # is bit-exact): batch 1 / batch 128 / prefill flip at 1 + 2 + 0 of 192 positions (1.6 %), each a
+    # single code step (2-6.4 % on the moved row). Here 3 steps x <= 10 rows: expected <= 0.5 flipped
+    # rows; at most 2 distinct rows (a flip stays in that row's cache, its later steps read the moved
+    # K/V), each < 8e-2 (asserted in the loop above at 0.1).
     events = len({b for _, b, _, _, _ in flips})
     print(f"batch {B} paged {kv}: worst logits rel-L2 {worst:.2e} over rows {rows}; isolated flips {flips}")
-    assert events <= max(1, checks // 10), flips
+    assert events <= 2, flips
+    assert all(e < 8e-2 and max(kv) < 8e-2 for _, _, _, e, kv in flips), flips
 
 
 # ------------------------------------------------------------------------------------------------
@@ -452,7 +456,9 @@ def test_prefill_8x2048_full_width_vs_oracle(orc):
                 dbad, dwhole, _ = layer_err(one, 0, l, npos, kr, vr)
                 print(f"  batch-1 decode seq 0 layer {l}: {dbad}/{npos} positions > 1e-3, layer rel-L2 {dwhole:.2e}")
                 assert bad <= 1.5 * dbad + 0.005 * npos and whole <= max(1.5 * dwhole, 1e-4), (l, bad, dbad, whole, dwhole)
-            assert bad <= 0.03 * npos and whole < 5e-3, (b, l, bad, whole)
+            # the GPU paths flip at 1.6 % of positions against the reference's own loop (3 of 192,
+            # tests/test_gpu_reference_golden.py; the oracle there is bit-exact): allowance 2.5 %
+            assert bad <= 0.025 * npos and whole < 5e-3, (b, l, bad, whole)
         if b == 0:  # next-step logits: the prefilled batch-16 step and the batch-1 path vs the oracle
             ologits, onext = m.step(prompts[0][n], n)
             one.set_state([prompts[0][n]], [n])
