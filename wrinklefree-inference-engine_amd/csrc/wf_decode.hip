@@ -164,7 +164,8 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
     WF_STAMP(0);
 
     // 1) the input row (issued first: vmcnt retires in order), 2) the weight stream, 3) residual
-    NormRow<PPT == 0 ? 1 : PPT, kNT> nr;
+    constexpr int kNormPPT = PPT == 0 ? 1 : PPT;
+    NormRow<kNormPPT, kNT> nr;
     constexpr bool kAttnIn = (MODE == MODE_O && PPT > 0);
     AttnRow<kAttnIn ? PPT : 1, kNT, kAttnPartSplits1> ar;  // batch < 16: the k_attn_part records
     constexpr int kMaxPiecesPerThread = 8192 / 16 / kNT;  // staged int8: K_pad <= 8192
@@ -226,14 +227,15 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
         float y[PPT][8];
         if constexpr (kAttnIn) {
             ar.finish(a.Hq, 128, y);
-            sf[0] = norm_core(nr, K, a.eps, y, red);
+            sf[0] = norm_core<kNormPPT, kNT, 512u * MODE>(nr, K, a.eps, y, red);
         } else if constexpr (MODE == MODE_LINEAR) {  // quantize x itself (no norm)
             unpack_row(nr, K, y);
             sf[0] = absmax_scale<PPT, kNT>(y, red);
         } else {
-            sf[0] = norm_row(nr, K, a.eps, y, red);
+            sf[0] = norm_row<kNormPPT, kNT, 512u * MODE>(nr, K, a.eps, y, red);
         }
-        int as = quant_row<PPT, kNT>(y, sf[0], F::k_pad(K) / 8, smem, [](int p) { return F::lds_off(8 * p); });
+        const auto lds_at = [](int p) { return F::lds_off(8 * p); };
+        int as = quant_row<PPT, kNT, decltype(lds_at), 512u * MODE>(y, sf[0], F::k_pad(K) / 8, smem, lds_at);
         as = wave_sum_i(as);
         if ((threadIdx.x & 63) == 0) red_i[threadIdx.x >> 6] = as;
     } else {
@@ -705,7 +707,7 @@ __device__ __forceinline__ float norm_core_e512(const NormRow<PPT2, 256>& r, int
         red[wave + 4] = ss[1];
     }
     __syncthreads();
-    const float rr = rbf(1.0f / sqrtf(tree_sum<8>(red) / (float)K + eps));
+    const float rr = rms_factor(div_rn(tree_sum<8>(red), (float)K, 1.0f / (float)K) + eps);
     float mx = 0.f;
 #pragma unroll
     for (int i = 0; i < PPT2; ++i) {
@@ -723,14 +725,14 @@ __device__ __forceinline__ float norm_core_e512(const NormRow<PPT2, 256>& r, int
     if (lane == 0) red[8 + wave] = mx;
     __syncthreads();
     mx = fmaxf(fmaxf(red[8], red[9]), fmaxf(red[10], red[11]));
-    return (float)act_scale_from_max(mx);
+    return act_scale_f(mx);
 }
 
 // codes of the NT-thread pieces into the tile layout, write-through (the in-launch hand-off)
 template <int PPT, int NT>
 __device__ __forceinline__ int quant_row_tiled_wt(const float (&y)[PPT][8], float sf, int npad, int8_t* base, int row,
                                                   int nkb) {
-    const float inv = 1.0f / sf;
+    const float inv = rcp_1ulp(sf);
     int asum = 0;
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
@@ -1554,7 +1556,7 @@ __global__ __launch_bounds__(512) void k_rownorm_tile8(const uint16_t* __restric
 #pragma unroll
     for (int v = 0; v < 8; ++v) W[v] = wave_sum(ss[v]);
     __syncthreads();  // s_nw complete
-    const float rr = rbf(1.0f / sqrtf(tree_sum<8>(W) / (float)K + eps));
+    const float rr = rms_factor(div_rn(tree_sum<8>(W), (float)K, 1.0f / (float)K) + eps);
     float m = 0.f;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {  // xv[j] <- the normalised row, packed bf16 (0 past the row)
@@ -1575,8 +1577,8 @@ __global__ __launch_bounds__(512) void k_rownorm_tile8(const uint16_t* __restric
     // the codes pass re-reads the packed row (without the fence hipcc keeps all 8 NP floats live)
 #pragma unroll
     for (int j = 0; j < NP; ++j) reg_fence(xv[j]);
-    const float s = (float)act_scale_from_max(wave_max(m));
-    const float inv = 1.0f / s;
+    const float s = act_scale_f(wave_max(m));
+    const float inv = rcp_1ulp(s);
     int as = 0;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {

@@ -176,26 +176,53 @@ __device__ __forceinline__ int8_t quant_one(float x, float sf) {
     v = fminf(fmaxf(v, -128.f), 127.f);
     return (int8_t)(int)v;
 }
-// Eight codes at once, bit-identical to quant_one. The exact product x * inv (inv = 1/s rounded)
-// is within 2^-17 of x/s for |x/s| <= 128, so rne(x/s) = rne(x * inv) unless x * inv lies within
-// 2^-13 of a half-integer; only then (p ~ 2.4e-4 per element) that element is redone with the
-// IEEE divide (per element: a wave pays one divide sequence when any of its lanes needs it for that
-// element, not eight -- with eight waves per block nearly every block had a wave on the slow path).
-// rne comes from the fma's own rounding: fma(x, inv, 1.5 * 2^23) keeps rne(x * inv) in the low
-// mantissa bits (low byte = the int8 code), fma(x, inv, -q) is the exact remainder. No clamp is
-// needed: s = max|x| / 127 bounds |x * inv| by 127 (1 + 2^-23). Returns the 8 codes packed
-// little-endian; adds them to `asum`.
+
+// Correctly rounded quotient without the IEEE divide sequence (Markstein): given yb within 1 ulp of
+// 1/b (RN(1/b) for the 1/K use), q = RN(a*yb) is within an ulp of a/b, the fma remainder
+// r = a - q*b is exact, and RN(q + r*yb) = RN(a/b) for finite a/b clear of over/underflow.
+// Checked on the host against the IEEE divide: 1.2e8 random a for K in {128 .. 6912}, every
+// positive bf16 numerator over 127, 1.8e8 quantizer cases incl. constructed half-integer ties, with
+// yb exact and +-1 ulp (round 4; tools/check_fast_arith.c).
+__device__ __forceinline__ float div_rn(float a, float b, float yb) {
+    const float q = a * yb;
+    const float r = fmaf(-q, b, a);
+    return fmaf(r, yb, q);
+}
+// 1/b within 1 ulp (v_rcp_f32 + one Newton step; b normal)
+__device__ __forceinline__ float rcp_1ulp(float b) {
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    return fmaf(fmaf(-b, y0, 1.0f), y0, y0);
+}
+// (float)act_scale_from_max(m) in fp32: float(double(m) / 127) == RN_f32(m / 127) (the double
+// rounding cannot bite: m / 127 has a 7-bit period, so bits 25..53 are never a midpoint pattern),
+// and double(m) < 1e-6 <=> m <= float(1e-6) = 9.99999997e-07f.
+__device__ __forceinline__ float act_scale_f(float m) {
+    if (m <= 9.99999997e-07f) return 1.0f / 127.0f;
+    return div_rn(m, 127.0f, 1.0f / 127.0f);
+}
+// rbf(1 / sqrtf(v)) (IEEE sqrt, IEEE divide, bf16 RNE: the rms_norm factor of
+// scripts/direct_inference_full.py:181-184 as the oracle computes it). v_rsq_f32 is within 1 ulp
+// of 1/sqrt(v) and the two-rounding reference within 1.5 ulp, so their bf16 roundings agree unless
+// the fp32 value sits within a few ulps of a bf16 midpoint: there (p ~ 2e-3, wave-uniform: v is
+// the same in every lane) the exact sequence runs.
+__device__ __forceinline__ float rms_factor(float v) {
+    const float a = __builtin_amdgcn_rsqf(v);
+    const uint32_t lo = __float_as_uint(a) & 0xffffu;
+    if (lo - (0x8000u - 64u) < 128u) return rbf(1.0f / sqrtf(v));
+    return rbf(a);
+}
+// Eight codes at once, bit-identical to quant_one: rne(RN(x / s)) -- the reference divides in
+// fp32 (tests/test_bitnet_core.py:144: (activations / scale).round()), so the quotient is rounded
+// to fp32 BEFORE the round-to-integer (x / s a hair below k + 1/2 can round up to k + 1/2 and then
+// to even). RN(x / s) by div_rn (inv = 1/s within 1 ulp), then + 1.5 * 2^23 rounds it to the
+// integer (RNE) in the add and leaves the code in the low byte. No clamp: s = max|x| / 127 bounds
+// |x / s| by 127 (1 + 2^-23). Branch-free (the former form re-divided near-ties under a branch per
+// element). Returns the 8 codes packed little-endian; adds them to `asum`.
 __device__ __forceinline__ uint2 quant8(const float (&x)[8], float sf, float inv, int& asum) {
     constexpr float kMagic = 12582912.0f;  // 1.5 * 2^23
     uint32_t b[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const float sm = fmaf(x[j], inv, kMagic);
-        const float q = sm - kMagic;
-        b[j] = __float_as_uint(sm);
-        if (fabsf(fmaf(x[j], inv, -q)) > 0.4998779296875f)  // within 2^-13 of a half-integer
-            b[j] = __float_as_uint(fminf(fmaxf(rintf(x[j] / sf), -128.f), 127.f) + kMagic);
-    }
+    for (int j = 0; j < 8; ++j) b[j] = __float_as_uint(div_rn(x[j], sf, inv) + kMagic);
     const uint32_t lo = __builtin_amdgcn_perm(b[1], b[0], 0x0c0c0400u) | __builtin_amdgcn_perm(b[3], b[2], 0x04000c0cu);
     const uint32_t hi = __builtin_amdgcn_perm(b[5], b[4], 0x0c0c0400u) | __builtin_amdgcn_perm(b[7], b[6], 0x04000c0cu);
     asum = sdot4_ones(lo, sdot4_ones(hi, asum));
