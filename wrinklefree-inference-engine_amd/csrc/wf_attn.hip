@@ -440,14 +440,35 @@ __device__ __forceinline__ void attn_part_body(const uint16_t* __restrict__ q, i
         }
     }
     WF_STAMP(1);
-    if (li == 0) {
+    // merge the NG lane groups: first the four groups of each wave (lanes l, l ^ 16, l ^ 32 hold the
+    // same dims) by two shuffle steps, then the waves through LDS -- a 4-way merge per output instead
+    // of NG = 16 (the former all-LDS merge took ~1 us of a ~4.9 us launch, in-graph stamps r03)
 #pragma unroll
-        for (int h = 0; h < G; ++h) { sm_m[gid][h] = m[h]; sm_l[gid][h] = l[h]; }
+    for (int off = 16; off <= 32; off *= 2) {
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            const float m2 = __shfl_xor(m[h], off, 64), l2 = __shfl_xor(l[h], off, 64);
+            const float M = fmaxf(m[h], m2);
+            const float a = (m[h] == -INFINITY) ? 0.f : __expf(m[h] - M);
+            const float c = (m2 == -INFINITY) ? 0.f : __expf(m2 - M);
+            l[h] = l[h] * a + l2 * c;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[h][j] = o[h][j] * a + __shfl_xor(o[h][j], off, 64) * c;
+            m[h] = M;
+        }
     }
+    constexpr int NWV = kAttnPartThreads / 64;
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) < LP) {  // lane group 0 of each wave holds the wave's merge
+        if (li == 0) {
 #pragma unroll
-    for (int h = 0; h < G; ++h) {
-        *reinterpret_cast<float4*>(&sm_o[gid][h][li * 8]) = make_float4(o[h][0], o[h][1], o[h][2], o[h][3]);
-        *reinterpret_cast<float4*>(&sm_o[gid][h][li * 8 + 4]) = make_float4(o[h][4], o[h][5], o[h][6], o[h][7]);
+            for (int h = 0; h < G; ++h) { sm_m[wv][h] = m[h]; sm_l[wv][h] = l[h]; }
+        }
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            *reinterpret_cast<float4*>(&sm_o[wv][h][li * 8]) = make_float4(o[h][0], o[h][1], o[h][2], o[h][3]);
+            *reinterpret_cast<float4*>(&sm_o[wv][h][li * 8 + 4]) = make_float4(o[h][4], o[h][5], o[h][6], o[h][7]);
+        }
     }
     __syncthreads();
     constexpr int D4 = D / 4;
@@ -455,10 +476,10 @@ __device__ __forceinline__ void attn_part_body(const uint16_t* __restrict__ q, i
         const int h = idx / D4, d = (idx - h * D4) * 4;
         float mx = -INFINITY;
 #pragma unroll
-        for (int w = 0; w < NG; ++w) mx = fmaxf(mx, sm_m[w][h]);
+        for (int w = 0; w < NWV; ++w) mx = fmaxf(mx, sm_m[w][h]);
         float ls = 0.f, os[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-        for (int w = 0; w < NG; ++w) {
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) {
             const float a = (sm_m[w][h] == -INFINITY) ? 0.f : __expf(sm_m[w][h] - mx);
             ls += sm_l[w][h] * a;
             const float4 ov = *reinterpret_cast<const float4*>(&sm_o[w][h][d]);

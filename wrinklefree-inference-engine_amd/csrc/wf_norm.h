@@ -205,52 +205,6 @@ __device__ __forceinline__ float tree_sum(const float* r) {
     if constexpr (W == 1) return r[0];
     else return tree_sum<W / 2>(r) + tree_sum<W / 2>(r + W / 2);
 }
-// The quantizer scale needs max|y| over the row, y = bf16(bf16(x r) w), r known only after the
-// sum-of-squares round. Every |y_i| lies within a factor (1 +- 2^-8)^2 of a_i r, a_i = |x_i w_i|
-// (exact in fp32: bf16 x bf16), so when the largest a_i beats the runner-up by more than that
-// factor (a2 < a1 * 63/64 < a1 ((1 - 2^-8) / (1 + 2^-8))^2) the max of y is that element's y: the
-// first round carries (a1, a2, x and w of a1) beside the sum of squares, and the second block
-// reduction runs only when the top two are that close (or tied) -- the result is max|y| exactly
-// either way. WF_NORM_TOP2=0 (study builds): always the second round.
-#ifndef WF_NORM_TOP2
-#define WF_NORM_TOP2 1
-#endif
-struct Top2 {
-    float a1, a2;
-    uint32_t pay;  // bf16 bits: x << 16 | w
-    __device__ __forceinline__ void add(float a, uint32_t p) {
-        const bool gt = a > a1;
-        a2 = __builtin_amdgcn_fmed3f(a1, a2, a);  // a1 >= a2: the second largest of the three
-        a1 = fmaxf(a1, a);
-        pay = gt ? p : pay;
-    }
-    __device__ __forceinline__ void merge(float o1, float o2, uint32_t op) {
-        const bool gt = o1 > a1;
-        a2 = fmaxf(fmaxf(a2, o2), fminf(a1, o1));
-        a1 = fmaxf(a1, o1);
-        pay = gt ? op : pay;
-    }
-    template <int CTRL, int RM = 0xF>
-    __device__ __forceinline__ void dpp_merge() {  // identity for rows outside RM: (-1, -1)
-        const float o1 = dpp_f<CTRL, RM>(a1, -1.0f), o2 = dpp_f<CTRL, RM>(a2, -1.0f);
-        const uint32_t op = (uint32_t)dpp_i<CTRL, RM>((int)pay, 0);
-        merge(o1, o2, op);
-    }
-    // whole wave -> lane 63 (wave_reduce's DPP pattern), broadcast by readlane
-    __device__ __forceinline__ void wave_reduce() {
-        dpp_merge<DPP_QP_1032>();
-        dpp_merge<DPP_QP_2301>();
-        dpp_merge<DPP_HALF_MIRROR>();
-        dpp_merge<DPP_MIRROR>();
-        dpp_merge<DPP_BCAST15, 0xA>();
-        dpp_merge<DPP_BCAST31, 0xC>();
-        a1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a1), 63));
-        a2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a2), 63));
-        pay = (uint32_t)__builtin_amdgcn_readlane((int)pay, 63);
-    }
-};
-
-// wf_stamp_base: the caller's stamp region (diagnostic stamps build only; shadows the default 0)
 template <int PPT, int NT, unsigned wf_stamp_base = 0>
 __device__ __forceinline__ float norm_core(const NormRow<PPT, NT>& r, int K, float eps, float (&y)[PPT][8], float* red,
                                            bool want_scale = true) {
@@ -264,45 +218,12 @@ __device__ __forceinline__ float norm_core(const NormRow<PPT, NT>& r, int K, flo
         for (int j = 0; j < 8; ++j) ss = fmaf(y[i][j], y[i][j], ss);
     WF_STAMP(8);
     ss = wave_sum(ss);
-    constexpr bool kTop2 = WF_NORM_TOP2 != 0;
-    __shared__ float4 top_red[kTop2 ? NW : 1];
-    Top2 t{-1.0f, -1.0f, 0u};
-    if (kTop2 && want_scale) {
-#pragma unroll
-        for (int i = 0; i < PPT; ++i) {
-            const uint32_t n4[4] = {r.w[i].x, r.w[i].y, r.w[i].z, r.w[i].w};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                // y holds x (0 past the row): a = |x w|, payload = the two bf16 bit patterns
-                t.add(fabsf(y[i][2 * j] * bf_lo(n4[j])), (__float_as_uint(y[i][2 * j]) & 0xffff0000u) | (n4[j] & 0xffffu));
-                t.add(fabsf(y[i][2 * j + 1] * bf_hi(n4[j])), (__float_as_uint(y[i][2 * j + 1]) & 0xffff0000u) | (n4[j] >> 16));
-            }
-        }
-        t.wave_reduce();
-        if (lane == 0) top_red[wave] = make_float4(t.a1, t.a2, __uint_as_float(t.pay), 0.f);
-    }
     if (lane == 0) red[wave] = ss;
     __syncthreads();
     WF_STAMP(9);
     ss = tree_sum<NW>(red);
     const float rr = rms_factor(div_rn(ss, fK, invK) + eps);  // == rbf(1 / sqrtf(ss / K + eps))
-    bool unique = false;
     float mx = 0.f;
-    if (kTop2 && want_scale) {
-        t = Top2{-1.0f, -1.0f, 0u};
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            const float4 v = top_red[w];
-            t.merge(v.x, v.y, __float_as_uint(v.z));
-        }
-        if (t.a1 <= 0.f) {  // an all-zero row
-            unique = true;
-        } else if (t.a2 < t.a1 * 0.984375f) {
-            unique = true;
-            const uint32_t a = pk_bf16(__uint_as_float(t.pay & 0xffff0000u) * rr, 0.f);
-            mx = fabsf(bf_lo(pk_bf16(bf_lo(a) * __uint_as_float(t.pay << 16), 0.f)));
-        }
-    }
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
         const uint32_t n4[4] = {r.w[i].x, r.w[i].y, r.w[i].z, r.w[i].w};
@@ -312,23 +233,18 @@ __device__ __forceinline__ float norm_core(const NormRow<PPT, NT>& r, int K, flo
             const uint32_t b = pk_bf16(bf_lo(a) * bf_lo(n4[j]), bf_hi(a) * bf_hi(n4[j]));
             y[i][2 * j] = bf_lo(b);
             y[i][2 * j + 1] = bf_hi(b);
+            mx = fmaxf(mx, fmaxf(fabsf(y[i][2 * j]), fabsf(y[i][2 * j + 1])));
         }
     }
     if (!want_scale) return 0.f;
     WF_STAMP(10);
-    if (!unique) {  // block-uniform (every thread merged the same records)
+    mx = wave_max(mx);
+    if (lane == 0) red[NW + wave] = mx;
+    __syncthreads();
+    WF_STAMP(11);
+    mx = red[NW];
 #pragma unroll
-        for (int i = 0; i < PPT; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(y[i][j]));
-        mx = wave_max(mx);
-        if (lane == 0) red[NW + wave] = mx;
-        __syncthreads();
-        WF_STAMP(11);
-        mx = red[NW];
-#pragma unroll
-        for (int i = 1; i < NW; ++i) mx = fmaxf(mx, red[NW + i]);
-    }
+    for (int i = 1; i < NW; ++i) mx = fmaxf(mx, red[NW + i]);
     return act_scale_f(mx);
 }
 // Activation scale of a row without normalisation (BitNetLinear's own quantizer,
