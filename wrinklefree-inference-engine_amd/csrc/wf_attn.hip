@@ -443,20 +443,34 @@ __device__ __forceinline__ void attn_part_body(const uint16_t* __restrict__ q, i
     // merge the NG lane groups: first the four groups of each wave (lanes l, l ^ 16, l ^ 32 hold the
     // same dims) by two shuffle steps, then the waves through LDS -- a 4-way merge per output instead
     // of NG = 16 (the former all-LDS merge took ~1 us of a ~4.9 us launch, in-graph stamps r03)
-#pragma unroll
-    for (int off = 16; off <= 32; off *= 2) {
+    // v_permlane16_swap / v_permlane32_swap on (v, v) hand every lane its (lower, upper) pair of
+    // lanes l, l ^ 16 (then l, l ^ 32) in the same order, so both partners compute the same merge
+    auto pair16 = [](float v) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        return make_float2(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    };
+    auto pair32 = [](float v) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        return make_float2(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    };
+    auto merge_step = [&](auto pair) {
 #pragma unroll
         for (int h = 0; h < G; ++h) {
-            const float m2 = __shfl_xor(m[h], off, 64), l2 = __shfl_xor(l[h], off, 64);
-            const float M = fmaxf(m[h], m2);
-            const float a = (m[h] == -INFINITY) ? 0.f : __expf(m[h] - M);
-            const float c = (m2 == -INFINITY) ? 0.f : __expf(m2 - M);
-            l[h] = l[h] * a + l2 * c;
+            const float2 mm = pair(m[h]), ll = pair(l[h]);
+            const float M = fmaxf(mm.x, mm.y);
+            const float a = (mm.x == -INFINITY) ? 0.f : __expf(mm.x - M);
+            const float c = (mm.y == -INFINITY) ? 0.f : __expf(mm.y - M);
+            l[h] = ll.x * a + ll.y * c;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) o[h][j] = o[h][j] * a + __shfl_xor(o[h][j], off, 64) * c;
+            for (int j = 0; j < 8; ++j) {
+                const float2 oo = pair(o[h][j]);
+                o[h][j] = oo.x * a + oo.y * c;
+            }
             m[h] = M;
         }
-    }
+    };
+    merge_step(pair16);
+    merge_step(pair32);
     constexpr int NWV = kAttnPartThreads / 64;
     const int wv = threadIdx.x >> 6;
     if ((threadIdx.x & 63) < LP) {  // lane group 0 of each wave holds the wave's merge
@@ -599,14 +613,17 @@ struct KvFrag<2> : KvFrag8<2> {};
 // PAIR: records of 2 waves -- grid.x = kAttnPartSplits / 2, the 16 waves of (b, g) take the
 // tiles round-robin and each block merges its wave pairs (0, 1) and (2, 3) into 2 records: half the
 // per-tile block overheads of the 4-wave records, twice the waves per sequence of WREC.
-template <bool DB, bool RR, bool WREC = false, int KV8 = 0, bool PAIR = false>
+// TAIL: the records are stored write-through and the last block of each sequence forms the O
+// projection's input row (wf_norm.h AttnTail) -- no k_rownorm_attn launch.
+template <bool DB, bool RR, bool WREC = false, int KV8 = 0, bool PAIR = false, bool TAIL = false>
 __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* __restrict__ q, int64_t q_sb,
                                                    const uint16_t* __restrict__ K, const uint16_t* __restrict__ Vt,
                                                    int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv, int S,
                                                    const int32_t* __restrict__ seq_lens, float sm_scale,
                                                    float2* __restrict__ ml_out, float* __restrict__ o_out,
                                                    const int32_t* __restrict__ pt, int pps, int npages, int64_t kv_pgs,
-                                                   float v_scale) {
+                                                   float v_scale, AttnTail tail) {
+    static_assert(!(TAIL && (WREC || PAIR)), "the tail follows the per-block records");
     constexpr int D = 128;
     using KF = KvFrag<KV8>;
     using FT = typename KF::T;
@@ -788,11 +805,52 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
             os[0] += ov.x * a; os[1] += ov.y * a; os[2] += ov.z * a; os[3] += ov.w * a;
         }
         const int64_t rec = (int64_t)(b * Hq + hq0 + h) * kAttnPartSplits + s;
-        *reinterpret_cast<float4*>(o_out + part_o_off(rec / kAttnPartSplits, (int)(rec % kAttnPartSplits), d)) =
-            make_float4(os[0], os[1], os[2], os[3]);
-        if (d == 0) ml_out[rec] = make_float2(mx, ls);
+        const int64_t oe = part_o_off(rec / kAttnPartSplits, (int)(rec % kAttnPartSplits), d);
+        if constexpr (TAIL) {  // write-through: the sequence's last block reads them in this launch
+            st16_sc1(make_rsrc(o_out), (int)(4 * oe), __builtin_bit_cast(uint4, make_float4(os[0], os[1], os[2], os[3])));
+            if (d == 0) st_sc1(reinterpret_cast<uint64_t*>(ml_out) + rec, __builtin_bit_cast(uint64_t, make_float2(mx, ls)));
+        } else {
+            *reinterpret_cast<float4*>(o_out + oe) = make_float4(os[0], os[1], os[2], os[3]);
+            if (d == 0) ml_out[rec] = make_float2(mx, ls);
+        }
     }
     WF_STAMP(2);
+    if constexpr (TAIL) {
+        // ticket of sequence b (MI355X_MICROARCH.md Valid forms row 1): every storing wave drains its
+        // write-through stores, the block meets at a barrier, one lane adds; the block whose add
+        // returns n - 1 re-arms the counter and reads the records with sc1 loads
+        __shared__ int sh_last;
+        __shared__ float red[16];
+        __shared__ int red_i[4];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned* c = tail.cnt + (int64_t)b * kTailLine;
+            const unsigned n = gridDim.x * gridDim.y;
+            const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sh_last = (old == n - 1u);
+            if (old == n - 1u) st_sc1(c, 0u);
+        }
+        __syncthreads();
+        if (!sh_last) return;
+        const int Kr = Hq * D, nkb = Kr >> 7;
+        AttnRow<2, 256, kAttnPartSplits> ar;
+        ar.template issue<true>(ml_out, o_out, b, Hq, D);
+        NormRow<2, 256> nr;
+        nr.issue_w(tail.nw, Kr);
+        float y[2][8];
+        ar.finish(Hq, D, y);
+        const float sf = norm_core_e512(nr, Kr, tail.eps, y, red);
+        int as = quant_row_tiled<2, 256>(y, sf, Kr / 8, tail.q8, b, nkb);
+        as = wave_sum_i(as);
+        if ((threadIdx.x & 63) == 0) red_i[threadIdx.x >> 6] = as;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            tail.asum[b] = red_i[0] + red_i[1] + red_i[2] + red_i[3];
+            tail.sf[b] = sf;
+        }
+        WF_STAMP(3);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1253,7 +1311,7 @@ int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const 
 int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
                               float2* ml, float* o, hipStream_t st, bool kv_tiled, const int32_t* pt, int pps,
-                              int npages, int64_t kv_pgs, int kv8, float k_scale, float v_scale) {
+                              int npages, int64_t kv_pgs, int kv8, float k_scale, float v_scale, const AttnTail* tail) {
     const int grp = Hq / Hkv;
     if (grp > 8) {
         set_error("decode_attention_partials: GQA group %d > 8", grp);
@@ -1274,15 +1332,25 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
             set_error("decode_attention_partials: tiled K/V need S %% 32 == 0 (S=%d)", S);
             return WF_EINVAL;
         }
-        if (kv8 == 2)  // int8 caches: as FP8, a wider in-register decode
-            hipLaunchKernelGGL((k_attn_mfma<false, false, false, 2>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
-                               kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale, ml, o, pt, pps, npages, kv_pgs, v_scale);
-        else if (kv8)  // FP8 caches: K scale folded into the score scale; one tile in flight per wave, 4 waves per SIMD
-            hipLaunchKernelGGL((k_attn_mfma<false, false, false, 1>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb,
-                               kv_sh, Hq, Hkv, S, seq_lens, sm_scale * k_scale, ml, o, pt, pps, npages, kv_pgs, v_scale);
-        else  // bf16: double-buffered tiles, 2 waves per SIMD (at 4 splits a wave takes >= 2 tiles at ctx >= 1024)
-            hipLaunchKernelGGL((k_attn_mfma<true, false>), grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv,
-                               S, seq_lens, sm_scale, ml, o, pt, pps, npages, kv_pgs, 1.0f);
+        if (tail && Hq * 128 > 4096) {
+            set_error("decode_attention_partials: the fused row norm handles Hq * 128 <= 4096 (Hq=%d)", Hq);
+            return WF_EINVAL;
+        }
+        const AttnTail tl = tail ? *tail : AttnTail{};
+#define WF_AM(DBV, KV8V, TAILV, SCALE, VSC)                                                                        \
+    hipLaunchKernelGGL((k_attn_mfma<DBV, false, false, KV8V, false, TAILV>), grid, dim3(256), 0, st, q, q_sb, k, v, \
+                       kv_sb, kv_sh, Hq, Hkv, S, seq_lens, SCALE, ml, o, pt, pps, npages, kv_pgs, VSC, tl)
+        if (kv8 == 2) {  // int8 caches: as FP8, a wider in-register decode
+            if (tail) WF_AM(false, 2, true, sm_scale * k_scale, v_scale);
+            else WF_AM(false, 2, false, sm_scale * k_scale, v_scale);
+        } else if (kv8) {  // FP8 caches: K scale folded into the score scale; one tile in flight per wave, 4 waves per SIMD
+            if (tail) WF_AM(false, 1, true, sm_scale * k_scale, v_scale);
+            else WF_AM(false, 1, false, sm_scale * k_scale, v_scale);
+        } else {  // bf16: double-buffered tiles, 2 waves per SIMD (at 4 splits a wave takes >= 2 tiles at ctx >= 1024)
+            if (tail) WF_AM(true, 0, true, sm_scale, 1.0f);
+            else WF_AM(true, 0, false, sm_scale, 1.0f);
+        }
+#undef WF_AM
         return check_launch("decode_attention_partials");
     }
     // batch >= 16 on untiled caches (TQ weights, or max_seq % 32 != 0): the VALU kernel, one block per

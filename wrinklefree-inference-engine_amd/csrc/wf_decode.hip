@@ -37,7 +37,7 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
                               float2* ml, float* o, hipStream_t st, bool kv_tiled, const int32_t* pt = nullptr,
                               int pps = 0, int npages = 0, int64_t kv_pgs = 0, int kv8 = 0, float k_scale = 1.f,
-                              float v_scale = 1.f);
+                              float v_scale = 1.f, const AttnTail* tail = nullptr);
 
 enum { MODE_QKV = 0, MODE_O = 1, MODE_GU = 2, MODE_DN = 3, MODE_LINEAR = 4 };  // LINEAR: BitNetLinear drop-in
 constexpr int kNT = 512;  // threads per GEMV / row-norm block (8 waves: 2 per SIMD hide the input-stage latency)
@@ -89,6 +89,12 @@ struct GemvArgs {
     // batched decode with the row norm fused into the GEMM launch (k_dec_gemm_t PRO != 0): arrival
     // and pass words per 32-sequence tile ([kSeamTiles] each), zero between launches
     unsigned* seam;
+    // batch 1, layer 0 (k_gemv PPT > 0): the input row (QKV) / residual row (O) is the token's row
+    // of the embedding table (x / resid = the table, row clamp(x_tok[b], 0, vocab - 1)) -- no embed
+    // launch; QKV also sets seq_out[b] = positions[b] + 1 (what k_embed did)
+    const int32_t* x_tok;
+    int vocab;
+    int32_t* seq_out;
 };
 constexpr int kSeamTiles = 8;  // 32-sequence tiles: batch <= 256 (kDecGemmMaxB)
 // one 128-byte line per seam word: memory-side atomics and polls on one line serialise (the batch-1
@@ -176,8 +182,9 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
         nr.issue_w(a.nw, K);
     } else if constexpr (PPT > 0 && MODE == MODE_LINEAR) {
         nr.issue_x(a.x + (int64_t)b0 * a.x_stride, K);
-} else if constexpr (PPT > 0) {
-        nr.issue(a.x + (int64_t)b0 * a.x_stride, a.nw, K);
+    } else if constexpr (PPT > 0) {
+        const int xrow = a.x_tok ? min(max(a.x_tok[b0], 0), a.vocab - 1) : b0;  // scalar load
+        nr.issue(a.x + (int64_t)xrow * a.x_stride, a.nw, K);
     } else {
 #pragma unroll
         for (int m = 0; m < MB; ++m)
@@ -200,8 +207,10 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
         resid_raw[m] = 0;
-        if constexpr (MODE == MODE_O || MODE == MODE_DN)
-            resid_raw[m] = a.resid[(int64_t)(b0 + m) * a.out_stride + min(row, N - 1)];
+        if constexpr (MODE == MODE_O || MODE == MODE_DN) {
+            const int rrow = (MODE == MODE_O && MB == 1 && a.x_tok) ? min(max(a.x_tok[b0], 0), a.vocab - 1) : b0 + m;
+            resid_raw[m] = a.resid[(int64_t)rrow * a.out_stride + min(row, N - 1)];
+        }
     }
     // batch 1 QKV: the RoPE entries of the epilogue (position: a scalar load, so the wait for it
     // does not drain the vector loads above)
@@ -306,6 +315,7 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
             for (int m = 0; m < MB; ++m) s_out[m][lrow] = rbf(corrected(acc[m], wsp, asum[m], sf[m]));
         }
         __syncthreads();
+        if (MB == 1 && a.seq_out && blockIdx.x == 0 && threadIdx.x == 0) a.seq_out[b0] = a.positions[b0] + 1;
         if (threadIdx.x < 8 * MB) {
             const int m = threadIdx.x >> 3, i = threadIdx.x & 7;
             const int bi = b0 + m;
@@ -348,6 +358,20 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
                 g.out[(int64_t)(b0 + m) * g.ld + g.col] = f2bf(s_out[m][i]);
             }
         }
+    } else if constexpr ((MODE == MODE_O || MODE == MODE_DN) && MB == 1 && LPR == 32) {
+        // O/DN at batch 1: a wave holds rows 2w (lanes 0-31) and 2w + 1 (lanes 32-63), every lane of a
+        // row has its sum; lane 0 takes its partner's value by v_permlane32_swap and stores the pair
+        // as one 4-byte word -- no LDS round and no block barrier before the store
+        const float v = rbf(bf2f(resid_raw[0]) + rbf(corrected(acc[0], a.ws0, asum[0], sf[0])));
+        const auto pr = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        if ((threadIdx.x & 63) == 0) {
+            uint16_t* o = a.out + (int64_t)b0 * a.out_stride + row;
+            if (row + 1 < N)
+                *reinterpret_cast<uint32_t*>(o) = pk_bf16(__uint_as_float(pr[0]), __uint_as_float(pr[1]));
+            else if (row < N)
+                *o = f2bf(__uint_as_float(pr[0]));
+        }
+        WF_STAMP(3);
     } else {
         // O/DN: out[row] = bf16(resid + bf16(o)); GU: act[8t+i] = bf16(bf16(relu(g)^2) * u)
         if (sub == 0) {
@@ -687,47 +711,6 @@ __global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm(GemvArgs a) {
 // gridDim.x >= 32. PRO 1: rms_norm of x (a.x, a.nw); PRO 2: the attention row merged from the
 // decode-attention records (a.part_ml / a.part_o, kAttnPartSplits per head), then rms_norm.
 constexpr unsigned kSeamSpin = 1u << 22;  // polls before a waiting block gives up (never in a valid launch)
-template <int PPT2>
-__device__ __forceinline__ float norm_core_e512(const NormRow<PPT2, 256>& r, int K, float eps, float (&y)[PPT2][8],
-                                                float* red) {
-    // 256 threads replaying the 512-thread norm_core: virtual thread t + 256 j owns pieces 2 i + j
-    static_assert(PPT2 % 2 == 0, "two virtual threads per lane");
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    float ss[2] = {0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < PPT2 / 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) ss[j] = fmaf(y[2 * i + j][e], y[2 * i + j][e], ss[j]);
-    ss[0] = wave_sum(ss[0]);
-    ss[1] = wave_sum(ss[1]);
-    if (lane == 0) {
-        red[wave] = ss[0];
-        red[wave + 4] = ss[1];
-    }
-    __syncthreads();
-    const float rr = rms_factor(div_rn(tree_sum<8>(red), (float)K, 1.0f / (float)K) + eps);
-    float mx = 0.f;
-#pragma unroll
-    for (int i = 0; i < PPT2; ++i) {
-        const uint32_t n4[4] = {r.w[i].x, r.w[i].y, r.w[i].z, r.w[i].w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t a = pk_bf16(y[i][2 * j] * rr, y[i][2 * j + 1] * rr);
-            const uint32_t b = pk_bf16(bf_lo(a) * bf_lo(n4[j]), bf_hi(a) * bf_hi(n4[j]));
-            y[i][2 * j] = bf_lo(b);
-            y[i][2 * j + 1] = bf_hi(b);
-            mx = fmaxf(mx, fmaxf(fabsf(y[i][2 * j]), fabsf(y[i][2 * j + 1])));
-        }
-    }
-    mx = wave_max(mx);
-    if (lane == 0) red[8 + wave] = mx;
-    __syncthreads();
-    mx = fmaxf(fmaxf(red[8], red[9]), fmaxf(red[10], red[11]));
-    return act_scale_f(mx);
-}
-
 // codes of the NT-thread pieces into the tile layout, write-through (the in-launch hand-off)
 template <int PPT, int NT>
 __device__ __forceinline__ int quant_row_tiled_wt(const float (&y)[PPT][8], float sf, int npad, int8_t* base, int row,
@@ -1772,6 +1755,178 @@ __global__ __launch_bounds__(256) void k_lm_head(const uint16_t* __restrict__ E,
     WF_STAMP(4);
 }
 
+// Batch < 16 LM head as one persistent stream with the final norm in its prologue (replaces a
+// k_rownorm launch + 8016 one-shot k_lm_head blocks): grid = a few blocks per CU, block g takes the
+// 32-row vocabulary tiles g, g + G, ...; every block first puts its first weight chunks in flight,
+// then normalises the MB final hidden rows itself (norm_row at 512 threads: k_rownorm's tree, so hn
+// and the logits are bit-identical to the two-launch form) into LDS, then streams its tiles with
+// the next round's chunks in flight while the current ones are summed (each lane the same chunk
+// order as k_lm_head: same fp32 sums). Logits bf16 per row; each lane-row keeps its running
+// (max, first index); one (max, index) record per block and row, one ticket arrival per block, the
+// last block reduces the G records (first index on ties) into the greedy token and advances the
+// position.
+template <int MB, int PPT>
+__global__ __launch_bounds__(kNT) void k_lm_head_p(const uint16_t* __restrict__ E, const uint16_t* __restrict__ h,
+                                                   const uint16_t* __restrict__ fnw, float eps, int H, int V, int B,
+                                                   uint16_t* __restrict__ logits, uint2* __restrict__ part,
+                                                   unsigned* ticket, int32_t* tokens, int32_t* positions, int max_seq,
+                                                   uint16_t* __restrict__ hn_out) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t sh[];  // [MB][H] normalised rows
+    __shared__ float red[2 * kNT / 64];
+    __shared__ float s_val[MB][32];
+    __shared__ int s_idx[MB][32];
+    __shared__ int sh_flag;
+    __shared__ float r_val[kNT];
+    __shared__ int r_idx[kNT];
+    const int b0 = blockIdx.y * MB, G = gridDim.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sub = lane & 15;
+    const int lrow = wave * 4 + (lane >> 4);  // 0..31
+    const int C = H / 8;                      // 16-byte chunks per row
+    constexpr int U = kLmU;
+    const int R = (C + 16 * U - 1) / (16 * U);  // rounds per tile
+    const int ntiles = (V + 31) / 32;
+    WF_STAMP_BASE(4096u);
+    WF_STAMP(0);
+    auto load = [&](uint4 (&w)[U], int t, int r) {
+        const uint16_t* er = E + (int64_t)min(32 * t + lrow, V - 1) * H;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = 16 * (U * r + u) + sub;
+            w[u] = ldg_nt(reinterpret_cast<const uint8_t*>(er + 8 * min(c, C - 1)));
+        }
+    };
+    uint4 wa[U], wb[U];
+    int t = blockIdx.x, r = 0;
+    if (t < ntiles) load(wa, t, 0);
+    // the final norm of this block's MB rows (scripts/direct_inference_full.py:296-297)
+#pragma unroll 1
+    for (int m = 0; m < MB; ++m) {
+        NormRow<PPT, kNT> nr;
+        nr.issue(h + (int64_t)(b0 + m) * H, fnw, H);
+        nr.fence(true, true);
+        float y[PPT][8];
+        (void)norm_row(nr, H, eps, y, red, false);
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) {
+            const int p = threadIdx.x + kNT * i;
+            if (p < C) {
+                const uint4 v = make_uint4(pk_bf16(y[i][0], y[i][1]), pk_bf16(y[i][2], y[i][3]), pk_bf16(y[i][4], y[i][5]),
+                                           pk_bf16(y[i][6], y[i][7]));
+                reinterpret_cast<uint4*>(sh + m * H)[p] = v;
+                if (blockIdx.x == 0) reinterpret_cast<uint4*>(hn_out + (int64_t)(b0 + m) * H)[p] = v;
+            }
+        }
+        __syncthreads();  // red reused by the next row
+    }
+    WF_STAMP(1);
+    float acc[MB], best[MB];
+    int bidx[MB];
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+        acc[m] = 0.f;
+        best[m] = -INFINITY;
+        bidx[m] = 0x7fffffff;
+    }
+    while (t < ntiles) {
+        int tn = t, rn = r + 1;
+        if (rn == R) {
+            rn = 0;
+            tn = t + G;
+        }
+        if (tn < ntiles) load(wb, tn, rn);  // the next round's chunks in flight while these are summed
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = 16 * (U * r + u) + sub;
+            if (c < C) {
+                const uint32_t wd[4] = {wa[u].x, wa[u].y, wa[u].z, wa[u].w};
+#pragma unroll
+                for (int m = 0; m < MB; ++m) {
+                    const uint4 hv = *reinterpret_cast<const uint4*>(sh + m * H + 8 * c);
+                    const uint32_t hd[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        acc[m] = fmaf(__uint_as_float(wd[q] << 16), __uint_as_float(hd[q] << 16), acc[m]);
+                        acc[m] = fmaf(__uint_as_float(wd[q] & 0xffff0000u), __uint_as_float(hd[q] & 0xffff0000u), acc[m]);
+                    }
+                }
+            }
+        }
+        if (r == R - 1) {  // tile done: logits of this lane-row, running max (rows increase: first index kept)
+            const int row = 32 * t + lrow;
+#pragma unroll
+            for (int m = 0; m < MB; ++m) {
+                const float v = group_reduce<16>(acc[m], OpAdd{});
+                acc[m] = 0.f;
+                if (sub == 0 && row < V) {
+                    const uint16_t lb = f2bf(v);
+                    logits[(int64_t)(b0 + m) * V + row] = lb;
+                    if (bf2f(lb) > best[m]) {
+                        best[m] = bf2f(lb);
+                        bidx[m] = row;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) wa[u] = wb[u];
+        t = tn;
+        r = rn;
+    }
+    WF_STAMP(2);
+    if (sub == 0) {
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+            s_val[m][lrow] = best[m];
+            s_idx[m][lrow] = bidx[m];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < MB) {
+        const int m = threadIdx.x;
+        float bv = s_val[m][0];
+        int bi = s_idx[m][0];
+        for (int i = 1; i < 32; ++i)
+            if (s_val[m][i] > bv || (s_val[m][i] == bv && s_idx[m][i] < bi)) { bv = s_val[m][i]; bi = s_idx[m][i]; }
+        const uint64_t pk = ((uint64_t)(uint32_t)bi << 32) | __float_as_uint(bv);
+        st_sc1(reinterpret_cast<uint64_t*>(part) + (int64_t)(b0 + m) * G + blockIdx.x, pk);
+    }
+    const bool last = ticket_arrive(ticket, gridDim.x * gridDim.y, linear_block_id(), &sh_flag);
+    WF_STAMP(3);
+    if (!last) return;
+    for (int b = 0; b < B; ++b) {
+        float bv = -INFINITY;
+        int bi = 0x7fffffff;
+        const uint64_t* pb = reinterpret_cast<const uint64_t*>(part) + (int64_t)b * G;
+        for (int i = threadIdx.x; i < G; i += kNT) {
+            const uint64_t v = ld_sc1(pb + i);
+            const float fv = __uint_as_float((uint32_t)v);
+            const int id = (int)(v >> 32);
+            if (fv > bv || (fv == bv && id < bi)) { bv = fv; bi = id; }
+        }
+        r_val[threadIdx.x] = bv;
+        r_idx[threadIdx.x] = bi;
+        __syncthreads();
+        for (int s2 = kNT / 2; s2 > 0; s2 >>= 1) {
+            if (threadIdx.x < s2) {
+                const float v2 = r_val[threadIdx.x + s2];
+                const int i2 = r_idx[threadIdx.x + s2];
+                if (v2 > r_val[threadIdx.x] || (v2 == r_val[threadIdx.x] && i2 < r_idx[threadIdx.x])) {
+                    r_val[threadIdx.x] = v2;
+                    r_idx[threadIdx.x] = i2;
+                }
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            tokens[b] = r_idx[0];
+            positions[b] = min(positions[b] + 1, max_seq - 1);
+        }
+        __syncthreads();
+    }
+    ticket_rearm(ticket);
+    WF_STAMP(4);
+}
+
 }  // namespace wf
 
 WF_STAMP_READER(wf_debug_stamps_decode)
@@ -1800,6 +1955,7 @@ struct wf_model {
     int* act_sum = nullptr;
     unsigned* tickets = nullptr;
     unsigned* seam = nullptr;  // fused row-norm hand-off words (k_dec_gemm_t PRO), zero between launches
+    unsigned* attn_cnt = nullptr;  // batched attention tail: one arrival counter per sequence (kTailLine apart)
     int fuse[4] = {0, 0, 0, 0};  // per GEMM op (QKV, O, GU, DN): row norm fused into the GEMM launch
     uint2* am_part = nullptr;
     int lm_blocks = 0;
@@ -1829,6 +1985,8 @@ constexpr int kLprQKV = kNT / 16;  // 240 blocks at 2B
 constexpr int kLprO = kNT / 16;    // 160 blocks
 constexpr int kLprGU = 8;          // 64 rows = four gate/up tiles per block: 216 blocks at I = 6912
 constexpr int kLprDN = kNT / 16;   // 160 blocks
+// batch < 16 LM head stream: blocks of kNT threads (two per CU at 256 CUs)
+constexpr int kLmStreamBlocks = 512;
 
 int64_t wrow_bytes(int fmt, int K) { return fmt == WF_FMT_TQ ? FmtTQ::row_bytes(K) : FmtI2S::row_bytes(K); }
 int k_pad(int fmt, int K) { return fmt == WF_FMT_TQ ? FmtTQ::k_pad(K) : FmtI2S::k_pad(K); }
@@ -2076,6 +2234,12 @@ int gemv_input(wf_model* m, GemvArgs& a, const uint16_t* x, int64_t xs, const ui
     return WF_OK;
 }
 
+// the batched attention forms the O input row in its tail (k_attn_mfma TAIL; its 256-thread norm
+// replays the 512-thread tree for rows of up to 4096)
+bool attn_tail_on(const wf_model* m) {
+    return m->d.batch >= 16 && m->kv_tiled && m->attn_cnt && m->d.n_heads * m->d.head_dim <= 4096 && !m->fuse[1];
+}
+
 // One op of the decode step (WF_OP_* in include/wf_bitnet.h).
 int run_op(wf_model* m, int l, int op, hipStream_t st) {
     const wf_model_desc& d = m->d;
@@ -2094,25 +2258,35 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             a.out = m->qbuf; a.out_stride = (int64_t)d.n_heads * D;
             if (m->fuse[0]) return fused_input(a, m->h_a, H, d.ln_in + (int64_t)l * H), launch_gemv_fmt<MODE_QKV, kLprQKV>(d.wfmt, a, st, 1);
             if ((rc = gemv_input(m, a, m->h_a, H, d.ln_in + (int64_t)l * H, st))) return rc;
+            if (B == 1 && l == 0) {  // the token's embedding row itself (no embed launch at batch 1)
+                a.x = d.embed; a.x_stride = H; a.x_tok = m->tokens; a.vocab = d.vocab; a.seq_out = m->seq_lens;
+            }
             return launch_gemv_fmt<MODE_QKV, kLprQKV>(d.wfmt, a, st);
-        case WF_OP_ATTN:  // split partials; merged by the O projection's input stage
+        case WF_OP_ATTN: {  // split partials; merged by the O projection's input stage or the tail
+            // batch >= 16 on tile-layout caches: the attention's last block per sequence forms the O
+            // input row (AttnTail) instead of a k_rownorm_attn launch
+            AttnTail tail{d.attn_sub + (int64_t)l * H, d.eps, m->q8, m->act_sf, m->act_sum, m->attn_cnt};
+            const AttnTail* tp = attn_tail_on(m) ? &tail : nullptr;
             if (a.pt)  // paged pool: kv head stride 32 * D inside a page
                 return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, 0, 32 * D, B, d.n_heads,
                                                  d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D), m->part_ml,
                                                  m->part_o, st, true, a.pt, a.pps, a.npages, a.kv_pgs, d.kv_quant,
-                                                 m->kv_scale[2 * l], m->kv_scale[2 * l + 1]);
+                                                 m->kv_scale[2 * l], m->kv_scale[2 * l + 1], tp);
             return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, a.kv_b_stride, (int64_t)S * D,
                                              B, d.n_heads, d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D),
                                              m->part_ml, m->part_o, st, m->kv_tiled != 0, nullptr, 0, 0, 0, d.kv_quant,
-                                             d.kv_quant ? m->kv_scale[2 * l] : 1.f, d.kv_quant ? m->kv_scale[2 * l + 1] : 1.f);
+                                             d.kv_quant ? m->kv_scale[2 * l] : 1.f, d.kv_quant ? m->kv_scale[2 * l + 1] : 1.f,
+                                             tp);
+        }
         case WF_OP_O:  // h_b = h_a + o_proj(rms_norm(attn_sub_norm)(attn))
             a.w = d.w_o + (int64_t)l * H * wrow_bytes(d.wfmt, H); a.N = H; a.K = H; a.ws0 = wsh[3];
             a.resid = m->h_a; a.out = m->h_b; a.out_stride = H;
+            if (B == 1 && l == 0) { a.resid = d.embed; a.x_tok = m->tokens; a.vocab = d.vocab; }
             a.nw = d.attn_sub + (int64_t)l * H;
             a.part_ml = m->part_ml;
             a.part_o = m->part_o;
             if (m->fuse[1]) return launch_gemv_fmt<MODE_O, kLprO>(d.wfmt, a, st, 2);
-            if (B > 1) {
+            if (B > 1 && !attn_tail_on(m)) {
 // the records of decode_attention_partials: kAttnPartSplits1 per head below batch 16, else kAttnPartSplits
 #define WF_RA(PPTV, TL, NS)                                                                                                 \
     hipLaunchKernelGGL((k_rownorm_attn<PPTV, TL, NS>), dim3(B), dim3(kNT), 0, st, m->part_ml, m->part_o, d.n_heads, a.nw, \
@@ -2142,9 +2316,9 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             if ((rc = gemv_input(m, a, m->act, I, d.ffn_sub + (int64_t)l * I, st))) return rc;
             return launch_gemv_fmt<MODE_DN, kLprDN>(d.wfmt, a, st);
         case WF_OP_LM_HEAD: {  // final norm -> hn, logits = hn @ embed^T, greedy token
-            launch_rownorm(m, m->h_a, H, d.final_norm, H, m->hn, st);
-            if ((rc = check_launch("final_norm"))) return rc;
             if (m->embed_t) {
+                launch_rownorm(m, m->h_a, H, d.final_norm, H, m->hn, st);
+                if ((rc = check_launch("final_norm"))) return rc;
                 const int nb = (d.vocab + 255) / 256;
                 hipLaunchKernelGGL(k_lm_head_mfma, dim3(nb, (B + 127) / 128), dim3(256), 0, st, m->embed_t, m->hn, H, d.vocab,
                                    B, m->logits, m->am_part, nb);
@@ -2152,13 +2326,20 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
                 break;
             }
             const size_t sh = (size_t)H * 2;
-#define WF_LM(MBV)                                                                                              \
-    hipLaunchKernelGGL((k_lm_head<MBV>), dim3(m->lm_blocks, B / MBV), dim3(256), sh * MBV, st, d.embed, m->hn, \
-                       H, d.vocab, B, m->logits, m->am_part, m->lm_blocks, m->tickets + TK_LM * kTicketWords, m->tokens,      \
-                       m->positions, S)
-            if (B % 4 == 0) WF_LM(4);
-            else if (B % 2 == 0) WF_LM(2);
-            else WF_LM(1);
+            const int G = std::min((d.vocab + 31) / 32, kLmStreamBlocks);
+#define WF_LM(MBV, PPTV)                                                                                            \
+    hipLaunchKernelGGL((k_lm_head_p<MBV, PPTV>), dim3(G, B / MBV), dim3(kNT), sh * MBV, st, d.embed, m->h_a,          \
+                       d.final_norm, d.eps, H, d.vocab, B, m->logits, m->am_part, m->tickets + TK_LM * kTicketWords,  \
+                       m->tokens, m->positions, S, m->hn)
+            if (norm_ppt(H) == 1) {
+                if (B % 4 == 0) WF_LM(4, 1);
+                else if (B % 2 == 0) WF_LM(2, 1);
+                else WF_LM(1, 1);
+            } else {
+                if (B % 4 == 0) WF_LM(4, 2);
+                else if (B % 2 == 0) WF_LM(2, 2);
+                else WF_LM(1, 2);
+            }
 #undef WF_LM
             break;
         }
@@ -2170,7 +2351,8 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
 }
 
 int model_step(wf_model* m, hipStream_t st) {
-    int rc = run_op(m, 0, WF_OP_EMBED, st);
+    // batch 1: layer 0's QKV / O read the token's embedding row themselves (GemvArgs::x_tok)
+    int rc = m->d.batch == 1 ? WF_OK : run_op(m, 0, WF_OP_EMBED, st);
     for (int l = 0; l < m->d.layers && !rc; ++l)
         for (int op = WF_OP_QKV; op <= WF_OP_DOWN && !rc; ++op) rc = run_op(m, l, op, st);
     if (!rc) rc = run_op(m, 0, WF_OP_LM_HEAD, st);
@@ -2273,11 +2455,13 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_ALLOC(m->act_sum, sizeof(int) * B);
     WF_ALLOC(m->tickets, sizeof(unsigned) * kTicketWords * TK_COUNT);
     WF_ALLOC(m->seam, sizeof(unsigned) * 2 * kSeamTiles * kSeamLine);
+    WF_ALLOC(m->attn_cnt, sizeof(unsigned) * (size_t)B * kTailLine);
     WF_ALLOC(m->am_part, sizeof(uint2) * B * m->lm_blocks);
 #undef WF_ALLOC
     // tickets start at zero; every launch re-arms the ones it uses
     if ((e = hipMemset(m->tickets, 0, sizeof(unsigned) * kTicketWords * TK_COUNT)) != hipSuccess) return fail(e);
     if ((e = hipMemset(m->seam, 0, sizeof(unsigned) * 2 * kSeamTiles * kSeamLine)) != hipSuccess) return fail(e);
+    if ((e = hipMemset(m->attn_cnt, 0, sizeof(unsigned) * (size_t)B * kTailLine)) != hipSuccess) return fail(e);
     fused_norm_plan(m);
     if ((e = hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking)) != hipSuccess) return fail(e);
     *out = m;
@@ -2289,7 +2473,7 @@ int wf_model_destroy(wf_model* m) {
     if (m->exec) (void)hipGraphExecDestroy(m->exec);
     if (m->graph) (void)hipGraphDestroy(m->graph);
     if (m->cap) (void)hipStreamDestroy(m->cap);
-    void* ptrs[] = {m->seq_lens, m->h_a, m->h_b, m->qbuf, m->part_ml, m->part_o, m->hn, m->act, m->q8, m->dec_ws,
+    void* ptrs[] = {m->attn_cnt, m->seq_lens, m->h_a, m->h_b, m->qbuf, m->part_ml, m->part_o, m->hn, m->act, m->q8, m->dec_ws,
                     m->act_sf, m->act_sum, m->tickets, m->seam, m->am_part, m->embed_t, m->pf_h_a, m->pf_h_b, m->pf_q,
                     m->pf_attn, m->pf_act, m->pf_q8, m->pf_sf, m->pf_asum, m->pf_seq};
     for (void* p : ptrs)

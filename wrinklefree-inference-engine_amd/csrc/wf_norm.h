@@ -275,6 +275,49 @@ __device__ __forceinline__ float norm_row(const NormRow<PPT, NT>& r, int K, floa
     return norm_core<PPT, NT, wf_stamp_base>(r, K, eps, y, red, want_scale);
 }
 
+// 256 threads replaying the 512-thread norm_core (the batch-1 / k_rownorm reduction tree, so the
+// codes are bit-identical): thread t holds pieces t + 256 i (NormRow<PPT2, 256> / AttnRow<PPT2, 256>).
+template <int PPT2>
+__device__ __forceinline__ float norm_core_e512(const NormRow<PPT2, 256>& r, int K, float eps, float (&y)[PPT2][8],
+                                                float* red) {
+    // 256 threads replaying the 512-thread norm_core: virtual thread t + 256 j owns pieces 2 i + j
+    static_assert(PPT2 % 2 == 0, "two virtual threads per lane");
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float ss[2] = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < PPT2 / 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ss[j] = fmaf(y[2 * i + j][e], y[2 * i + j][e], ss[j]);
+    ss[0] = wave_sum(ss[0]);
+    ss[1] = wave_sum(ss[1]);
+    if (lane == 0) {
+        red[wave] = ss[0];
+        red[wave + 4] = ss[1];
+    }
+    __syncthreads();
+    const float rr = rms_factor(div_rn(tree_sum<8>(red), (float)K, 1.0f / (float)K) + eps);
+    float mx = 0.f;
+#pragma unroll
+    for (int i = 0; i < PPT2; ++i) {
+        const uint32_t n4[4] = {r.w[i].x, r.w[i].y, r.w[i].z, r.w[i].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t a = pk_bf16(y[i][2 * j] * rr, y[i][2 * j + 1] * rr);
+            const uint32_t b = pk_bf16(bf_lo(a) * bf_lo(n4[j]), bf_hi(a) * bf_hi(n4[j]));
+            y[i][2 * j] = bf_lo(b);
+            y[i][2 * j + 1] = bf_hi(b);
+            mx = fmaxf(mx, fmaxf(fabsf(y[i][2 * j]), fabsf(y[i][2 * j + 1])));
+        }
+    }
+    mx = wave_max(mx);
+    if (lane == 0) red[8 + wave] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(red[8], red[9]), fmaxf(red[10], red[11]));
+    return act_scale_f(mx);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Attention row of sequence b from the decode-step attention partials (wf_attn.hip k_attn_part:
 // kAttnPartSplits records per (b, head): ml = (m, l), o unnormalised). Piece p (outputs
@@ -381,21 +424,34 @@ template <int PPT, int NT, int NS = kAttnPartSplits, class PC = PieceNT<NT>>
 struct AttnRow {
     float4 ml[PPT][NS / 2];  // (m0, l0, m1, l1) pairs
     float4 oa[PPT][NS], ob[PPT][NS];
+    // SC1: the records were published in this launch (the attention's tail hand-off, write-through
+    // stores + ticket): L1-bypassing 16-byte buffer loads (MI355X_MICROARCH.md Valid forms row 1)
+    template <bool SC1 = false>
     __device__ __forceinline__ void issue(const float2* __restrict__ ml_in, const float* __restrict__ o_in, int b, int Hq,
                                           int D) {
         const int npk = Hq * D / 8;
         const PC piece;
+        const __amdgpu_buffer_rsrc_t rml = make_rsrc(ml_in), ro = make_rsrc(o_in);
 #pragma unroll
         for (int i = 0; i < PPT; ++i) {
             const int pc = min(piece(i), npk - 1);
             const int h = (8 * pc) / D, d0 = 8 * pc - h * D;
             const int64_t rec = (int64_t)(b * Hq + h) * NS;
 #pragma unroll
-            for (int u = 0; u < NS / 2; ++u) ml[i][u] = reinterpret_cast<const float4*>(ml_in + rec)[u];
+            for (int u = 0; u < NS / 2; ++u) {
+                if constexpr (SC1) ml[i][u] = __builtin_bit_cast(float4, ld16_sc1(rml, (int)(8 * rec + 16 * u)));
+                else ml[i][u] = reinterpret_cast<const float4*>(ml_in + rec)[u];
+            }
 #pragma unroll
             for (int u = 0; u < NS; ++u) {
-                oa[i][u] = *reinterpret_cast<const float4*>(o_in + part_o_off<NS>(b * Hq + h, u, d0));
-                ob[i][u] = *reinterpret_cast<const float4*>(o_in + part_o_off<NS>(b * Hq + h, u, d0 + 4));
+                const int64_t ea = part_o_off<NS>(b * Hq + h, u, d0), eb = part_o_off<NS>(b * Hq + h, u, d0 + 4);
+                if constexpr (SC1) {
+                    oa[i][u] = __builtin_bit_cast(float4, ld16_sc1(ro, (int)(4 * ea)));
+                    ob[i][u] = __builtin_bit_cast(float4, ld16_sc1(ro, (int)(4 * eb)));
+                } else {
+                    oa[i][u] = *reinterpret_cast<const float4*>(o_in + ea);
+                    ob[i][u] = *reinterpret_cast<const float4*>(o_in + eb);
+                }
             }
         }
     }
@@ -442,6 +498,19 @@ struct AttnRow {
         }
     }
 };
+
+// The batched decode attention's tail (k_attn_mfma TAIL): the last of a sequence's blocks to finish
+// merges its Hq heads' records into the O projection's input row -- attn_sub_norm rms_norm + int8
+// codes in the tile layout, scale and code sum -- in place of a k_rownorm_attn launch.
+struct AttnTail {
+    const uint16_t* nw;  // attn_sub_norm weight of the layer [Hq * 128]
+    float eps;
+    int8_t* q8;          // codes, tile layout (tile_code_pos)
+    float* sf;           // [B]
+    int* asum;           // [B]
+    unsigned* cnt;       // one arrival counter per sequence, kTailLine words apart, zero between launches
+};
+constexpr int kTailLine = 32;  // one 128-byte line per counter
 
 // Batch-1 GEMV prologue (k_gemv PPT > 0: NormRow + norm_core + quant_row) is VALU-issue /
 // dependency-latency bound, not memory-bound (in-graph stamps, tools/stamps_graph.py). Measured
