@@ -11,7 +11,8 @@ if [ -n "${TESTS:-}" ]; then
   rc=$?; tail -4 "$O/pytest.log"; [ $rc -eq 0 ] || exit $rc
 fi
 L=$(pwd)/wrinklefree-inference-engine_amd/lib
-for args in "${BENCH1:---steps 200 --warmup 20}" "${BENCH2:---batch 128 --steps 50 --warmup 5}"; do
+IFS=';' read -ra BENCHES <<< "${BENCHES:---steps 200 --warmup 20;--batch 128 --steps 50 --warmup 5}"
+for args in "${BENCHES[@]}"; do
   for rep in 1 2; do
     for lib in ${LIBS:-libwfbitnet.so}; do
       WF_BITNET_LIB=$L/$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-gemv $args > "$O/last.log" 2>&1 || { tail -20 "$O/last.log"; exit 1; }

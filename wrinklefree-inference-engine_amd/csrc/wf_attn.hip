@@ -344,7 +344,8 @@ template <int G, int NS, int U>
 __device__ __forceinline__ void attn_part_body(const uint16_t* __restrict__ q, int64_t q_sb, const uint16_t* __restrict__ K,
                                                const uint16_t* __restrict__ V, int64_t kv_sb, int64_t kv_sh, int Hq,
                                                int Hkv, int S, const int32_t* __restrict__ seq_lens, float sm_scale,
-                                               float2* __restrict__ ml_out, float* __restrict__ o_out) {
+                                               float2* __restrict__ ml_out, float* __restrict__ o_out,
+                                               uint16_t* __restrict__ row_out, unsigned* __restrict__ cnt) {
     constexpr int D = 128, LP = D / 8, NG = kAttnPartThreads / LP, CH = U * NG;
     // block (s, y, b): query heads hq0 .. hq0 + G - 1 (G = whole GQA group, or 1: one block per query
     // head, 4x the blocks for a group of 4 -- the K/V re-reads hit the caches)
@@ -500,11 +501,58 @@ __device__ __forceinline__ void attn_part_body(const uint16_t* __restrict__ q, i
             os[0] += ov.x * a; os[1] += ov.y * a; os[2] += ov.z * a; os[3] += ov.w * a;
         }
         const int64_t rec = (int64_t)(b * Hq + hq0 + h) * NS + s;
-        *reinterpret_cast<float4*>(o_out + part_o_off<NS>(rec / NS, (int)(rec % NS), d)) =
-            make_float4(os[0], os[1], os[2], os[3]);
-        if (d == 0) ml_out[rec] = make_float2(mx, ls);
+        const int64_t oe = part_o_off<NS>(rec / NS, (int)(rec % NS), d);
+        if (row_out) {  // write-through: the head's last block merges them in this launch
+            st16_sc1(make_rsrc(o_out), (int)(4 * oe), __builtin_bit_cast(uint4, make_float4(os[0], os[1], os[2], os[3])));
+            if (d == 0) st_sc1(reinterpret_cast<uint64_t*>(ml_out) + rec, __builtin_bit_cast(uint64_t, make_float2(mx, ls)));
+        } else {
+            *reinterpret_cast<float4*>(o_out + oe) = make_float4(os[0], os[1], os[2], os[3]);
+            if (d == 0) ml_out[rec] = make_float2(mx, ls);
+        }
     }
     WF_STAMP(2);
+    if (G == 1 && row_out) {
+        // batch < 16: the head's last block merges its NS records into the bf16
+        // attention row (AttnRow::finish's arithmetic) so the O projection reads 256 B per head
+        // instead of every record: ticket per (sequence, head) (MI355X_MICROARCH.md Valid forms row 1)
+        __shared__ int sh_last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned* c = cnt + (int64_t)(b * Hq + hq0) * 32;
+            const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sh_last = (old == (unsigned)NS - 1u);
+            if (old == (unsigned)NS - 1u) st_sc1(c, 0u);
+        }
+        __syncthreads();
+        if (!sh_last || threadIdx.x >= D / 4) return;
+        const int d = 4 * threadIdx.x;
+        const int64_t bh = (int64_t)b * Hq + hq0;
+        const __amdgpu_buffer_rsrc_t rml = make_rsrc(ml_out), ro = make_rsrc(o_out);
+        float mm[NS], ll[NS];
+        float4 ov[NS];
+#pragma unroll
+        for (int u = 0; u < NS / 2; ++u) {
+            const float4 v = __builtin_bit_cast(float4, ld16_sc1(rml, (int)(8 * (bh * NS) + 16 * u)));
+            mm[2 * u] = v.x; ll[2 * u] = v.y; mm[2 * u + 1] = v.z; ll[2 * u + 1] = v.w;
+        }
+#pragma unroll
+        for (int u = 0; u < NS; ++u) ov[u] = __builtin_bit_cast(float4, ld16_sc1(ro, (int)(4 * part_o_off<NS>(bh, u, d))));
+        float M = mm[0];
+#pragma unroll
+        for (int u = 1; u < NS; ++u) M = fmaxf(M, mm[u]);
+        float L = 0.f, O[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < NS; ++u) {
+            const float w = (mm[u] == -INFINITY) ? 0.f : __expf(mm[u] - M);
+            L = fmaf(w, ll[u], L);
+            O[0] = fmaf(w, ov[u].x, O[0]); O[1] = fmaf(w, ov[u].y, O[1]);
+            O[2] = fmaf(w, ov[u].z, O[2]); O[3] = fmaf(w, ov[u].w, O[3]);
+        }
+        const float inv = 1.0f / L;
+        *reinterpret_cast<uint2*>(row_out + bh * D + d) =
+            make_uint2(pk_bf16(rbf(O[0] * inv), rbf(O[1] * inv)), pk_bf16(rbf(O[2] * inv), rbf(O[3] * inv)));
+    }
 }
 
 template <int G, int NS>
@@ -513,16 +561,18 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
                                                                 const uint16_t* __restrict__ V, int64_t kv_sb,
                                                                 int64_t kv_sh, int Hq, int Hkv, int S,
                                                                 const int32_t* __restrict__ seq_lens, float sm_scale,
-                                                                float2* __restrict__ ml_out, float* __restrict__ o_out) {
+                                                                float2* __restrict__ ml_out, float* __restrict__ o_out,
+                                                                uint16_t* __restrict__ row_out, unsigned* __restrict__ cnt) {
     constexpr int NG = kAttnPartThreads / 16;
     const int Sb = min(seq_lens[blockIdx.z], S);
     const int T = ((Sb + NS - 1) / NS + 15) / 16 * 16;  // the body's split length
     // (the batched untiled fallback, G > 1, keeps one body: two would double its LDS)
     if (G == 1 && T <= kApUShort * NG)  // block-uniform
         attn_part_body<G, NS, G == 1 ? kApUShort : kApULong>(q, q_sb, K, V, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale,
-                                                             ml_out, o_out);
+                                                             ml_out, o_out, row_out, cnt);
     else
-        attn_part_body<G, NS, kApULong>(q, q_sb, K, V, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, ml_out, o_out);
+        attn_part_body<G, NS, kApULong>(q, q_sb, K, V, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, ml_out, o_out,
+                                        row_out, cnt);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1311,7 +1361,8 @@ int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const 
 int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
                               float2* ml, float* o, hipStream_t st, bool kv_tiled, const int32_t* pt, int pps,
-                              int npages, int64_t kv_pgs, int kv8, float k_scale, float v_scale, const AttnTail* tail) {
+                              int npages, int64_t kv_pgs, int kv8, float k_scale, float v_scale, const AttnTail* tail,
+                              uint16_t* merged_row, unsigned* merge_cnt) {
     const int grp = Hq / Hkv;
     if (grp > 8) {
         set_error("decode_attention_partials: GQA group %d > 8", grp);
@@ -1322,7 +1373,7 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
         // of the per-lane arithmetic (at batch 1 the kernel is latency-bound on its score/softmax
         // chain; the K/V re-reads of the group's heads hit L2)
         hipLaunchKernelGGL((k_attn_part<1, kAttnPartSplits1>), dim3(kAttnPartSplits1, Hq, B), dim3(kAttnPartThreads), 0, st, q, q_sb, k, v,
-                           kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, ml, o);
+                           kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, ml, o, merged_row, merge_cnt);
         return check_launch("decode_attention_partials");
     }
     // batched: one block per kv head, the group's query heads share every K/V load (KV-bound)
@@ -1357,7 +1408,7 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
     // kv head, with the batched record count (the reader, k_rownorm_attn, merges kAttnPartSplits)
 #define WF_AP(GV)                                                                                                   \
     hipLaunchKernelGGL((k_attn_part<GV, kAttnPartSplits>), grid, dim3(kAttnPartThreads), 0, st, q, q_sb, k, v, kv_sb,  \
-                       kv_sh, Hq, Hkv, S, seq_lens, sm_scale, ml, o)
+                       kv_sh, Hq, Hkv, S, seq_lens, sm_scale, ml, o, nullptr, nullptr)
     if (grp == 1) WF_AP(1);
     else if (grp == 2) WF_AP(2);
     else if (grp <= 4) WF_AP(4);

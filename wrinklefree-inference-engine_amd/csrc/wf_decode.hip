@@ -37,7 +37,35 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
                               float2* ml, float* o, hipStream_t st, bool kv_tiled, const int32_t* pt = nullptr,
                               int pps = 0, int npages = 0, int64_t kv_pgs = 0, int kv8 = 0, float k_scale = 1.f,
-                              float v_scale = 1.f, const AttnTail* tail = nullptr);
+                              float v_scale = 1.f, const AttnTail* tail = nullptr, uint16_t* merged_row = nullptr,
+                              unsigned* merge_cnt = nullptr);
+
+// study switches (same-box A/B builds, tools/build_var.sh; measured r04, profiles/ab_r04.txt):
+// WF_NO_XTOK restores the batch-1 embed launch (-0.5 %); WF_OLD_EPI the LDS-round O/DN epilogue
+// (+-0.1 %); WF_ATTN_TAIL has the batched attention form the O input row in its per-sequence tail
+// (batch 128 -2.2 %: attention +7.5 us, k_rownorm_attn -4.5 us per layer); WF_NO_MERGE1 has the O
+// projection merge the batch < 16 attention records itself instead of reading the bf16 row each
+// head's last attention block merges (-1.7 % batch 1: O 4.35 -> 6.01 us, attention 5.86 -> 4.55 us)
+#ifdef WF_NO_XTOK
+constexpr bool kXTok = false;
+#else
+constexpr bool kXTok = true;
+#endif
+#ifdef WF_OLD_EPI
+constexpr bool kPermEpi = false;
+#else
+constexpr bool kPermEpi = true;
+#endif
+#ifdef WF_ATTN_TAIL
+constexpr bool kAttnTail = true;
+#else
+constexpr bool kAttnTail = false;
+#endif
+#ifdef WF_NO_MERGE1
+constexpr bool kMerge1 = false;
+#else
+constexpr bool kMerge1 = true;
+#endif
 
 enum { MODE_QKV = 0, MODE_O = 1, MODE_GU = 2, MODE_DN = 3, MODE_LINEAR = 4 };  // LINEAR: BitNetLinear drop-in
 constexpr int kNT = 512;  // threads per GEMV / row-norm block (8 waves: 2 per SIMD hide the input-stage latency)
@@ -172,7 +200,7 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
     // 1) the input row (issued first: vmcnt retires in order), 2) the weight stream, 3) residual
     constexpr int kNormPPT = PPT == 0 ? 1 : PPT;
     NormRow<kNormPPT, kNT> nr;
-    constexpr bool kAttnIn = (MODE == MODE_O && PPT > 0);
+    constexpr bool kAttnIn = (MODE == MODE_O && PPT > 0 && !kMerge1);
     AttnRow<kAttnIn ? PPT : 1, kNT, kAttnPartSplits1> ar;  // batch < 16: the k_attn_part records
     constexpr int kMaxPiecesPerThread = 8192 / 16 / kNT;  // staged int8: K_pad <= 8192
     uint4 apre[MB][kMaxPiecesPerThread];
@@ -183,7 +211,7 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
     } else if constexpr (PPT > 0 && MODE == MODE_LINEAR) {
         nr.issue_x(a.x + (int64_t)b0 * a.x_stride, K);
     } else if constexpr (PPT > 0) {
-        const int xrow = a.x_tok ? min(max(a.x_tok[b0], 0), a.vocab - 1) : b0;  // scalar load
+        const int xrow = (MODE == MODE_QKV && a.x_tok) ? min(max(a.x_tok[b0], 0), a.vocab - 1) : b0;  // scalar load
         nr.issue(a.x + (int64_t)xrow * a.x_stride, a.nw, K);
     } else {
 #pragma unroll
@@ -358,7 +386,7 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
                 g.out[(int64_t)(b0 + m) * g.ld + g.col] = f2bf(s_out[m][i]);
             }
         }
-    } else if constexpr ((MODE == MODE_O || MODE == MODE_DN) && MB == 1 && LPR == 32) {
+    } else if constexpr (kPermEpi && (MODE == MODE_O || MODE == MODE_DN) && MB == 1 && LPR == 32) {
         // O/DN at batch 1: a wave holds rows 2w (lanes 0-31) and 2w + 1 (lanes 32-63), every lane of a
         // row has its sum; lane 0 takes its partner's value by v_permlane32_swap and stores the pair
         // as one 4-byte word -- no LDS round and no block barrier before the store
@@ -1956,6 +1984,7 @@ struct wf_model {
     unsigned* tickets = nullptr;
     unsigned* seam = nullptr;  // fused row-norm hand-off words (k_dec_gemm_t PRO), zero between launches
     unsigned* attn_cnt = nullptr;  // batched attention tail: one arrival counter per sequence (kTailLine apart)
+    uint16_t* attn_row = nullptr;  // batch < 16: the merged bf16 attention rows [B][H] (kMerge1)
     int fuse[4] = {0, 0, 0, 0};  // per GEMM op (QKV, O, GU, DN): row norm fused into the GEMM launch
     uint2* am_part = nullptr;
     int lm_blocks = 0;
@@ -1986,7 +2015,10 @@ constexpr int kLprO = kNT / 16;    // 160 blocks
 constexpr int kLprGU = 8;          // 64 rows = four gate/up tiles per block: 216 blocks at I = 6912
 constexpr int kLprDN = kNT / 16;   // 160 blocks
 // batch < 16 LM head stream: blocks of kNT threads (two per CU at 256 CUs)
-constexpr int kLmStreamBlocks = 512;
+#ifndef WF_LM_BLOCKS  // study builds: blocks of the batch < 16 LM head stream
+#define WF_LM_BLOCKS 512
+#endif
+constexpr int kLmStreamBlocks = WF_LM_BLOCKS;
 
 int64_t wrow_bytes(int fmt, int K) { return fmt == WF_FMT_TQ ? FmtTQ::row_bytes(K) : FmtI2S::row_bytes(K); }
 int k_pad(int fmt, int K) { return fmt == WF_FMT_TQ ? FmtTQ::k_pad(K) : FmtI2S::k_pad(K); }
@@ -2237,7 +2269,7 @@ int gemv_input(wf_model* m, GemvArgs& a, const uint16_t* x, int64_t xs, const ui
 // the batched attention forms the O input row in its tail (k_attn_mfma TAIL; its 256-thread norm
 // replays the 512-thread tree for rows of up to 4096)
 bool attn_tail_on(const wf_model* m) {
-    return m->d.batch >= 16 && m->kv_tiled && m->attn_cnt && m->d.n_heads * m->d.head_dim <= 4096 && !m->fuse[1];
+    return kAttnTail && m->d.batch >= 16 && m->kv_tiled && m->attn_cnt && m->d.n_heads * m->d.head_dim <= 4096 && !m->fuse[1];
 }
 
 // One op of the decode step (WF_OP_* in include/wf_bitnet.h).
@@ -2258,7 +2290,7 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             a.out = m->qbuf; a.out_stride = (int64_t)d.n_heads * D;
             if (m->fuse[0]) return fused_input(a, m->h_a, H, d.ln_in + (int64_t)l * H), launch_gemv_fmt<MODE_QKV, kLprQKV>(d.wfmt, a, st, 1);
             if ((rc = gemv_input(m, a, m->h_a, H, d.ln_in + (int64_t)l * H, st))) return rc;
-            if (B == 1 && l == 0) {  // the token's embedding row itself (no embed launch at batch 1)
+            if (kXTok && B == 1 && l == 0) {  // the token's embedding row itself (no embed launch at batch 1)
                 a.x = d.embed; a.x_stride = H; a.x_tok = m->tokens; a.vocab = d.vocab; a.seq_out = m->seq_lens;
             }
             return launch_gemv_fmt<MODE_QKV, kLprQKV>(d.wfmt, a, st);
@@ -2267,21 +2299,24 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             // input row (AttnTail) instead of a k_rownorm_attn launch
             AttnTail tail{d.attn_sub + (int64_t)l * H, d.eps, m->q8, m->act_sf, m->act_sum, m->attn_cnt};
             const AttnTail* tp = attn_tail_on(m) ? &tail : nullptr;
+            uint16_t* mrow = (kMerge1 && B < 16) ? m->attn_row : nullptr;
+            unsigned* mcnt = mrow ? m->attn_cnt : nullptr;
             if (a.pt)  // paged pool: kv head stride 32 * D inside a page
                 return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, 0, 32 * D, B, d.n_heads,
                                                  d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D), m->part_ml,
                                                  m->part_o, st, true, a.pt, a.pps, a.npages, a.kv_pgs, d.kv_quant,
-                                                 m->kv_scale[2 * l], m->kv_scale[2 * l + 1], tp);
+                                                 m->kv_scale[2 * l], m->kv_scale[2 * l + 1], tp, mrow, mcnt);
             return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, a.kv_b_stride, (int64_t)S * D,
                                              B, d.n_heads, d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D),
                                              m->part_ml, m->part_o, st, m->kv_tiled != 0, nullptr, 0, 0, 0, d.kv_quant,
                                              d.kv_quant ? m->kv_scale[2 * l] : 1.f, d.kv_quant ? m->kv_scale[2 * l + 1] : 1.f,
-                                             tp);
+                                             tp, mrow, mcnt);
         }
         case WF_OP_O:  // h_b = h_a + o_proj(rms_norm(attn_sub_norm)(attn))
             a.w = d.w_o + (int64_t)l * H * wrow_bytes(d.wfmt, H); a.N = H; a.K = H; a.ws0 = wsh[3];
             a.resid = m->h_a; a.out = m->h_b; a.out_stride = H;
-            if (B == 1 && l == 0) { a.resid = d.embed; a.x_tok = m->tokens; a.vocab = d.vocab; }
+            if (kXTok && B == 1 && l == 0) { a.resid = d.embed; a.x_tok = m->tokens; a.vocab = d.vocab; }
+            if (kMerge1 && B < 16) { a.x = m->attn_row; a.x_stride = H; }
             a.nw = d.attn_sub + (int64_t)l * H;
             a.part_ml = m->part_ml;
             a.part_o = m->part_o;
@@ -2326,7 +2361,10 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
                 break;
             }
             const size_t sh = (size_t)H * 2;
-            const int G = std::min((d.vocab + 31) / 32, kLmStreamBlocks);
+            // every block the same number of 32-row tiles (4008 tiles: 501 blocks x 8, not 512 blocks
+            // of 7 or 8 -- the 8-tile blocks set the launch's end)
+            const int ntl = (d.vocab + 31) / 32, per = (ntl + kLmStreamBlocks - 1) / kLmStreamBlocks;
+            const int G = (ntl + per - 1) / per;
 #define WF_LM(MBV, PPTV)                                                                                            \
     hipLaunchKernelGGL((k_lm_head_p<MBV, PPTV>), dim3(G, B / MBV), dim3(kNT), sh * MBV, st, d.embed, m->h_a,          \
                        d.final_norm, d.eps, H, d.vocab, B, m->logits, m->am_part, m->tickets + TK_LM * kTicketWords,  \
@@ -2352,7 +2390,7 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
 
 int model_step(wf_model* m, hipStream_t st) {
     // batch 1: layer 0's QKV / O read the token's embedding row themselves (GemvArgs::x_tok)
-    int rc = m->d.batch == 1 ? WF_OK : run_op(m, 0, WF_OP_EMBED, st);
+    int rc = (kXTok && m->d.batch == 1) ? WF_OK : run_op(m, 0, WF_OP_EMBED, st);
     for (int l = 0; l < m->d.layers && !rc; ++l)
         for (int op = WF_OP_QKV; op <= WF_OP_DOWN && !rc; ++op) rc = run_op(m, l, op, st);
     if (!rc) rc = run_op(m, 0, WF_OP_LM_HEAD, st);
@@ -2455,13 +2493,15 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_ALLOC(m->act_sum, sizeof(int) * B);
     WF_ALLOC(m->tickets, sizeof(unsigned) * kTicketWords * TK_COUNT);
     WF_ALLOC(m->seam, sizeof(unsigned) * 2 * kSeamTiles * kSeamLine);
-    WF_ALLOC(m->attn_cnt, sizeof(unsigned) * (size_t)B * kTailLine);
+    // arrival lines: one per sequence (batched tail) or per (sequence, head) (kMerge1)
+    WF_ALLOC(m->attn_cnt, sizeof(unsigned) * (size_t)B * d.n_heads * kTailLine);
+    if (kMerge1) WF_ALLOC(m->attn_row, 2 * (size_t)B * d.hidden);
     WF_ALLOC(m->am_part, sizeof(uint2) * B * m->lm_blocks);
 #undef WF_ALLOC
     // tickets start at zero; every launch re-arms the ones it uses
     if ((e = hipMemset(m->tickets, 0, sizeof(unsigned) * kTicketWords * TK_COUNT)) != hipSuccess) return fail(e);
     if ((e = hipMemset(m->seam, 0, sizeof(unsigned) * 2 * kSeamTiles * kSeamLine)) != hipSuccess) return fail(e);
-    if ((e = hipMemset(m->attn_cnt, 0, sizeof(unsigned) * (size_t)B * kTailLine)) != hipSuccess) return fail(e);
+    if ((e = hipMemset(m->attn_cnt, 0, sizeof(unsigned) * (size_t)B * d.n_heads * kTailLine)) != hipSuccess) return fail(e);
     fused_norm_plan(m);
     if ((e = hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking)) != hipSuccess) return fail(e);
     *out = m;
@@ -2473,7 +2513,7 @@ int wf_model_destroy(wf_model* m) {
     if (m->exec) (void)hipGraphExecDestroy(m->exec);
     if (m->graph) (void)hipGraphDestroy(m->graph);
     if (m->cap) (void)hipStreamDestroy(m->cap);
-    void* ptrs[] = {m->attn_cnt, m->seq_lens, m->h_a, m->h_b, m->qbuf, m->part_ml, m->part_o, m->hn, m->act, m->q8, m->dec_ws,
+    void* ptrs[] = {m->attn_cnt, m->attn_row, m->seq_lens, m->h_a, m->h_b, m->qbuf, m->part_ml, m->part_o, m->hn, m->act, m->q8, m->dec_ws,
                     m->act_sf, m->act_sum, m->tickets, m->seam, m->am_part, m->embed_t, m->pf_h_a, m->pf_h_b, m->pf_q,
                     m->pf_attn, m->pf_act, m->pf_q8, m->pf_sf, m->pf_asum, m->pf_seq};
     for (void* p : ptrs)
