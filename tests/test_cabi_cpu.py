@@ -66,6 +66,8 @@ def test_reference_surface_names():
     assert hasattr(torch.ops.sgl_kernel, "bitnet_gemv_cpu")
     assert hasattr(torch.ops.sgl_kernel, "bitnet_gemm_cpu")
     assert hasattr(torch.ops.sgl_kernel, "bitnet_quantize_activations_cpu")
+    assert hasattr(torch.ops.sgl_kernel, "bitnet_qkv_forward_cpu")
+    assert hasattr(torch.ops.sgl_kernel, "bitnet_mlp_forward_cpu")
 
 
 def test_torch_op_fake_impls():
@@ -80,6 +82,14 @@ def test_torch_op_fake_impls():
         assert torch.ops.sgl_kernel.bitnet_gemm_cpu(w, a2, 0.5).shape == (4, 640)
         q, s = torch.ops.sgl_kernel.bitnet_quantize_activations_cpu(torch.empty(3, 2560))
         assert q.dtype == torch.int8 and q.shape == (3, 2560)
+        x = torch.empty(2, 3, 2560, dtype=torch.bfloat16)
+        wqkv = torch.empty(3840, 640, dtype=torch.uint8)
+        yq, yk, yv = torch.ops.sgl_kernel.bitnet_qkv_forward_cpu(x, wqkv, 2560, 640, 640, 0.5, 0.5, 0.5)
+        assert (yq.shape, yk.shape, yv.shape) == ((2, 3, 2560), (2, 3, 640), (2, 3, 640)) and yq.dtype == torch.bfloat16
+        y = torch.ops.sgl_kernel.bitnet_mlp_forward_cpu(x, torch.empty(13824, 640, dtype=torch.uint8),
+                                                        torch.empty(2560, 1728, dtype=torch.uint8), 0.5, 0.5, 0.5,
+                                                        torch.empty(6912, dtype=torch.bfloat16))
+        assert y.shape == (2, 3, 2560) and y.dtype == torch.bfloat16
 
 
 def test_native_numpy_helpers_match_reference():

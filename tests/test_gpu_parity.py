@@ -494,6 +494,11 @@ def test_bitnet_linear_fused_vs_oracle(orc, m, k, rows, fmt):
         for r in ([0, m - 1] if m > 16 else range(m)):
             ref = orc.bitnet_linear_bf16(np.ascontiguousarray(xb[r, :k]), p, w)
             assert np.array_equal(got[r], ref), (s, r)
+    if len(rows) == 3:  # the torch.ops schema (sgl_kernel::bitnet_qkv_forward_cpu) runs the same launch
+        assert ops.register_torch_ops()
+        top = torch.ops.sgl_kernel.bitnet_qkv_forward_cpu(xt[:, :k].contiguous(), packed, *rows, *ws, fmt)
+        for s in range(3):
+            assert np.array_equal(bits(top[s]), bits(outs[s])), s
     with pytest.raises(ValueError):
         ops.bitnet_linear_fused(xt, packed, [rows[0] + 16] + list(rows[1:]), ws, fmt, in_features=k)
 
@@ -520,6 +525,10 @@ def test_bitnet_mlp_vs_oracle(orc, m, h, i, fmt):
     mlp = BitNetMLP(*layers, cu(fw.view(np.int16)).view(torch.bfloat16), eps=1e-5)
     xt = cu(xb.view(np.int16)).view(torch.bfloat16)
     got = bits(mlp(xt))
+    assert ops.register_torch_ops()  # sgl_kernel::bitnet_mlp_forward_cpu: the same launch
+    top = torch.ops.sgl_kernel.bitnet_mlp_forward_cpu(xt, mlp.packed_gate_up, mlp.packed_down, *ws, mlp.ffn_sub_norm,
+                                                      1e-5, fmt)
+    assert np.array_equal(bits(top), got)
     exact = 0
     for r in range(m):
         g = orc.bf16_to_f32(orc.bitnet_linear_bf16(xb[r], pg, ws[0]))

@@ -428,6 +428,13 @@ def register_torch_ops() -> bool:
         lib.define("bitnet_gemv_cpu(Tensor packed_weights, Tensor activations, float scale) -> Tensor")
         lib.define("bitnet_gemm_cpu(Tensor packed_weights, Tensor activations, float scale) -> Tensor")
         lib.define("bitnet_quantize_activations_cpu(Tensor activations) -> (Tensor, Tensor)")
+        # the fused ops the reference attempted (docs/research/sglang_optimization_plan.md:326-331;
+        # their schemas are un-vendored, so these are this build's own): q|k|v on one shared
+        # activation quantization, and the whole MLP block
+        lib.define("bitnet_qkv_forward_cpu(Tensor x, Tensor packed_qkv, int q_rows, int k_rows, int v_rows, "
+                   "float ws_q, float ws_k, float ws_v, int fmt=0) -> (Tensor, Tensor, Tensor)")
+        lib.define("bitnet_mlp_forward_cpu(Tensor x, Tensor packed_gate_up, Tensor packed_down, float ws_gate, "
+                   "float ws_up, float ws_down, Tensor ffn_sub_norm, float eps=1e-05, int fmt=0) -> Tensor")
     except RuntimeError:
         return False
 
@@ -441,10 +448,27 @@ def register_torch_ops() -> bool:
         q, s = quantize_activations_i8(x)
         return q, torch.tensor([s], dtype=torch.float32, device=q.device)
 
+    def _qkv(x, w, qr, kr, vr, wq, wk, wv, fmt):
+        return tuple(bitnet_linear_fused(x, w, [qr, kr, vr], [wq, wk, wv], fmt))
+
+    def _mlp(x, wgu, wd, wg, wu, wdn, nw, eps, fmt):
+        return bitnet_mlp(x, wgu, wd, wg, wu, wdn, nw, eps, fmt)
+
     for key in ("CUDA", "CPU"):
         lib.impl("bitnet_gemv_cpu", _gemv, key)
         lib.impl("bitnet_gemm_cpu", _gemm, key)
         lib.impl("bitnet_quantize_activations_cpu", _quant, key)
+        lib.impl("bitnet_qkv_forward_cpu", _qkv, key)  # host tensors are staged through the GPU
+    lib.impl("bitnet_mlp_forward_cpu", _mlp, "CUDA")  # device tensors only (bitnet_mlp)
+
+    @torch.library.register_fake("sgl_kernel::bitnet_qkv_forward_cpu", lib=lib)
+    def _(x, packed_qkv, q_rows, k_rows, v_rows, ws_q, ws_k, ws_v, fmt=0):
+        lead = x.shape[:-1]
+        return tuple(x.new_empty((*lead, r), dtype=torch.bfloat16) for r in (q_rows, k_rows, v_rows))
+
+    @torch.library.register_fake("sgl_kernel::bitnet_mlp_forward_cpu", lib=lib)
+    def _(x, packed_gate_up, packed_down, ws_gate, ws_up, ws_down, ffn_sub_norm, eps=1e-5, fmt=0):
+        return x.new_empty(x.shape, dtype=torch.bfloat16)
 
     @torch.library.register_fake("sgl_kernel::bitnet_gemv_cpu", lib=lib)
     def _(packed_weights, activations, scale):
