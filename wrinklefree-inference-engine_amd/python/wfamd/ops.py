@@ -448,10 +448,10 @@ def register_torch_ops() -> bool:
         q, s = quantize_activations_i8(x)
         return q, torch.tensor([s], dtype=torch.float32, device=q.device)
 
-    def _qkv(x, w, qr, kr, vr, wq, wk, wv, fmt):
+    def _qkv(x, w, qr, kr, vr, wq, wk, wv, fmt=0):  # torch drops arguments equal to the schema default
         return tuple(bitnet_linear_fused(x, w, [qr, kr, vr], [wq, wk, wv], fmt))
 
-    def _mlp(x, wgu, wd, wg, wu, wdn, nw, eps, fmt):
+    def _mlp(x, wgu, wd, wg, wu, wdn, nw, eps=1e-5, fmt=0):
         return bitnet_mlp(x, wgu, wd, wg, wu, wdn, nw, eps, fmt)
 
     for key in ("CUDA", "CPU"):
