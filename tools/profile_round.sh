@@ -48,6 +48,9 @@ for B in 1 128; do
         python3 "$R/bench.py" --batch $B --steps 100 --warmup 10 --no-cpu-baseline --no-gemv > "$O/prof_b$B.log" 2>&1 || exit $?
     cd "$R" && python3 tools/prof_summary.py "$O/prof_b$B" > "$O/kernel_stats_b$B.txt" 2>&1 || exit $?
     rm -rf "$O/prof_b$B"  # raw traces: gpurun_out/ must stay under 64 MiB
+    OPS=rocprof_ops; [ $B -gt 1 ] && OPS=rocprof_ops_b$B
+    python3 tools/rocprof_ops.py "$O/kernel_stats_b$B.txt" "$TAG" $OPS > /dev/null || exit $?
+    cp profiles/$OPS.json profiles/${OPS}_$TAG.json "$O/" || exit $?
     for C in FETCH_SIZE WRITE_SIZE; do
         step "pmc $C b$B"
         cd /tmp && timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$O/pmc_${C}_b$B" -o run -- \
@@ -59,9 +62,14 @@ for B in 1 128; do
     cp profiles/$STEM.json "$O/" && rm -rf "$O/pmc_FETCH_SIZE_b$B" "$O/pmc_WRITE_SIZE_b$B"
 done
 step gemv
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_gemv" -o run -- python3 "$R/tools/gemv_bench.py" > "$O/prof_gemv.log" 2>&1 || exit $?
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_gemv" -o run -- python3 "$R/tools/gemv_bench.py" > "$O/prof_gemv.log" 2>&1 || exit $?
 cd "$R" && python3 tools/prof_summary.py "$O/prof_gemv" > "$O/kernel_stats_gemv.txt" 2>&1 || exit $?
+python3 tools/trace_gaps.py "$O/prof_gemv" k_gemv_rows > "$O/gemv_trace_gaps.txt" 2>&1 || exit $?
 rm -rf "$O/prof_gemv"
+step gemv-stamps
+timeout -k 10 300 python tools/gemv_stamps.py > "$O/gemv_stamps.txt" 2>&1 || exit $?
+step stamps-b1
+timeout -k 10 300 python tools/stamps_graph.py --ctx 1024 > "$O/stamps_b1.txt" 2>&1 || exit $?
 tail -1 "$O/prof_gemv.log" | cut -c1-300
 step replicas-same-gpu
 timeout -k 10 300 python tools/replica_node.py --replicas 2 --same-gpu --steps 50 > "$O/replicas.log" 2>&1 || exit $?
