@@ -72,7 +72,7 @@ step stamps-b1
 timeout -k 10 300 python tools/stamps_graph.py --ctx 1024 > "$O/stamps_b1.txt" 2>&1 || exit $?
 tail -1 "$O/prof_gemv.log" | cut -c1-300
 step replicas-same-gpu
-timeout -k 10 300 python tools/replica_node.py --replicas 2 --same-gpu --steps 50 > "$O/replicas.log" 2>&1 || exit $?
+timeout -k 10 300 python tools/replica_node.py --replicas 2 --same-gpu --steps 300 > "$O/replicas.log" 2>&1 || exit $?
 tail -1 "$O/replicas.log" | cut -c1-300
 step prefill
 timeout -k 10 300 python tools/prefill_gemm_bench.py > "$O/prefill.log" 2>&1 || exit $?
