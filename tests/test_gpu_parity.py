@@ -374,6 +374,34 @@ def test_decode_graph_equals_eager_and_batch_rows_independent():
         assert int(decb.tokens[b]) == int(dec1.tokens[0])
 
 
+@pytest.mark.parametrize("B,wfmt", [(5, 1), (6, 0)])
+def test_decode_small_batch_distinct_rows_match_single(B, wfmt):
+    """Batch 2..15 runs the batch-1 kernels per row (GEMV blocks per row, one attention block per
+    (split, head, sequence) with the per-(sequence, head) merge ticket, the LM head stream with 1 or 2
+    rows per block): every row, each with its own start token, must equal a batch-1 run of that
+    token bit for bit over 4 greedy steps (distinct rows catch a ticket or row index mixed across
+    sequences, which identical rows would hide)."""
+    g, decb = _small_decoder(wfmt, batch=B)
+    toks = [int(t) for t in g["tokens"]]
+    starts = [toks[(3 * b + 1) % len(toks)] for b in range(B)]
+    assert len(set(starts)) > 1
+    decb.set_state(starts, [0] * B)
+    singles = {}
+    for t in sorted(set(starts)):
+        _, d1 = _small_decoder(wfmt, batch=1)
+        d1.set_state([t], [0])
+        singles[t] = d1
+    for _ in range(4):
+        decb.step(graph=True)
+        for d1 in singles.values():
+            d1.step(graph=True)
+        torch.cuda.synchronize()
+        for b in range(B):
+            d1 = singles[starts[b]]
+            assert torch.equal(decb.logits[b], d1.logits[0]), b
+            assert int(decb.tokens[b]) == int(d1.tokens[0]), b
+
+
 def test_decode_batched_mfma_rows_match_single():
     """Batch >= 16 runs the int8-MFMA GEMMs, the bf16-MFMA LM head and the row argmax; every row
     (its own start token, positions 0..3) must match a batch-1 run of the same sequence: logits
