@@ -1000,6 +1000,18 @@ __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int b
     }
     __syncthreads();
     const int head0 = bn * 2, nheads = g.Hq + 2 * g.Hkv;
+    // the row tile of fragment (i, j) does not depend on j in the 2 x 4 wave grid: its rows' scale
+    // and code sum are read from LDS once per (i, r), not once per fragment
+    float sfv[4][4];
+    int asv[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int rl = pg_frag_rt<4, CW>(wave, i, 0) * 16 + 4 * q + r;
+            sfv[i][r] = s_sf[rl];
+            asv[i][r] = s_as[rl];
+        }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
 #pragma unroll
@@ -1009,7 +1021,8 @@ __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int b
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int rl = pg_frag_rt<4, CW>(wave, i, j) * 16 + 4 * q + r;
-                const float v = rbf(corrected(acc[i][j][r], ws, s_as[rl], s_sf[rl]));
+                const float v = CW ? rbf(corrected(acc[i][j][r], ws, s_as[rl], s_sf[rl]))
+                                   : rbf(corrected(acc[i][j][r], ws, asv[i][r], sfv[i][r]));
                 const float nv = dpp_f<DPP_QP_1032>(v);  // column l16 ^ 1
                 if (!(l16 & 1)) *reinterpret_cast<uint32_t*>(tile + rl * kPfEpiRS + (16 * ct + l16) * 2) = pk_bf16(v, nv);
             }
@@ -1017,16 +1030,29 @@ __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int b
     }
     __syncthreads();
     const int8_t kv8 = (int8_t)g.kv8;
-    // q and k heads: item = (row, column tile) -> 8 dims of each RoPE half
-    for (int it = threadIdx.x; it < 128 * 16; it += 512) {
+    // q and k heads: item = (row, column tile) -> 8 dims of each RoPE half. Every item's cos / sin
+    // pieces are in flight before the first item is processed (a load inside the item loop waited
+    // one L2 round trip per item: its stores may alias the tables)
+    constexpr int kQkItems = 128 * 16 / 512;
+    uint4 csv[kQkItems], snv[kQkItems];
+#pragma unroll
+    for (int k = 0; k < kQkItems; ++k) {
+        const int it = threadIdx.x + 512 * k, rl = it >> 4, tt = it & 7;
+        const int pos = s_pos[rl];
+        csv[k] = *reinterpret_cast<const uint4*>(g.rope_cos + (int64_t)pos * 64 + 8 * tt);
+        snv[k] = *reinterpret_cast<const uint4*>(g.rope_sin + (int64_t)pos * 64 + 8 * tt);
+    }
+#pragma unroll
+    for (int k = 0; k < kQkItems; ++k) {
+        const int it = threadIdx.x + 512 * k;
         const int rl = it >> 4, ct = it & 15, tt = ct & 7, head = head0 + (ct >> 3);
         const int m = bm * 128 + rl;
         if (m >= g.B || head >= g.Hq + g.Hkv) continue;
         const uint4 lo = *reinterpret_cast<const uint4*>(tile + rl * kPfEpiRS + ct * 32);
         const uint4 hi = *reinterpret_cast<const uint4*>(tile + rl * kPfEpiRS + ct * 32 + 16);
         const int pos = s_pos[rl];
-        const uint4 cs = *reinterpret_cast<const uint4*>(g.rope_cos + (int64_t)pos * 64 + 8 * tt);
-        const uint4 sn = *reinterpret_cast<const uint4*>(g.rope_sin + (int64_t)pos * 64 + 8 * tt);
+        const uint4 cs = csv[k];
+        const uint4 sn = snv[k];
         const uint32_t x1[4] = {lo.x, lo.y, lo.z, lo.w}, x2[4] = {hi.x, hi.y, hi.z, hi.w};
         const uint32_t c4[4] = {cs.x, cs.y, cs.z, cs.w}, s4[4] = {sn.x, sn.y, sn.z, sn.w};
         float y1[8], y2[8];  // RotaryEmbedding._rotate (direct_inference_full.py:58-70)
