@@ -499,6 +499,21 @@ struct EpiDec {
         load_rope(c0, l16, in);
         apply(r0, c0, acc, l16, q, in);
     }
+    // GU: act = bf16(bf16(relu(g)^2) * u) of the fragment's rows, quad-transposed: lane (quad k <
+    // 2, qi) gets row 4q + qi, act columns 4k .. 4k + 3 of the fragment's 8, as 4 packed bf16
+    __device__ __forceinline__ uint2 gu_pack(const v4i_t& acc, const EpiIn& in, int l16) const {
+        const GemvArgs& g = *a;
+        const float ws = l16 < 8 ? g.ws0 : g.ws1;
+        float y[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float v = rbf(corrected(acc[r], ws, in.as[r], in.sf[r]));
+            const float pv = dpp_f<DPP_ROW_ROR8>(v);  // partner column l16 ^ 8 (same rows)
+            const float gt = fmaxf(v, 0.f);
+            y[r] = rbf(rbf(gt * gt) * pv);
+        }
+        return quad_transpose_bf16(y, l16 & 3);
+    }
     __device__ __forceinline__ void apply(int r0, int c0, const v4i_t& acc, int l16, int q, const EpiIn& in) {
         const GemvArgs& g = *a;
         const int tile = c0 >> 4, n = c0 + l16, B = g.B, N = g.N;
@@ -509,17 +524,8 @@ struct EpiDec {
             // one 8-byte store per lane instead of four 2-byte ones (the stores were the epilogue's cost:
             // a quarter of them took the prefill gate|up GEMM from 570 to 472 us per layer).
             if (((g.out_stride & 3) | (reinterpret_cast<uintptr_t>(g.out) & 7)) == 0) {
-                const float ws = l16 < 8 ? g.ws0 : g.ws1;
-                float y[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float v = rbf(corrected(acc[r], ws, in.as[r], in.sf[r]));
-                    const float pv = dpp_f<DPP_ROW_ROR8>(v);  // partner column l16 ^ 8 (same rows)
-                    const float gt = fmaxf(v, 0.f);
-                    y[r] = rbf(rbf(gt * gt) * pv);
-                }
                 const int qi = l16 & 3, m = r0 + 4 * q + qi;
-                const uint2 pk = quad_transpose_bf16(y, qi);
+                const uint2 pk = gu_pack(acc, in, l16);
                 if (l16 < 8 && m < B && tile * 16 < N)
                     *reinterpret_cast<uint2*>(g.out + (int64_t)m * g.out_stride + tile * 8 + 4 * (l16 >> 2)) = pk;
                 return;
@@ -1245,6 +1251,37 @@ __global__ __launch_bounds__(512) void k_pgemm_fused(GemvArgs a, int nbm, int nb
     } else if constexpr (STAGED) {
         pf_tile_epilogue<MODE, TNW, CW>(a, bm, bn, acc, lds);
     } else {
+    if constexpr (MODE == MODE_GU && !CW && TNW % 2 == 0) {
+        // gate|up, 16-byte stores: fragments j, j + 1 hold act columns 8 T .. 8 T + 15 of the same
+        // rows (T = their first 16-column tile, even). After gu_pack lane quad 0 has columns 0-3 and
+        // quad 1 columns 4-7 of each; quad 0 takes quad 1's part of fragment j (DPP row_shl:4), quad 1
+        // quad 0's part of fragment j + 1 (row_shr:4), and each stores 8 columns = one dwordx4: half
+        // the store instructions of one dwordx2 per fragment (the epilogue is store-issue-bound)
+        if (((a.out_stride & 7) | (reinterpret_cast<uintptr_t>(a.out) & 15)) == 0) {
+            EpiDec<MODE> e{&a};
+            const int k = (l16 >> 2) & 1, qi = l16 & 3;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r0 = bm * 128 + pg_frag_rt<TNW, CW>(wave, i, 0) * 16, m = r0 + 4 * q + qi;
+                EpiIn in;
+                e.load(r0, bn * BC + pg_frag_ct<TNW, CW>(wave, i, 0) * 16, l16, q, in);
+#pragma unroll
+                for (int p = 0; p < TNW / 2; ++p) {
+                    const uint2 y0 = e.gu_pack(acc[i][2 * p], in, l16), y1 = e.gu_pack(acc[i][2 * p + 1], in, l16);
+                    // both exchanges in every lane (a DPP inside a divergent branch reads disabled lanes as 0)
+                    const int sx = (int)(k ? y0.x : y1.x), sy = (int)(k ? y0.y : y1.y);
+                    const uint32_t ux = (uint32_t)dpp_i<0x104>(sx), uy = (uint32_t)dpp_i<0x104>(sy);  // lane + 4
+                    const uint32_t dx = (uint32_t)dpp_i<0x114>(sx), dy = (uint32_t)dpp_i<0x114>(sy);  // lane - 4
+                    const uint32_t rx = k ? dx : ux, ry = k ? dy : uy;
+                    const uint4 o = k ? make_uint4(rx, ry, y1.x, y1.y) : make_uint4(y0.x, y0.y, rx, ry);
+                    const int T = (bn * BC + pg_frag_ct<TNW, CW>(wave, i, 2 * p) * 16) / 16 + k;
+                    if (l16 < 8 && m < a.B && T * 16 < a.N)
+                        *reinterpret_cast<uint4*>(a.out + (int64_t)m * a.out_stride + T * 8) = o;
+                }
+            }
+            return;
+        }
+    }
     // epilogue per row tile: the column tiles' per-row inputs (scale, code sum, residual) are all
     // issued before the first store -- one round trip per row tile instead of per fragment (stores
     // in between would pin the loads behind them): o 159 -> 141, down 291 -> 274 us
