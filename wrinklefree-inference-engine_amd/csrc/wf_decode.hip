@@ -501,18 +501,29 @@ struct EpiDec {
     }
     // GU: act = bf16(bf16(relu(g)^2) * u) of the fragment's rows, quad-transposed: lane (quad k <
     // 2, qi) gets row 4q + qi, act columns 4k .. 4k + 3 of the fragment's 8, as 4 packed bf16
+    // (rows in pairs through the packed-fp32 VALU: v_pk_mul_f32 / v_pk_add_f32 round each lane like
+    // the scalar ops, so the float sequence of corrected() and the activation is unchanged)
     __device__ __forceinline__ uint2 gu_pack(const v4i_t& acc, const EpiIn& in, int l16) const {
+        typedef float f2 __attribute__((ext_vector_type(2)));
         const GemvArgs& g = *a;
         const float ws = l16 < 8 ? g.ws0 : g.ws1;
-        float y[4];
+        const f2 W = {ws, ws};
+        uint32_t yp[2];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float v = rbf(corrected(acc[r], ws, in.as[r], in.sf[r]));
-            const float pv = dpp_f<DPP_ROW_ROR8>(v);  // partner column l16 ^ 8 (same rows)
-            const float gt = fmaxf(v, 0.f);
-            y[r] = rbf(rbf(gt * gt) * pv);
+        for (int h = 0; h < 2; ++h) {
+            const f2 S = {(float)acc[2 * h], (float)acc[2 * h + 1]};
+            const f2 C = W * f2{(float)in.as[2 * h], (float)in.as[2 * h + 1]};
+            const f2 SF = {in.sf[2 * h], in.sf[2 * h + 1]};
+            const f2 u = (S * W - C) * SF;  // corrected(): fl32(fl32(S ws) - fl32(ws asum)) * sf
+            const uint32_t vp = pk_bf16(u.x, u.y);
+            const f2 v = {bf_lo(vp), bf_hi(vp)};
+            const f2 pv = {dpp_f<DPP_ROW_ROR8>(v.x), dpp_f<DPP_ROW_ROR8>(v.y)};  // partner column l16 ^ 8
+            const f2 gt = {fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
+            const uint32_t gp = pk_bf16((gt * gt).x, (gt * gt).y);
+            const f2 y = f2{bf_lo(gp), bf_hi(gp)} * pv;
+            yp[h] = pk_bf16(y.x, y.y);
         }
-        return quad_transpose_bf16(y, l16 & 3);
+        return quad_transpose_pk(yp[0], yp[1], l16 & 3);
     }
     __device__ __forceinline__ void apply(int r0, int c0, const v4i_t& acc, int l16, int q, const EpiIn& in) {
         const GemvArgs& g = *a;

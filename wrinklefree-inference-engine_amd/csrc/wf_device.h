@@ -73,8 +73,12 @@ __device__ __forceinline__ T dpp_cast(T v, T old = T(0)) {
 // bf16-representable); returns row qi of M^T packed as bf16 pairs: (M[0][qi], M[1][qi]),
 // (M[2][qi], M[3][qi]). Two DPP exchanges: 2 x 2 blocks across lanes qi ^ 2, then 16-bit halves
 // across lanes qi ^ 1 (v_perm_b32 selects the halves).
+__device__ __forceinline__ uint2 quad_transpose_pk(uint32_t A, uint32_t B, int qi);
 __device__ __forceinline__ uint2 quad_transpose_bf16(const float (&y)[4], int qi) {
-    const uint32_t A = pk_bf16(y[0], y[1]), B = pk_bf16(y[2], y[3]);
+    return quad_transpose_pk(pk_bf16(y[0], y[1]), pk_bf16(y[2], y[3]), qi);
+}
+// the same on the packed pairs A = (y0, y1), B = (y2, y3)
+__device__ __forceinline__ uint2 quad_transpose_pk(uint32_t A, uint32_t B, int qi) {
     const bool hi2 = qi & 2, odd = qi & 1;
     // own = (M[qi][r0], M[qi][r0 + 1]), other = (M[qi ^ 2][r0], M[qi ^ 2][r0 + 1]), r0 = qi & 2
     const uint32_t own = hi2 ? B : A;
