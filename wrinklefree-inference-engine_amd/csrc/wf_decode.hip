@@ -1036,12 +1036,18 @@ __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int b
             const int ct = pg_frag_ct<4, CW>(wave, i, j), head = head0 + (ct >> 3);
             const float ws = head < g.Hq ? g.ws0 : (head < g.Hq + g.Hkv ? g.ws1 : g.ws2);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int rl = pg_frag_rt<4, CW>(wave, i, j) * 16 + 4 * q + r;
-                const float v = CW ? rbf(corrected(acc[i][j][r], ws, s_as[rl], s_sf[rl]))
-                                   : rbf(corrected(acc[i][j][r], ws, asv[i][r], sfv[i][r]));
-                const float nv = dpp_f<DPP_QP_1032>(v);  // column l16 ^ 1
-                if (!(l16 & 1)) *reinterpret_cast<uint32_t*>(tile + rl * kPfEpiRS + (16 * ct + l16) * 2) = pk_bf16(v, nv);
+            for (int h = 0; h < 2; ++h) {  // rows in pairs (pf_tile_epilogue's packed form)
+                const int rl = pg_frag_rt<4, CW>(wave, i, j) * 16 + 4 * q + 2 * h;
+                const uint32_t vp =
+                    CW ? corrected_pk(acc[i][j][2 * h], acc[i][j][2 * h + 1], ws, s_as[rl], s_as[rl + 1], s_sf[rl], s_sf[rl + 1])
+                       : corrected_pk(acc[i][j][2 * h], acc[i][j][2 * h + 1], ws, asv[i][2 * h], asv[i][2 * h + 1],
+                                      sfv[i][2 * h], sfv[i][2 * h + 1]);
+                const uint32_t np = (uint32_t)dpp_i<DPP_QP_1032>((int)vp);  // column l16 ^ 1, same rows
+                if (!(l16 & 1)) {
+                    *reinterpret_cast<uint32_t*>(tile + rl * kPfEpiRS + (16 * ct + l16) * 2) = __builtin_amdgcn_perm(np, vp, 0x05040100u);
+                    *reinterpret_cast<uint32_t*>(tile + (rl + 1) * kPfEpiRS + (16 * ct + l16) * 2) =
+                        __builtin_amdgcn_perm(np, vp, 0x07060302u);
+                }
             }
         }
     }
@@ -1207,7 +1213,7 @@ __device__ __forceinline__ void pf_tile_epilogue(const GemvArgs& g, int bm, int 
             const int rt = pg_frag_rt<TNW, CW>(wave, i, j), ct = pg_frag_ct<TNW, CW>(wave, i, j);
             const float ws = (MODE == MODE_GU && l16 >= 8) ? g.ws1 : g.ws0;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
+            for (int r = 0; r < 4 && MODE == MODE_GU; ++r) {
                 const int rl = rt * 16 + 4 * q + r;
                 const float v = rbf(corrected(acc[i][j][r], ws, s_as[rl], s_sf[rl]));
                 if constexpr (MODE == MODE_GU) {
@@ -1216,9 +1222,22 @@ __device__ __forceinline__ void pf_tile_epilogue(const GemvArgs& g, int bm, int 
                     const float y = rbf(rbf(gt * gt) * pv);
                     const float ny = dpp_f<DPP_QP_1032>(y);  // column l16 ^ 1
                     if (l16 < 8 && !(l16 & 1)) *reinterpret_cast<uint32_t*>(tile + rl * RS + (ct * 8 + l16) * 2) = pk_bf16(y, ny);
-                } else {
-                    const float nv = dpp_f<DPP_QP_1032>(v);
-                    if (!(l16 & 1)) *reinterpret_cast<uint32_t*>(tile + rl * RS + (ct * 16 + l16) * 2) = pk_bf16(v, nv);
+                }
+            }
+            if constexpr (MODE != MODE_GU) {
+                // rows in pairs: one packed correction, one DPP for both rows' column l16 ^ 1, and
+                // the (column l16, l16 ^ 1) words of each row assembled by v_perm
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int rl = rt * 16 + 4 * q + 2 * h;
+                    const uint32_t vp = corrected_pk(acc[i][j][2 * h], acc[i][j][2 * h + 1], ws, s_as[rl], s_as[rl + 1],
+                                                     s_sf[rl], s_sf[rl + 1]);
+                    const uint32_t np = (uint32_t)dpp_i<DPP_QP_1032>((int)vp);  // column l16 ^ 1, same rows
+                    if (!(l16 & 1)) {
+                        *reinterpret_cast<uint32_t*>(tile + rl * RS + (ct * 16 + l16) * 2) = __builtin_amdgcn_perm(np, vp, 0x05040100u);
+                        *reinterpret_cast<uint32_t*>(tile + (rl + 1) * RS + (ct * 16 + l16) * 2) =
+                            __builtin_amdgcn_perm(np, vp, 0x07060302u);
+                    }
                 }
             }
         }

@@ -95,6 +95,16 @@ __device__ __forceinline__ uint2 quad_transpose_pk(uint32_t A, uint32_t B, int q
     return hi2 ? make_uint2(p23, p01) : make_uint2(p01, p23);
 }
 
+// Two rows of one 16 x 16 accumulator column through the reference correction
+// (direct_inference_full.py:201-208: fl32(fl32(S ws) - fl32(ws asum)) * s) on the packed-fp32 VALU
+// (v_pk_mul_f32 / v_pk_add_f32 round each lane like the scalar ops), returned as a bf16 pair.
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t corrected_pk(int s0, int s1, float ws, int a0, int a1, float f0, float f1) {
+    const f32x2_t W = {ws, ws};
+    const f32x2_t u = (f32x2_t{(float)s0, (float)s1} * W - W * f32x2_t{(float)a0, (float)a1}) * f32x2_t{f0, f1};
+    return pk_bf16(u.x, u.y);
+}
+
 struct OpAdd {
     template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return a + b; }
 };
