@@ -1427,34 +1427,42 @@ __global__ void k_bf_tile(const uint16_t* __restrict__ src, int R, int H, uint16
 // Per (row, block) the (max, first index) of the block's 256 logits goes to `part`.
 typedef short v8s_t __attribute__((ext_vector_type(8)));
 typedef float v4f_t __attribute__((ext_vector_type(4)));
-#ifndef WF_LM_STAGES  // study builds only (tools/build_variant.sh)
-#define WF_LM_STAGES 4
+// NW waves of 64 vocabulary rows per block (round 4: 8 waves = 512 rows): every block re-reads the
+// whole 640 KB A (hn) from L2 through LDS, so at 256 rows A was a third of the LDS-DMA traffic the
+// launch is bound by (984 MB for 657 MB of E); at 512 rows a fifth (816 MB). P stages in the ring
+// (3 at 8 waves: 40 KiB stages).
+#ifndef WF_LM_WAVES  // study builds only (tools/build_var.sh)
+#define WF_LM_WAVES 8
 #endif
-constexpr int kLmStages = WF_LM_STAGES;
-constexpr int kLmStageBytes = 8 * 1024 + 4 * 4096;
-__global__ __launch_bounds__(256) void k_lm_head_mfma(const uint16_t* __restrict__ E, const uint16_t* __restrict__ hn,
-                                                      int H, int V, int B, uint16_t* __restrict__ logits,
-                                                      uint2* __restrict__ part, int nblk) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLmStages * kLmStageBytes];
-    __shared__ float s_val[4][128];
-    __shared__ int s_idx[4][128];
-    constexpr int P = kLmStages;
+constexpr int kLmWaves = WF_LM_WAVES;
+constexpr int kLmStages = kLmWaves == 4 ? 4 : 3;
+template <int NW>
+constexpr int lm_stage_bytes() { return 8 * 1024 + NW * 4096; }
+template <int NW, int P>
+__global__ __launch_bounds__(NW * 64) void k_lm_head_mfma(const uint16_t* __restrict__ E, const uint16_t* __restrict__ hn,
+                                                          int H, int V, int B, uint16_t* __restrict__ logits,
+                                                          uint2* __restrict__ part, int nblk) {
+    static_assert(NW == 4 || NW == 8, "A row tiles: 2 per wave at 4 waves, 1 at 8");
+    constexpr int SB = lm_stage_bytes<NW>(), AU = 8 / NW, NDMA = AU + 4;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[P * SB];
+    __shared__ float s_val[NW][128];
+    __shared__ int s_idx[NW][128];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
-    const int m0 = blockIdx.y * 128, n0 = blockIdx.x * 256 + wave * 64;
+    const int m0 = blockIdx.y * 128, n0 = blockIdx.x * (64 * NW) + wave * 64;
     const int steps = H / 32;
     // both operands in the fragment layout (bf_tile_off): fragment (tile, k-step c) of this lane at
     // tile_base + 512 c elements -- one contiguous KiB per wave-instruction
     const int nrt = (B + 15) >> 4, nvt = V >> 4;
-    const uint16_t* asrc[2];
+    const uint16_t* asrc[AU];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) asrc[u] = hn + (((int64_t)min((m0 >> 4) + 2 * wave + u, nrt - 1) * steps) << 9) + lane * 8;
+    for (int u = 0; u < AU; ++u) asrc[u] = hn + (((int64_t)min((m0 >> 4) + AU * wave + u, nrt - 1) * steps) << 9) + lane * 8;
     const uint16_t* bsrc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) bsrc[j] = E + (((int64_t)min((n0 >> 4) + j, nvt - 1) * steps) << 9) + lane * 8;
     auto issue = [&](int c) {
-        uint8_t* st = lds + (c % P) * kLmStageBytes;
+        uint8_t* st = lds + (c % P) * SB;
 #pragma unroll
-        for (int u = 0; u < 2; ++u) glds16_asm(asrc[u] + 512 * c, st + (2 * wave + u) * 1024);
+        for (int u = 0; u < AU; ++u) glds16_asm(asrc[u] + 512 * c, st + (AU * wave + u) * 1024);
 #pragma unroll
         for (int j = 0; j < 4; ++j) glds16_asm(bsrc[j] + 512 * c, st + 8192 + wave * 4096 + j * 1024);
     };
@@ -1467,11 +1475,11 @@ __global__ __launch_bounds__(256) void k_lm_head_mfma(const uint16_t* __restrict
     for (int c = 0; c < P - 1; ++c)
         if (c < steps) issue(c);
     for (int c = 0; c < steps; ++c) {
-        if (c + P - 2 < steps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * (P - 2)) : "memory");
+        if (c + P - 2 < steps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA * (P - 2)) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if (c + P - 1 < steps) issue(c + P - 1);
-        const uint8_t* st = lds + (c % P) * kLmStageBytes;
+        const uint8_t* st = lds + (c % P) * SB;
         v8s_t bf[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const v8s_t*>(st + 8192 + wave * 4096 + j * 1024 + lane * 16);
@@ -1514,7 +1522,7 @@ __global__ __launch_bounds__(256) void k_lm_head_mfma(const uint16_t* __restrict
         const int row = threadIdx.x;
         float bv = s_val[0][row];
         int bi = s_idx[0][row];
-        for (int w = 1; w < 4; ++w)
+        for (int w = 1; w < NW; ++w)
             if (s_val[w][row] > bv || (s_val[w][row] == bv && s_idx[w][row] < bi)) { bv = s_val[w][row]; bi = s_idx[w][row]; }
         part[(int64_t)(m0 + row) * nblk + blockIdx.x] = make_uint2(__float_as_uint(bv), (uint32_t)bi);
     }
@@ -2447,9 +2455,9 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             if (m->embed_t) {
                 launch_rownorm(m, m->h_a, H, d.final_norm, H, m->hn, st);
                 if ((rc = check_launch("final_norm"))) return rc;
-                const int nb = (d.vocab + 255) / 256;
-                hipLaunchKernelGGL(k_lm_head_mfma, dim3(nb, (B + 127) / 128), dim3(256), 0, st, m->embed_t, m->hn, H, d.vocab,
-                                   B, m->logits, m->am_part, nb);
+                const int nb = (d.vocab + 64 * kLmWaves - 1) / (64 * kLmWaves);
+                hipLaunchKernelGGL((k_lm_head_mfma<kLmWaves, kLmStages>), dim3(nb, (B + 127) / 128), dim3(64 * kLmWaves), 0,
+                                   st, m->embed_t, m->hn, H, d.vocab, B, m->logits, m->am_part, nb);
                 hipLaunchKernelGGL(k_argmax_rows, dim3(B), dim3(256), 0, st, m->am_part, nb, m->tokens, m->positions, S);
                 break;
             }
