@@ -1078,22 +1078,21 @@ __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int b
         const uint4 sn = snv[k];
         const uint32_t x1[4] = {lo.x, lo.y, lo.z, lo.w}, x2[4] = {hi.x, hi.y, hi.z, hi.w};
         const uint32_t c4[4] = {cs.x, cs.y, cs.z, cs.w}, s4[4] = {sn.x, sn.y, sn.z, sn.w};
-        float y1[8], y2[8];  // RotaryEmbedding._rotate (direct_inference_full.py:58-70)
+        // RotaryEmbedding._rotate (direct_inference_full.py:58-70) on packed bf16 pairs: y1 = x1 c -
+        // x2 s, y2 = x1 s + x2 c, every product and sum rounded to bf16 (rope_pk)
+        uint32_t p1[4], p2[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) rope_pk(x1[t], x2[t], c4[t], s4[t], p1[t], p2[t]);
+        float y1[8], y2[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            const float a = (e & 1) ? bf_hi(x1[e >> 1]) : bf_lo(x1[e >> 1]);
-            const float b = (e & 1) ? bf_hi(x2[e >> 1]) : bf_lo(x2[e >> 1]);
-            const float c = (e & 1) ? bf_hi(c4[e >> 1]) : bf_lo(c4[e >> 1]);
-            const float sv = (e & 1) ? bf_hi(s4[e >> 1]) : bf_lo(s4[e >> 1]);
-            y1[e] = rbf(rbf(a * c) - rbf(b * sv));
-            y2[e] = rbf(rbf(a * sv) + rbf(b * c));
+            y1[e] = (e & 1) ? bf_hi(p1[e >> 1]) : bf_lo(p1[e >> 1]);
+            y2[e] = (e & 1) ? bf_hi(p2[e >> 1]) : bf_lo(p2[e >> 1]);
         }
         if (head < g.Hq) {
             uint16_t* qo = g.out + (int64_t)m * g.out_stride + head * 128 + 8 * tt;
-            *reinterpret_cast<uint4*>(qo) = make_uint4(pk_bf16(y1[0], y1[1]), pk_bf16(y1[2], y1[3]),
-                                                       pk_bf16(y1[4], y1[5]), pk_bf16(y1[6], y1[7]));
-            *reinterpret_cast<uint4*>(qo + 64) = make_uint4(pk_bf16(y2[0], y2[1]), pk_bf16(y2[2], y2[3]),
-                                                            pk_bf16(y2[4], y2[5]), pk_bf16(y2[6], y2[7]));
+            *reinterpret_cast<uint4*>(qo) = make_uint4(p1[0], p1[1], p1[2], p1[3]);
+            *reinterpret_cast<uint4*>(qo + 64) = make_uint4(p2[0], p2[1], p2[2], p2[3]);
             continue;
         }
         const int kvh = head - g.Hq;
@@ -1112,10 +1111,8 @@ __device__ __forceinline__ void pf_qkv_epilogue(const GemvArgs& g, int bm, int b
             *reinterpret_cast<uint2*>(c8 + o1) = make_uint2(b1[0], b1[1]);
             *reinterpret_cast<uint2*>(c8 + o2) = make_uint2(b2[0], b2[1]);
         } else {
-            *reinterpret_cast<uint4*>(g.kc + o1) = make_uint4(pk_bf16(y1[0], y1[1]), pk_bf16(y1[2], y1[3]),
-                                                              pk_bf16(y1[4], y1[5]), pk_bf16(y1[6], y1[7]));
-            *reinterpret_cast<uint4*>(g.kc + o2) = make_uint4(pk_bf16(y2[0], y2[1]), pk_bf16(y2[2], y2[3]),
-                                                              pk_bf16(y2[4], y2[5]), pk_bf16(y2[6], y2[7]));
+            *reinterpret_cast<uint4*>(g.kc + o1) = make_uint4(p1[0], p1[1], p1[2], p1[3]);
+            *reinterpret_cast<uint4*>(g.kc + o2) = make_uint4(p2[0], p2[1], p2[2], p2[3]);
         }
     }
     // v heads: item = (8-row group, dim) -> one V tile piece of 8 keys
@@ -1255,7 +1252,7 @@ __device__ __forceinline__ void pf_tile_epilogue(const GemvArgs& g, int bm, int 
             const uint32_t rv[4] = {rs.x, rs.y, rs.z, rs.w};
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-                ov[e] = pk_bf16(rbf(bf_lo(rv[e]) + bf_lo(ov[e])), rbf(bf_hi(rv[e]) + bf_hi(ov[e])));
+                ov[e] = bf16_add_pk(rv[e], ov[e]);
             v = make_uint4(ov[0], ov[1], ov[2], ov[3]);
         }
         *reinterpret_cast<uint4*>(g.out + (int64_t)m * g.out_stride + n) = v;

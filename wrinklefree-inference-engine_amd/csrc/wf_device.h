@@ -105,6 +105,24 @@ __device__ __forceinline__ uint32_t corrected_pk(int s0, int s1, float ws, int a
     return pk_bf16(u.x, u.y);
 }
 
+// bf16(a + b) for two packed bf16 pairs (the residual add bf16(resid + bf16(o)))
+__device__ __forceinline__ uint32_t bf16_add_pk(uint32_t a, uint32_t b) {
+    const f32x2_t s = f32x2_t{bf_lo(a), bf_hi(a)} + f32x2_t{bf_lo(b), bf_hi(b)};
+    return pk_bf16(s.x, s.y);
+}
+// RoPE on a packed bf16 pair of each half: y1 = bf16(bf16(x1 c) - bf16(x2 s)), y2 = bf16(bf16(x1 s) +
+// bf16(x2 c)) (scripts/direct_inference_full.py:58-70, bf16 tensor ops)
+__device__ __forceinline__ void rope_pk(uint32_t x1, uint32_t x2, uint32_t c, uint32_t s, uint32_t& y1, uint32_t& y2) {
+    const f32x2_t a = {bf_lo(x1), bf_hi(x1)}, b = {bf_lo(x2), bf_hi(x2)};
+    const f32x2_t cc = {bf_lo(c), bf_hi(c)}, ss = {bf_lo(s), bf_hi(s)};
+    const f32x2_t ac = a * cc, bs = b * ss, as = a * ss, bc = b * cc;
+    const uint32_t pac = pk_bf16(ac.x, ac.y), pbs = pk_bf16(bs.x, bs.y), pas = pk_bf16(as.x, as.y), pbc = pk_bf16(bc.x, bc.y);
+    const f32x2_t d = f32x2_t{bf_lo(pac), bf_hi(pac)} - f32x2_t{bf_lo(pbs), bf_hi(pbs)};
+    const f32x2_t u = f32x2_t{bf_lo(pas), bf_hi(pas)} + f32x2_t{bf_lo(pbc), bf_hi(pbc)};
+    y1 = pk_bf16(d.x, d.y);
+    y2 = pk_bf16(u.x, u.y);
+}
+
 struct OpAdd {
     template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return a + b; }
 };
