@@ -858,20 +858,30 @@ __global__ __launch_bounds__(NW * 64, 2) void k_dec_gemm_t(GemvArgs a) {  // 2 w
         for (int j = 0; j < TNT; ++j) lw[j] = *reinterpret_cast<const uint2*>(wp[j] + ((int64_t)kb << 9));
     };
     auto mma = [&](const uint4 (&la)[TMT][2], const uint2 (&lw)[TNT]) {
+        // TNT <= 4: both halves of each code pair decoded at once (wf_mfma.h pg_decode_pair); at
+        // TNT = 8 the second half's fragments would not fit beside the accumulators (spills)
+        constexpr int NH = TNT <= 4 ? 2 : 1;
+        v4i_t bf[NH][TNT];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            v4i_t bf[TNT];
+            if constexpr (NH == 2) {
+                if (h == 0)
 #pragma unroll
-            for (int j = 0; j < TNT; ++j) {
-                const uint32_t w = h ? lw[j].y : lw[j].x;
-                bf[j] = v4i_t{(int)((w >> 6) & 0x03030303u), (int)((w >> 4) & 0x03030303u), (int)((w >> 2) & 0x03030303u),
-                              (int)(w & 0x03030303u)};
+                    for (int j = 0; j < TNT; ++j) pg_decode_pair(lw[j], bf[0][j], bf[1][j]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < TNT; ++j) {
+                    const uint32_t w = h ? lw[j].y : lw[j].x;
+                    bf[0][j] = v4i_t{(int)((w >> 6) & 0x03030303u), (int)((w >> 4) & 0x03030303u),
+                                     (int)((w >> 2) & 0x03030303u), (int)(w & 0x03030303u)};
+                }
             }
 #pragma unroll
             for (int i = 0; i < TMT; ++i) {
                 const v4i_t af = __builtin_bit_cast(v4i_t, la[i][h]);
 #pragma unroll
-                for (int j = 0; j < TNT; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[j], acc[i][j], 0, 0, 0);
+                for (int j = 0; j < TNT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[NH == 2 ? h : 0][j], acc[i][j], 0, 0, 0);
             }
         }
     };

@@ -161,6 +161,23 @@ __device__ __forceinline__ void pg_tile_of(int bid, int nbm, int nbn, int& bm, i
     bn = t / rows;
 }
 
+// The B fragments of one I2_S code pair (x: k-half 0, y: k-half 1): quarter q of each 32-bit word is
+// (word >> (6 - 2q)) & 0x03030303. One 64-bit shift of (y:x) serves both words: the bits of y that
+// enter x's top land in bits >= 26, above every kept 2-bit field (3 shifts + 8 ANDs for two
+// fragments instead of 6 + 8). Inline asm: the compiler's demanded-bits pass splits a C++ 64-bit
+// shift back into two 32-bit ones.
+__device__ __forceinline__ void pg_decode_pair(uint2 wp, v4i_t& b0, v4i_t& b1) {
+    const uint64_t w = ((uint64_t)wp.y << 32) | wp.x;
+    uint64_t s6, s4, s2;
+    asm("v_lshrrev_b64 %0, 6, %1" : "=v"(s6) : "v"(w));
+    asm("v_lshrrev_b64 %0, 4, %1" : "=v"(s4) : "v"(w));
+    asm("v_lshrrev_b64 %0, 2, %1" : "=v"(s2) : "v"(w));
+    constexpr uint32_t M = 0x03030303u;
+    b0 = v4i_t{(int)((uint32_t)s6 & M), (int)((uint32_t)s4 & M), (int)((uint32_t)s2 & M), (int)(wp.x & M)};
+    b1 = v4i_t{(int)((uint32_t)(s6 >> 32) & M), (int)((uint32_t)(s4 >> 32) & M), (int)((uint32_t)(s2 >> 32) & M),
+               (int)(wp.y & M)};
+}
+
 // Fragments of one stage for one wave: A row tiles 4 wr + i (both halves), W column tiles TNW wc + j.
 // At TNW = 8 the 128 accumulators leave no room for a second fragment set: each stage reads its
 // own fragments after its barrier (at TNW = 4 they are read one stage ahead).
@@ -243,6 +260,12 @@ __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const 
         uint2 wl[CT];
 #pragma unroll
         for (int j = 0; j < CT; ++j) wl[j] = *reinterpret_cast<const uint2*>(st + 16384 + (CT * wave + j) * 512 + lane * 8);
+        // CT <= 2: both halves decoded at once (pg_decode_pair); at CT = 4 they would spill
+        constexpr int NH = CT <= 2 ? 2 : 1;
+        v4i_t bf[NH][CT];
+        if constexpr (NH == 2)
+#pragma unroll
+            for (int j = 0; j < CT; ++j) pg_decode_pair(wl[j], bf[0][j], bf[1][j]);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             v4i_t fa[8];
@@ -250,12 +273,14 @@ __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const 
             for (int r = 0; r < 8; ++r) fa[r] = *reinterpret_cast<const v4i_t*>(st + r * 2048 + h * 1024 + lane * 16);
 #pragma unroll
             for (int j = 0; j < CT; ++j) {
-                const uint32_t w = h ? wl[j].y : wl[j].x;
-                const v4i_t bf = v4i_t{(int)((w >> 6) & 0x03030303u), (int)((w >> 4) & 0x03030303u),
-                                       (int)((w >> 2) & 0x03030303u), (int)(w & 0x03030303u)};
+                if constexpr (NH == 1) {
+                    const uint32_t w = h ? wl[j].y : wl[j].x;
+                    bf[0][j] = v4i_t{(int)((w >> 6) & 0x03030303u), (int)((w >> 4) & 0x03030303u),
+                                     (int)((w >> 2) & 0x03030303u), (int)(w & 0x03030303u)};
+                }
 #pragma unroll
                 for (int r = 0; r < 8; ++r)
-                    acc[r & 3][(r >> 2) * CT + j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[r], bf, acc[r & 3][(r >> 2) * CT + j], 0, 0, 0);
+                    acc[r & 3][(r >> 2) * CT + j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[r], bf[NH == 2 ? h : 0][j], acc[r & 3][(r >> 2) * CT + j], 0, 0, 0);
             }
         }
     };
@@ -274,33 +299,30 @@ __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const 
             read(fl, kb);
         }
         const PgFrag<TNW>& f = TNW == 4 ? fc : fl;
+#ifdef WF_PG_DEC32  // study: one 32-bit code word decoded per half (3 shifts + 4 ANDs per B fragment)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if constexpr (TNW == 4) {
-                v4i_t bf[TNW];
+        for (int h = 0; h < 2; ++h)
 #pragma unroll
-                for (int j = 0; j < TNW; ++j) {
-                    const uint32_t w = h ? wl[j].y : wl[j].x;
-                    bf[j] = v4i_t{(int)((w >> 6) & 0x03030303u), (int)((w >> 4) & 0x03030303u),
-                                  (int)((w >> 2) & 0x03030303u), (int)(w & 0x03030303u)};
-                }
+            for (int j = 0; j < TNW; ++j) {
+                const uint32_t w = h ? wl[j].y : wl[j].x;
+                const v4i_t bf = v4i_t{(int)((w >> 6) & 0x03030303u), (int)((w >> 4) & 0x03030303u),
+                                       (int)((w >> 2) & 0x03030303u), (int)(w & 0x03030303u)};
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < TNW; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[h][i], bf[j], acc[i][j], 0, 0, 0);
-            } else {  // one column tile's decoded B fragment live at a time (register budget)
-#pragma unroll
-                for (int j = 0; j < TNW; ++j) {
-                    const uint32_t w = h ? wl[j].y : wl[j].x;
-                    const v4i_t bf = v4i_t{(int)((w >> 6) & 0x03030303u), (int)((w >> 4) & 0x03030303u),
-                                           (int)((w >> 2) & 0x03030303u), (int)(w & 0x03030303u)};
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[h][i], bf, acc[i][j], 0, 0, 0);
-                }
+                    acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[h][i], bf, acc[i][j], 0, 0, 0);
             }
+#else
+        // a column tile's two halves decoded together (pg_decode_pair), then its 8 MFMAs
+#pragma unroll
+        for (int j = 0; j < TNW; ++j) {
+            v4i_t b0, b1;
+            pg_decode_pair(wl[j], b0, b1);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[0][i], b0, acc[i][j], 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[1][i], b1, acc[i][j], 0, 0, 0);
         }
+#endif
     };
     // one iteration: stage c + 1 published and read into `nxt`, stage c computed from `cur`
 #ifdef WF_STAMPS
