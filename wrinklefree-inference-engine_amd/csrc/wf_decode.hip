@@ -1637,8 +1637,12 @@ __global__ __launch_bounds__(kNT) void k_rownorm(const uint16_t* __restrict__ x,
 // 16-byte slot, its 4 dwords gathered by conflict-free ds_read_b32), so every line of the code
 // tensor is written by one block of one XCD (the former 4-rows-per-block kernel split each line
 // over four blocks' 4-byte stores: 76 us at K 2560, 98 us at K 6912 for 16384 rows).
-template <int NP>
-__global__ __launch_bounds__(512) void k_rownorm_tile8(const uint16_t* __restrict__ x, int64_t xs,
+// FULL: the launcher saw K / 8 > 64 (NP - 1), so pieces j < NP - 1 exist for every lane (no per-piece
+// bound checks; only the last piece is checked).
+// Two blocks per CU (4 waves per SIMD, <= 128 VGPRs) up to K 7168, as the LDS allows; unbounded,
+// hipcc gave a FULL K-6912 form 146 VGPRs, so one block per CU (72 -> 102 us).
+template <int NP, bool FULL = false>
+__global__ __launch_bounds__(512, NP <= 14 ? 4 : 1) void k_rownorm_tile8(const uint16_t* __restrict__ x, int64_t xs,
                                                        const uint16_t* __restrict__ nw, int K, float eps,
                                                        int8_t* __restrict__ q8, float* __restrict__ sf,
                                                        int* __restrict__ asum_out) {
@@ -1660,7 +1664,7 @@ __global__ __launch_bounds__(512) void k_rownorm_tile8(const uint16_t* __restric
     float ss[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-        const bool valid = 64 * j + lane < npk;
+        const bool valid = (FULL && j < NP - 1) || 64 * j + lane < npk;
         const uint32_t w4[4] = {xv[j].x, xv[j].y, xv[j].z, xv[j].w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1673,13 +1677,13 @@ __global__ __launch_bounds__(512) void k_rownorm_tile8(const uint16_t* __restric
     for (int j = 0; j < NP; ++j) reg_fence(xv[j]);  // pass 2 unpacks again (no 8 NP floats kept live)
     float W[8];
 #pragma unroll
-    for (int v = 0; v < 8; ++v) W[v] = wave_sum(ss[v]);
+    for (int v = 0; v < 8; ++v) W[v] = v < NP ? wave_sum(ss[v]) : 0.f;  // chains >= NP are +0
     __syncthreads();  // s_nw complete
     const float rr = rms_factor(div_rn(tree_sum<8>(W), (float)K, 1.0f / (float)K) + eps);
     float m = 0.f;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {  // xv[j] <- the normalised row, packed bf16 (0 past the row)
-        const bool valid = 64 * j + lane < npk;
+        const bool valid = (FULL && j < NP - 1) || 64 * j + lane < npk;
         const uint4 wv = reinterpret_cast<const uint4*>(s_nw)[min(64 * j + lane, npk - 1)];
         const uint32_t w4[4] = {xv[j].x, xv[j].y, xv[j].z, xv[j].w}, n4[4] = {wv.x, wv.y, wv.z, wv.w};
         uint32_t o4[4];
@@ -1701,10 +1705,7 @@ __global__ __launch_bounds__(512) void k_rownorm_tile8(const uint16_t* __restric
     int as = 0;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-        const uint32_t w4[4] = {xv[j].x, xv[j].y, xv[j].z, xv[j].w};
-        const float y[8] = {bf_lo(w4[0]), bf_hi(w4[0]), bf_lo(w4[1]), bf_hi(w4[1]),
-                            bf_lo(w4[2]), bf_hi(w4[2]), bf_lo(w4[3]), bf_hi(w4[3])};
-        const uint2 c = quant8(y, s, inv, as);
+        const uint2 c = quant8_bf16x8(xv[j], s, inv, as);
         const int p = 64 * j + lane;
         if (p < npk) *reinterpret_cast<uint2*>(s_codes + wave * KS + 8 * p) = c;
     }
@@ -1720,9 +1721,10 @@ __global__ __launch_bounds__(512) void k_rownorm_tile8(const uint16_t* __restric
     for (int pr = threadIdx.x >> 5; pr < 2 * nkb; pr += 16) {
         const int kb = pr >> 1, h = pr & 1;
         const int8_t* src = s_codes + r8 * KS + 128 * kb + 16 * h + 4 * qq;
-        const uint4 v = make_uint4(*reinterpret_cast<const uint32_t*>(src), *reinterpret_cast<const uint32_t*>(src + 32),
-                                   *reinterpret_cast<const uint32_t*>(src + 64), *reinterpret_cast<const uint32_t*>(src + 96));
-        *reinterpret_cast<uint4*>(q8 + ((((int64_t)rt * nkb + kb) * 2 + h) << 10) + (((r8 + 8 * half8) + 16 * qq) << 4)) = v;
+        // u32x4 (not uint4, a struct the compiler stored as four dword stores): one dwordx4 per lane
+        const u32x4 v = {*reinterpret_cast<const uint32_t*>(src), *reinterpret_cast<const uint32_t*>(src + 32),
+                         *reinterpret_cast<const uint32_t*>(src + 64), *reinterpret_cast<const uint32_t*>(src + 96)};
+        *reinterpret_cast<u32x4*>(q8 + ((((int64_t)rt * nkb + kb) * 2 + h) << 10) + (((r8 + 8 * half8) + 16 * qq) << 4)) = v;
     }
 }
 
@@ -2708,18 +2710,20 @@ static void prefill_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, co
     const dim3 grid(rows / 8);
     const size_t lds = 2 * (size_t)K + 8 * (size_t)(K + 16);
     const int np = (K / 8 + 63) / 64;
-#define WF_RN8(NPV) \
-    hipLaunchKernelGGL((k_rownorm_tile8<NPV>), grid, dim3(512), lds, st, x, xs, nw, K, m->d.eps, m->pf_q8, m->pf_sf, m->pf_asum)
-    if (np <= 5) {
-        WF_RN8(5);
-    } else if (np <= 14) {
-        WF_RN8(14);
+#define WF_RN8(NPV, FV) \
+    hipLaunchKernelGGL((k_rownorm_tile8<NPV, FV>), grid, dim3(512), lds, st, x, xs, nw, K, m->d.eps, m->pf_q8, m->pf_sf, m->pf_asum)
+    if (np == 5) {  // the 2B-4T hidden width (2560)
+        WF_RN8(5, true);
+    } else if (np < 5) {
+        WF_RN8(5, false);
+    } else if (np <= 14) {  // incl. the FFN width 6912 (FULL there: 128 VGPRs + a spill, measured slower)
+        WF_RN8(14, false);
     } else {  // K up to 8192: 2 K + 8 (K + 16) bytes of LDS pass 64 KiB
         static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rownorm_tile8<16>),
                                                            hipFuncAttributeMaxDynamicSharedMemorySize,
                                                            2 * 8192 + 8 * (8192 + 16));
         (void)attr;
-        WF_RN8(16);
+        WF_RN8(16, false);
     }
 #undef WF_RN8
 }

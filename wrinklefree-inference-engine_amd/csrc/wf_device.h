@@ -261,6 +261,27 @@ __device__ __forceinline__ uint2 quant8(const float (&x)[8], float sf, float inv
     return make_uint2(lo, hi);
 }
 
+// quant8 of eight packed bf16 values on fp32 pairs: v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32
+// round each lane exactly as the scalar ops do, so the codes and the sum are quant8's.
+__device__ __forceinline__ uint2 quant8_bf16x8(uint4 v, float sf, float inv, int& asum) {
+    const f32x2_t S = {sf, sf}, I = {inv, inv}, G = {12582912.0f, 12582912.0f};
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t b[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const f32x2_t x = {bf_lo(w[e]), bf_hi(w[e])};
+        const f32x2_t q = x * I;
+        const f32x2_t r = __builtin_elementwise_fma(-q, S, x);
+        const f32x2_t d = __builtin_elementwise_fma(r, I, q) + G;
+        b[2 * e] = __float_as_uint(d.x);
+        b[2 * e + 1] = __float_as_uint(d.y);
+    }
+    const uint32_t lo = __builtin_amdgcn_perm(b[1], b[0], 0x0c0c0400u) | __builtin_amdgcn_perm(b[3], b[2], 0x04000c0cu);
+    const uint32_t hi = __builtin_amdgcn_perm(b[5], b[4], 0x0c0c0400u) | __builtin_amdgcn_perm(b[7], b[6], 0x04000c0cu);
+    asum = sdot4_ones(lo, sdot4_ones(hi, asum));
+    return make_uint2(lo, hi);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Packed-weight formats and their LDS activation images.
 //
