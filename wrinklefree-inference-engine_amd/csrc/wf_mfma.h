@@ -181,10 +181,16 @@ __device__ __forceinline__ void pg_decode_pair(uint2 wp, v4i_t& b0, v4i_t& b1) {
 // Fragments of one stage for one wave: A row tiles 4 wr + i (both halves), W column tiles TNW wc + j.
 // At TNW = 8 the 128 accumulators leave no room for a second fragment set: each stage reads its
 // own fragments after its barrier (at TNW = 4 they are read one stage ahead).
+#ifndef WF_PG_AHEAD8  // study switch: 1 = TNW 8 also reads its fragments one stage ahead (254 VGPRs
+#define WF_PG_AHEAD8 0  // once the paired decode freed registers): gate|up 526 -> 525 us, not kept
+#endif
+// Fragments read one stage ahead (below): TNW = 4
+template <int TNW>
+constexpr bool pg_ahead() { return TNW == 4 || WF_PG_AHEAD8; }
 template <int TNW>
 struct PgFrag {
     v4i_t a[2][4];
-    uint2 w[TNW == 4 ? TNW : 1];
+    uint2 w[pg_ahead<TNW>() ? TNW : 1];
 };
 
 // The fragments of stage c are read from LDS one iteration ahead (while the MFMAs of stage c - 1
@@ -243,7 +249,7 @@ __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const 
     };
     auto read = [&](PgFrag<TNW>& f, int kb) {
         const uint8_t* st = lds + (kb % P) * SB;
-        if constexpr (TNW == 4) read_w(f.w, kb);
+        if constexpr (pg_ahead<TNW>()) read_w(f.w, kb);
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -290,15 +296,15 @@ __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const 
             return;
         }
         uint2 wl[TNW];
-        PgFrag<TNW> fl;  // TNW = 8: this stage's A fragments, read here (no second set in registers)
-        if constexpr (TNW == 4) {
+        PgFrag<TNW> fl;  // !pg_ahead: this stage's A fragments, read here (no second set in registers)
+        if constexpr (pg_ahead<TNW>()) {
 #pragma unroll
             for (int j = 0; j < TNW; ++j) wl[j] = fc.w[j];
         } else {
             read_w(wl, kb);
             read(fl, kb);
         }
-        const PgFrag<TNW>& f = TNW == 4 ? fc : fl;
+        const PgFrag<TNW>& f = pg_ahead<TNW>() ? fc : fl;
 #ifdef WF_PG_DEC32  // study: one 32-bit code word decoded per half (3 shifts + 4 ANDs per B fragment)
 #pragma unroll
         for (int h = 0; h < 2; ++h)
@@ -342,7 +348,7 @@ __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const 
 #if !defined(WF_PG_STUDY) || WF_PG_STUDY != 1  // diagnostic build 1: no ring refills
             if (c + P - 1 < nkb) issue(c + P - 1);
 #endif
-            if constexpr (TNW == 4 && !CW) read(nxt, c + 1);
+            if constexpr (pg_ahead<TNW>() && !CW) read(nxt, c + 1);
         }
         WF_PG_STAMP(4);
         mma(cur, c);
@@ -358,7 +364,7 @@ __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const 
     if (P - 2 < nkb) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA * (P - 2)) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if constexpr (TNW == 4 && !CW) read(f0, 0);
+    if constexpr (pg_ahead<TNW>() && !CW) read(f0, 0);
     int c = 0;
     for (; c + 1 < nkb; c += 2) {
         step(c, f0, f1);
