@@ -1272,22 +1272,12 @@ __device__ __forceinline__ void pf_tile_epilogue(const GemvArgs& g, int bm, int 
 // Prefill GEMM (rows = prompt tokens) on the tile layouts with the decode step's fused epilogues:
 // the wf_mfma.h 128 x 256 tile main loop (pgemm_tile), then EpiDec<MODE> per 16 x 16 fragment
 // (correction, RoPE + K/V cache write through row_slot, residual, ReLU^2 * up).
-template <int MODE, int TNW = 4, int ALG = 0, bool STAGED = false>
-__global__ __launch_bounds__(512) void k_pgemm_fused(GemvArgs a, int nbm, int nbn) {
-    static_assert(MODE != MODE_QKV || TNW == 4, "the q|k|v epilogue stages 256 columns (two heads)");
+// Per-fragment epilogue of a prefill GEMM tile (gate|up, or any mode without the staged tile)
+template <int MODE, int TNW, bool CW>
+__device__ __forceinline__ void pf_frag_epilogue(const GemvArgs& a, int bm, int bn, v4i_t (&acc)[4][TNW]) {
     constexpr int BC = pg_block_cols<TNW>();
-    __shared__ __attribute__((aligned(16))) uint8_t lds[PgCfg<TNW, ALG>::LDS];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
-    constexpr bool CW = PgCfg<TNW, ALG>::CW;
-    int bm, bn;
-    pg_tile_of(blockIdx.x, nbm, nbn, bm, bn);
-    v4i_t acc[4][TNW];
-    pg_main<TNW, ALG>(a.w, a.q8, a.B, a.N, a.K, bm, bn, lds, acc);
-    if constexpr (MODE == MODE_QKV) {
-        pf_qkv_epilogue<CW>(a, bm, bn, acc, lds);
-    } else if constexpr (STAGED) {
-        pf_tile_epilogue<MODE, TNW, CW>(a, bm, bn, acc, lds);
-    } else {
+    (void)lane;
     if constexpr (MODE == MODE_GU && !CW && TNW % 2 == 0) {
         // gate|up, 16-byte stores: fragments j, j + 1 hold act columns 8 T .. 8 T + 15 of the same
         // rows (T = their first 16-column tile, even). After gu_pack lane quad 0 has columns 0-3 and
@@ -1334,6 +1324,58 @@ __global__ __launch_bounds__(512) void k_pgemm_fused(GemvArgs a, int nbm, int nb
             e.apply(bm * 128 + pg_frag_rt<TNW, CW>(wave, i, j) * 16, bn * BC + pg_frag_ct<TNW, CW>(wave, i, j) * 16, acc[i][j], l16,
                     q, in[j]);
     }
+}
+
+// Prefill GEMM (rows = prompt tokens) on the tile layouts with the decode step's fused epilogues:
+// the wf_mfma.h 128 x 256 tile main loop (pgemm_tile), then EpiDec<MODE> per 16 x 16 fragment
+// (correction, RoPE + K/V cache write through row_slot, residual, ReLU^2 * up).
+template <int MODE, int TNW = 4, int ALG = 0, bool STAGED = false>
+__global__ __launch_bounds__(512) void k_pgemm_fused(GemvArgs a, int nbm, int nbn) {
+    static_assert(MODE != MODE_QKV || TNW == 4, "the q|k|v epilogue stages 256 columns (two heads)");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[PgCfg<TNW, ALG>::LDS];
+    constexpr bool CW = PgCfg<TNW, ALG>::CW;
+    int bm, bn;
+    pg_tile_of(blockIdx.x, nbm, nbn, bm, bn);
+    v4i_t acc[4][TNW];
+    pg_main<TNW, ALG>(a.w, a.q8, a.B, a.N, a.K, bm, bn, lds, acc);
+    if constexpr (MODE == MODE_QKV) {
+        pf_qkv_epilogue<CW>(a, bm, bn, acc, lds);
+    } else if constexpr (STAGED) {
+        pf_tile_epilogue<MODE, TNW, CW>(a, bm, bn, acc, lds);
+    } else {
+        pf_frag_epilogue<MODE, TNW, CW>(a, bm, bn, acc);
+    }
+}
+
+// The same GEMM as a persistent tile loop (per-fragment epilogues only: the staged epilogues use the
+// ring's LDS): one block per CU takes tiles blockIdx.x + i gridDim.x (gridDim.x % 8 == 0 keeps every
+// tile on the XCD pg_tile_of gives it), and the next tile's first P - 1 ring stages are issued before
+// this tile's epilogue, so their HBM / L2 latency overlaps the epilogue's VALU and stores instead of
+// following them (one-shot blocks pay it after the previous block on the CU has exited).
+template <int MODE, int TNW>
+__global__ __launch_bounds__(512) void k_pgemm_fused_pt(GemvArgs a, int nbm, int nbn) {
+    constexpr int P = PgCfg<TNW, 0>::P;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[PgCfg<TNW, 0>::LDS];
+    const int nt = nbm * nbn;
+    int t = blockIdx.x, bm, bn;
+    if (t >= nt) return;  // whole block
+    pg_tile_of(t, nbm, nbn, bm, bn);
+    PgDma<P, TNW>(a.w, a.q8, a.B, a.N, a.K, bm, bn).prologue(lds, a.K);
+    for (;;) {
+        v4i_t acc[4][TNW];
+        pg_main<TNW, 0, true>(a.w, a.q8, a.B, a.N, a.K, bm, bn, lds, acc);
+        const int tn = t + (int)gridDim.x;
+        int bm2 = 0, bn2 = 0;
+        __builtin_amdgcn_s_barrier();  // every wave's last fragment reads are done: the ring is free
+        if (tn < nt) {
+            pg_tile_of(tn, nbm, nbn, bm2, bn2);
+            PgDma<P, TNW>(a.w, a.q8, a.B, a.N, a.K, bm2, bn2).prologue(lds, a.K);
+        }
+        pf_frag_epilogue<MODE, TNW, false>(a, bm, bn, acc);
+        if (tn >= nt) break;
+        t = tn;
+        bm = bm2;
+        bn = bn2;
     }
 }
 
@@ -2736,10 +2778,25 @@ static bool pf_staged_ok(const GemvArgs& a, bool wide) {
                     (!a.resid || reinterpret_cast<uintptr_t>(a.resid) % 16 == 0);
     return !wide && al;
 }
+#ifndef WF_PG_PERSIST  // 0 = one-shot gate|up blocks (one tile each): same time, bit-identical
+#define WF_PG_PERSIST 1  // (ab_prefill_persist_r04.txt)
+#endif
+constexpr bool kPgPersist = WF_PG_PERSIST;
+[[maybe_unused]] static int pg_cu_count() {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    return n;
+}
 template <int MODE, int TNW, int ALG>
 static void pg_launch(const GemvArgs& a, int nbm, int nbn, hipStream_t st) {
     // (the 512-column o / down tile of a wide model does not fit the staged tile into the ring)
     constexpr bool kStaged = MODE != MODE_QKV && pf_tile_epilogue_bytes<MODE, TNW>() <= PgCfg<TNW, ALG>::LDS;
+    if constexpr (kPgPersist && MODE == MODE_GU && TNW == 8 && ALG == 0) {  // gate|up: persistent tile loop
+        const int nt = nbm * nbn, ncu = pg_cu_count() / 8 * 8;
+        hipLaunchKernelGGL((k_pgemm_fused_pt<MODE, TNW>), dim3(ncu >= 8 ? min(nt, ncu) : nt), dim3(512), 0, st, a, nbm, nbn);
+        return;
+    }
     if (kStaged && pf_staged_ok(a, TNW == 8))
         hipLaunchKernelGGL((k_pgemm_fused<MODE, TNW, ALG, kStaged>), dim3(nbm * nbn), dim3(512), 0, st, a, nbm, nbn);
     else

@@ -216,7 +216,46 @@ __device__ __forceinline__ int pg_frag_ct(int wave, int i, int j) {
     return CW ? (TNW / 2) * wave + j % (TNW / 2) : TNW * (wave & 3) + j;
 }
 
-template <int P, int TNW = 4, bool CW = false>
+// LDS-DMA sources of one 128 x (64 TNW) tile and its stage issue (3 or 4 DMAs per wave per stage)
+template <int P, int TNW>
+struct PgDma {
+    static constexpr int SB = pg_stage_bytes<TNW>();
+    const int8_t* asrc;
+    const uint8_t* wsrc[TNW / 4];
+    // A row tile 8 bm + wave (both halves); W column tiles 4 TNW bn + (TNW / 2) wave + 2 u + (lane >=
+    // 32), u < TNW / 4 (two 512-byte column tiles per KiB piece)
+    __device__ __forceinline__ PgDma(const uint8_t* __restrict__ W, const int8_t* __restrict__ A, int M, int N, int K,
+                                     int bm, int bn) {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        const int nkb = K >> 7, nrt = (M + 15) >> 4, nct = N >> 4;
+        const int rt = min(bm * 8 + wave, nrt - 1);
+        asrc = A + ((int64_t)rt * nkb << 11) + lane * 16;
+#pragma unroll
+        for (int u = 0; u < TNW / 4; ++u) {
+            const int ct = min(bn * 4 * TNW + (TNW / 2) * wave + 2 * u + (lane >> 5), nct - 1);
+            wsrc[u] = W + ((int64_t)ct * nkb << 9) + (lane & 31) * 16;
+        }
+    }
+    __device__ __forceinline__ void issue(uint8_t* lds, int kb) const {
+        const int wave = threadIdx.x >> 6;
+        uint8_t* st = lds + (kb % P) * SB;
+        glds16_asm(asrc + ((int64_t)kb << 11), st + wave * 2048);
+        glds16_asm(asrc + ((int64_t)kb << 11) + 1024, st + wave * 2048 + 1024);
+#pragma unroll
+        for (int u = 0; u < TNW / 4; ++u) glds16_asm(wsrc[u] + ((int64_t)kb << 9), st + 16384 + ((TNW / 4) * wave + u) * 1024);
+    }
+    // the ring's first P - 1 stages (pgemm_tile<.., PRE = true> expects them issued)
+    __device__ __forceinline__ void prologue(uint8_t* lds, int K) const {
+#pragma unroll
+        for (int c = 0; c < P - 1; ++c)
+            if (c < (K >> 7)) issue(lds, c);
+    }
+};
+
+// PRE: the caller issued the ring's first P - 1 stages (PgDma::prologue) before other vector-memory
+// work of its own (a persistent block's previous epilogue: loads and stores count in the same
+// vmcnt), so the first wait drains everything (vmcnt(0)) instead of counting.
+template <int P, int TNW = 4, bool CW = false, bool PRE = false>
 __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const int8_t* __restrict__ A, int M, int N,
                                            int K, int bm, int bn, uint8_t* lds, v4i_t (&acc)[4][TNW]) {
     static_assert(P >= 4, "two stages in flight beyond the one being read");
@@ -224,24 +263,9 @@ __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const 
     constexpr int SB = pg_stage_bytes<TNW>(), NDMA = 2 + TNW / 4;  // DMAs per wave per stage
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wr = wave >> 2, wc = wave & 3;
-    const int nkb = K >> 7, nrt = (M + 15) >> 4, nct = N >> 4;
-    // DMA sources: A row tile 8 bm + wave (both halves); W column tiles 4 TNW bn + (TNW / 2) wave
-    // + 2 u + (lane >= 32), u < TNW / 4 (two 512-byte column tiles per KiB piece)
-    const int rt = min(bm * 8 + wave, nrt - 1);
-    const int8_t* asrc = A + ((int64_t)rt * nkb << 11) + lane * 16;
-    const uint8_t* wsrc[TNW / 4];
-#pragma unroll
-    for (int u = 0; u < TNW / 4; ++u) {
-        const int ct = min(bn * 4 * TNW + (TNW / 2) * wave + 2 * u + (lane >> 5), nct - 1);
-        wsrc[u] = W + ((int64_t)ct * nkb << 9) + (lane & 31) * 16;
-    }
-    auto issue = [&](int kb) {
-        uint8_t* st = lds + (kb % P) * SB;
-        glds16_asm(asrc + ((int64_t)kb << 11), st + wave * 2048);
-        glds16_asm(asrc + ((int64_t)kb << 11) + 1024, st + wave * 2048 + 1024);
-#pragma unroll
-        for (int u = 0; u < TNW / 4; ++u) glds16_asm(wsrc[u] + ((int64_t)kb << 9), st + 16384 + ((TNW / 4) * wave + u) * 1024);
-    };
+    const int nkb = K >> 7;
+    const PgDma<P, TNW> dma(W, A, M, N, K, bm, bn);
+    auto issue = [&](int kb) { dma.issue(lds, kb); };
     auto read_w = [&](uint2 (&w)[TNW], int kb) {
         const uint8_t* st = lds + (kb % P) * SB;
 #pragma unroll
@@ -357,11 +381,12 @@ __device__ __forceinline__ void pgemm_tile(const uint8_t* __restrict__ W, const 
 #if defined(WF_PG_STUDY) && WF_PG_STUDY == 5  // diagnostic build 5: no main loop (epilogue cost)
     return;
 #endif
+    if constexpr (!PRE)
 #pragma unroll
-    for (int c = 0; c < P - 1; ++c)
-        if (c < nkb) issue(c);
+        for (int c = 0; c < P - 1; ++c)
+            if (c < nkb) issue(c);
     PgFrag<TNW> f0, f1;
-    if (P - 2 < nkb) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA * (P - 2)) : "memory");
+    if (!PRE && P - 2 < nkb) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA * (P - 2)) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if constexpr (pg_ahead<TNW>() && !CW) read(f0, 0);
@@ -390,9 +415,9 @@ struct PgCfg {
     static constexpr int LDS = P * SB;
     static constexpr bool CW = ALG == 3;  // fragment -> tile mapping: pg_frag_rt / pg_frag_ct
 };
-template <int TNW, int ALG>
+template <int TNW, int ALG, bool PRE = false>
 __device__ __forceinline__ void pg_main(const uint8_t* __restrict__ W, const int8_t* __restrict__ A, int M, int N,
                                         int K, int bm, int bn, uint8_t* lds, v4i_t (&acc)[4][TNW]) {
-    pgemm_tile<PgCfg<TNW, ALG>::P, TNW, PgCfg<TNW, ALG>::CW>(W, A, M, N, K, bm, bn, lds, acc);
+    pgemm_tile<PgCfg<TNW, ALG>::P, TNW, PgCfg<TNW, ALG>::CW, PRE>(W, A, M, N, K, bm, bn, lds, acc);
 }
 }  // namespace wf
