@@ -7,7 +7,7 @@ O=gpurun_out/r4ab
 mkdir -p "$O"
 export TMPDIR=/tmp
 if [ -n "${TESTS:-}" ]; then
-  timeout -k 10 900 python -u -m pytest -q -x --timeout 400 --timeout-method thread -p no:cacheprovider $TESTS > "$O/pytest.log" 2>&1
+  eval "timeout -k 10 900 python -u -m pytest -q -x --timeout 400 --timeout-method thread -p no:cacheprovider $TESTS" > "$O/pytest.log" 2>&1
   rc=$?; tail -4 "$O/pytest.log"; [ $rc -eq 0 ] || exit $rc
 fi
 L=$(pwd)/wrinklefree-inference-engine_amd/lib

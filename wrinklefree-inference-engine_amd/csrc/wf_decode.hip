@@ -2157,6 +2157,9 @@ struct wf_model {
 };
 
 using namespace wf;
+// (defined with the prefill launches below; the batched decode's row norm uses it too)
+static void rownorm_tile8_launch(const uint16_t* x, int64_t xs, const uint16_t* nw, int K, int rows, float eps,
+                                 int8_t* q8, float* sf, int* asum, hipStream_t st);
 
 namespace {
 
@@ -2286,6 +2289,9 @@ int launch_gemv_fmt(int fmt, const GemvArgs& ga, hipStream_t st, int pro = 0) {
     return launch_gemv<FmtI2S, MODE, LPR>(ga, st);
 }
 
+#ifndef WF_DEC_TILE8  // study: 1 = batch >= 16 GEMM inputs through the prefill row norm k_rownorm_tile8
+#define WF_DEC_TILE8 0  // (bit-identical; 16 blocks at batch 128: 35.0k -> 32.3k tok/s, ab_dec_tile8_r04.txt)
+#endif
 // rows of x [B, xs] -> int8 codes in m->q8 (batch > 1), or bf16 into y16 (final norm)
 void launch_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, const uint16_t* nw, int K, uint16_t* y16,
                     hipStream_t st) {
@@ -2304,7 +2310,9 @@ void launch_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, const uint
             else WF_RN(1, true, false);
         }
     } else if (tl) {
-        if (big) WF_RN(2, false, true);
+        // (study: the prefill row norm, one wave per row, whole 128-byte code lines)
+        if (WF_DEC_TILE8 && d.batch % 16 == 0) rownorm_tile8_launch(x, xs, nw, K, d.batch, d.eps, m->q8, m->act_sf, m->act_sum, st);
+        else if (big) WF_RN(2, false, true);
         else WF_RN(1, false, true);
     } else {
         if (big) WF_RN(2, false, false);
@@ -2746,14 +2754,14 @@ int wf_model_prefill_reserve(wf_model* m, int rows) {
 }
 
 extern "C++" {
-static void prefill_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, const uint16_t* nw, int K, int rows,
-                            hipStream_t st) {
-    // rows % 16 == 0 (wf_model_prefill); 8 rows per block
+// k_rownorm_tile8 over `rows` rows (rows % 16 == 0) into the tile-layout codes q8 + sf / asum
+static void rownorm_tile8_launch(const uint16_t* x, int64_t xs, const uint16_t* nw, int K, int rows, float eps,
+                                 int8_t* q8, float* sf, int* asum, hipStream_t st) {
     const dim3 grid(rows / 8);
     const size_t lds = 2 * (size_t)K + 8 * (size_t)(K + 16);
     const int np = (K / 8 + 63) / 64;
 #define WF_RN8(NPV, FV) \
-    hipLaunchKernelGGL((k_rownorm_tile8<NPV, FV>), grid, dim3(512), lds, st, x, xs, nw, K, m->d.eps, m->pf_q8, m->pf_sf, m->pf_asum)
+    hipLaunchKernelGGL((k_rownorm_tile8<NPV, FV>), grid, dim3(512), lds, st, x, xs, nw, K, eps, q8, sf, asum)
     if (np == 5) {  // the 2B-4T hidden width (2560)
         WF_RN8(5, true);
     } else if (np < 5) {
@@ -2768,6 +2776,11 @@ static void prefill_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, co
         WF_RN8(16, false);
     }
 #undef WF_RN8
+}
+static void prefill_rownorm(const wf_model* m, const uint16_t* x, int64_t xs, const uint16_t* nw, int K, int rows,
+                            hipStream_t st) {
+    // rows % 16 == 0 (wf_model_prefill); 8 rows per block
+    rownorm_tile8_launch(x, xs, nw, K, rows, m->d.eps, m->pf_q8, m->pf_sf, m->pf_asum, st);
 }
 
 // LDS-staged row-tile epilogue (pf_tile_epilogue) where the output rows are 16-byte pieces: o / down
