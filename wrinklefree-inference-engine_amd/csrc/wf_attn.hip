@@ -623,11 +623,15 @@ __device__ __forceinline__ uint4 i8x8_to_bf16(uint2 r) {
     return make_uint4(i8x2_to_bf16(x, 0), i8x2_to_bf16(x, 16), i8x2_to_bf16(y, 0), i8x2_to_bf16(y, 16));
 }
 // KVQ: K/V cache element type -- 0 bf16, 1 OCP e4m3fn, 2 int8 (include/wf_bitnet.h WF_KV_*)
+#ifndef WF_KV_NT  // K/V fragment loads of the batched attention with the non-temporal hint
+#define WF_KV_NT 1
+#endif
 template <int KVQ>
 struct KvFrag {
     using T = uint4;  // 8 bf16
     __device__ static __forceinline__ T ld(const uint16_t* base, int64_t elem) {
-        return *reinterpret_cast<const uint4*>(base + elem);
+        if constexpr (WF_KV_NT) return ldg_nt(reinterpret_cast<const uint8_t*>(base + elem));
+        else return *reinterpret_cast<const uint4*>(base + elem);
     }
     __device__ static __forceinline__ uint4 bf(const T& t) { return t; }
     // zero the keys >= lim of a V fragment (8 keys)
