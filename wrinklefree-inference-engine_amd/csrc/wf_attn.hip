@@ -340,6 +340,17 @@ constexpr int kApUShort = WF_AP_U, kApULong = WF_AP_U;
 #else
 constexpr int kApUShort = 10, kApULong = 8;
 #endif
+#ifndef WF_KV_NT  // decode-attention K/V loads with the non-temporal hint (each byte is read once per step)
+#define WF_KV_NT 1
+#endif
+__device__ __forceinline__ uint4 kv_ld16(const uint16_t* p) {
+    if constexpr (WF_KV_NT) return ldg_nt(reinterpret_cast<const uint8_t*>(p));
+    else return *reinterpret_cast<const uint4*>(p);
+}
+#ifndef WF_KV_NT_B1  // study: 1 = the hint in the batch < 16 attention too (5.8 -> 6.4 us there: not kept)
+#define WF_KV_NT_B1 0
+#endif
+
 template <int G, int NS, int U>
 __device__ __forceinline__ void attn_part_body(const uint16_t* __restrict__ q, int64_t q_sb, const uint16_t* __restrict__ K,
                                                const uint16_t* __restrict__ V, int64_t kv_sb, int64_t kv_sh, int Hq,
@@ -377,8 +388,8 @@ __device__ __forceinline__ void attn_part_body(const uint16_t* __restrict__ q, i
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int t = min(c0 + gid + NG * u, t1 - 1);
-                kr[u] = *reinterpret_cast<const uint4*>(K + kvb + (int64_t)t * D);
-                vr[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)t * D);
+                kr[u] = WF_KV_NT_B1 ? kv_ld16(K + kvb + (int64_t)t * D) : *reinterpret_cast<const uint4*>(K + kvb + (int64_t)t * D);
+                vr[u] = WF_KV_NT_B1 ? kv_ld16(V + kvb + (int64_t)t * D) : *reinterpret_cast<const uint4*>(V + kvb + (int64_t)t * D);
             }
         };
         uint4 qv[G];  // bf16 pairs
@@ -623,16 +634,10 @@ __device__ __forceinline__ uint4 i8x8_to_bf16(uint2 r) {
     return make_uint4(i8x2_to_bf16(x, 0), i8x2_to_bf16(x, 16), i8x2_to_bf16(y, 0), i8x2_to_bf16(y, 16));
 }
 // KVQ: K/V cache element type -- 0 bf16, 1 OCP e4m3fn, 2 int8 (include/wf_bitnet.h WF_KV_*)
-#ifndef WF_KV_NT  // K/V fragment loads of the batched attention with the non-temporal hint
-#define WF_KV_NT 1
-#endif
 template <int KVQ>
 struct KvFrag {
     using T = uint4;  // 8 bf16
-    __device__ static __forceinline__ T ld(const uint16_t* base, int64_t elem) {
-        if constexpr (WF_KV_NT) return ldg_nt(reinterpret_cast<const uint8_t*>(base + elem));
-        else return *reinterpret_cast<const uint4*>(base + elem);
-    }
+    __device__ static __forceinline__ T ld(const uint16_t* base, int64_t elem) { return kv_ld16(base + elem); }
     __device__ static __forceinline__ uint4 bf(const T& t) { return t; }
     // zero the keys >= lim of a V fragment (8 keys)
     __device__ static __forceinline__ T mask(const T& t, int lim) {
@@ -647,7 +652,14 @@ template <int KVQ>
 struct KvFrag8 {
     using T = uint2;  // 8 one-byte codes
     __device__ static __forceinline__ T ld(const uint16_t* base, int64_t elem) {
-        return *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(base) + elem);
+        const uint2* p = reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(base) + elem);
+        if constexpr (WF_KV_NT) {
+            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
+            return make_uint2(v.x, v.y);
+        } else {
+            return *p;
+        }
     }
     __device__ static __forceinline__ uint4 bf(const T& t) {
         if constexpr (KVQ == 2) return i8x8_to_bf16(t);

@@ -818,6 +818,9 @@ __device__ __forceinline__ void dec_row_prologue(const GemvArgs& a, int r, float
     }
 }
 
+#ifndef WF_DG_WNT  // study: batched decode GEMM weight loads non-temporal, 1 for o / down, 2 for all
+#define WF_DG_WNT 0  // (all: gate|up 15.8 -> 17.1 us; o / down alone: no change; ab_kv_nt_r04.txt)
+#endif
 template <int TMT, int TNT, int NB, int MODE, int NW = kDgWaves, int PRO = 0, int PP = 1>
 __global__ __launch_bounds__(NW * 64, 2) void k_dec_gemm_t(GemvArgs a) {  // 2 waves / SIMD: 4-wave blocks 2 per CU
     constexpr int EPT = TMT * TNT / NW;  // epilogue tiles per wave
@@ -855,7 +858,15 @@ __global__ __launch_bounds__(NW * 64, 2) void k_dec_gemm_t(GemvArgs a) {  // 2 w
     };
     auto load_w = [&](uint2 (&lw)[TNT], int kb) {
 #pragma unroll
-        for (int j = 0; j < TNT; ++j) lw[j] = *reinterpret_cast<const uint2*>(wp[j] + ((int64_t)kb << 9));
+        for (int j = 0; j < TNT; ++j) {
+            if constexpr (WF_DG_WNT == 2 || (WF_DG_WNT == 1 && (MODE == MODE_O || MODE == MODE_DN))) {
+                typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+                const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(wp[j] + ((int64_t)kb << 9)));
+                lw[j] = make_uint2(v.x, v.y);
+            } else {
+                lw[j] = *reinterpret_cast<const uint2*>(wp[j] + ((int64_t)kb << 9));
+            }
+        }
     };
     auto mma = [&](const uint4 (&la)[TMT][2], const uint2 (&lw)[TNT]) {
         // TNT <= 4: both halves of each code pair decoded at once (wf_mfma.h pg_decode_pair); at
@@ -1487,6 +1498,9 @@ constexpr int kLmWaves = WF_LM_WAVES;
 constexpr int kLmStages = kLmWaves == 4 ? 4 : 3;
 template <int NW>
 constexpr int lm_stage_bytes() { return 8 * 1024 + NW * 4096; }
+#ifndef WF_LM_NT  // study: 0 = the batched LM head's embedding DMAs without the non-temporal hint
+#define WF_LM_NT 1
+#endif
 template <int NW, int P>
 __global__ __launch_bounds__(NW * 64) void k_lm_head_mfma(const uint16_t* __restrict__ E, const uint16_t* __restrict__ hn,
                                                           int H, int V, int B, uint16_t* __restrict__ logits,
@@ -1513,7 +1527,10 @@ __global__ __launch_bounds__(NW * 64) void k_lm_head_mfma(const uint16_t* __rest
 #pragma unroll
         for (int u = 0; u < AU; ++u) glds16_asm(asrc[u] + 512 * c, st + (AU * wave + u) * 1024);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) glds16_asm(bsrc[j] + 512 * c, st + 8192 + wave * 4096 + j * 1024);
+        for (int j = 0; j < 4; ++j) {  // embedding tiles: read once per step (non-temporal); hn is re-read
+            if constexpr (WF_LM_NT) glds16_asm_nt(bsrc[j] + 512 * c, st + 8192 + wave * 4096 + j * 1024);
+            else glds16_asm(bsrc[j] + 512 * c, st + 8192 + wave * 4096 + j * 1024);
+        }
     };
     v4f_t acc[8][4];
 #pragma unroll

@@ -51,6 +51,16 @@ __device__ __forceinline__ void glds16_asm(const void* g, const void* lds) {
                  : "memory");
 }
 
+// The same with the non-temporal hint, for streams read once (the batched LM head's embedding tiles)
+__device__ __forceinline__ void glds16_asm_nt(const void* g, const void* lds) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(lds));
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(dst)
+                 : "memory");
+}
+
 // Epi::apply(i_tile_row0, j_tile_col0, acc, l16, q): called once per 16x16 output tile with its
 // first row / column; lane holds D[row0 + 4q + r][col0 + l16], r < 4. k-steps [c_begin, c_end)
 // (a split-K slice; the whole K is [0, K/64)).
