@@ -1696,6 +1696,9 @@ __global__ __launch_bounds__(kNT) void k_rownorm(const uint16_t* __restrict__ x,
 // 16-byte slot, its 4 dwords gathered by conflict-free ds_read_b32), so every line of the code
 // tensor is written by one block of one XCD (the former 4-rows-per-block kernel split each line
 // over four blocks' 4-byte stores: 76 us at K 2560, 98 us at K 6912 for 16384 rows).
+#ifndef WF_RN8_NT  // FFN-width row loads with the non-temporal hint (that buffer is read only here): 71.0
+#define WF_RN8_NT 1  // -> 70.1 us; the hidden-width rows are re-read as the residual (27.0 vs 26.2 us with it)
+#endif
 // FULL: the launcher saw K / 8 > 64 (NP - 1), so pieces j < NP - 1 exist for every lane (no per-piece
 // bound checks; only the last piece is checked).
 // Two blocks per CU (4 waves per SIMD, <= 128 VGPRs) up to K 7168, as the LDS allows; unbounded,
@@ -1716,7 +1719,8 @@ __global__ __launch_bounds__(512, NP <= 14 ? 4 : 1) void k_rownorm_tile8(const u
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
         const int pc = min(64 * j + lane, npk - 1);
-        xv[j] = *reinterpret_cast<const uint4*>(x + (int64_t)row * xs + 8 * pc);
+        if constexpr (WF_RN8_NT && NP > 5) xv[j] = ldg_nt(reinterpret_cast<const uint8_t*>(x + (int64_t)row * xs + 8 * pc));
+        else xv[j] = *reinterpret_cast<const uint4*>(x + (int64_t)row * xs + 8 * pc);
     }
     for (int p = threadIdx.x; p < npk; p += 512)
         reinterpret_cast<uint4*>(s_nw)[p] = reinterpret_cast<const uint4*>(nw)[p];
