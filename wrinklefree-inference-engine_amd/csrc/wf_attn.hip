@@ -1404,15 +1404,19 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
             return WF_EINVAL;
         }
         const AttnTail tl = tail ? *tail : AttnTail{};
+#ifndef WF_KV8_DB  // study: 1 = double-buffered tiles (2 waves per SIMD) for the FP8 / INT8 caches too
+#define WF_KV8_DB 0
+#endif
+        constexpr bool kKv8Db = WF_KV8_DB;
 #define WF_AM(DBV, KV8V, TAILV, SCALE, VSC)                                                                        \
     hipLaunchKernelGGL((k_attn_mfma<DBV, false, false, KV8V, false, TAILV>), grid, dim3(256), 0, st, q, q_sb, k, v, \
                        kv_sb, kv_sh, Hq, Hkv, S, seq_lens, SCALE, ml, o, pt, pps, npages, kv_pgs, VSC, tl)
         if (kv8 == 2) {  // int8 caches: as FP8, a wider in-register decode
             if (tail) WF_AM(false, 2, true, sm_scale * k_scale, v_scale);
-            else WF_AM(false, 2, false, sm_scale * k_scale, v_scale);
+            else WF_AM(kKv8Db, 2, false, sm_scale * k_scale, v_scale);
         } else if (kv8) {  // FP8 caches: K scale folded into the score scale; one tile in flight per wave, 4 waves per SIMD
             if (tail) WF_AM(false, 1, true, sm_scale * k_scale, v_scale);
-            else WF_AM(false, 1, false, sm_scale * k_scale, v_scale);
+            else WF_AM(kKv8Db, 1, false, sm_scale * k_scale, v_scale);
         } else {  // bf16: double-buffered tiles, 2 waves per SIMD (at 4 splits a wave takes >= 2 tiles at ctx >= 1024)
             if (tail) WF_AM(true, 0, true, sm_scale, 1.0f);
             else WF_AM(true, 0, false, sm_scale, 1.0f);
