@@ -60,6 +60,7 @@ def _load(path: Path):
         "orc_bitnet_linear_bf16": [vp, vp, f32, i32, i32, vp],
         "orc_attention_gqa_bf16": [vp, vp, vp, i32, i32, i32, i32, i32, f32, vp],
         "orc_attention_gqa_f32": [vp, vp, vp, i32, i32, i32, i32, i32, f32, vp],
+        "orc_attention_sdpa_cpu_bf16": [vp, vp, vp, i32, i32, i32, i32, i32, vp],
         "orc_decode_step": [vp, i32, i32, vp, vp],
         "orc_msb_ternarize": [vp, i32, i32, i32, f32, vp], "orc_msb_dequant": [vp, i32, i32, f32, vp],
         "orc_msb_linear": [vp, f32, vp, vp, i32, i32, i32, i32, vp],
@@ -74,6 +75,8 @@ def _load(path: Path):
     L.orc_f32_to_e4m3.restype = C.c_uint8
     L.orc_e4m3_to_f32.argtypes = [C.c_uint8]
     L.orc_e4m3_to_f32.restype = f32
+    L.orc_fexp_u20.argtypes = [f32]
+    L.orc_fexp_u20.restype = f32
     L.orc_vnni_build.argtypes = []
     L.orc_vnni_build.restype = C.c_int
     L.orc_num_threads.argtypes = []
@@ -245,6 +248,25 @@ def attention_gqa_f32(q_bits, k_bits, v_bits, s: int, scale: float | None = None
     return out
 
 
+def attention_sdpa_cpu_bf16(q_bits, k_bits, v_bits, s: int) -> np.ndarray:
+    """The reference's SDPA call as torch's CPU flash kernel computes it on bf16 (wf_oracle.c
+    orc_attention_sdpa_cpu_bf16). q [Hq, D]; k/v [Hkv, S_max, D] (bf16 bit patterns)."""
+    q_bits = np.ascontiguousarray(q_bits, dtype=np.uint16)
+    k_bits = np.ascontiguousarray(k_bits, dtype=np.uint16)
+    v_bits = np.ascontiguousarray(v_bits, dtype=np.uint16)
+    hq, d = q_bits.shape
+    hkv, smax, _ = k_bits.shape
+    out = np.zeros((hq, d), np.uint16)
+    _ck(lib().orc_attention_sdpa_cpu_bf16(_p(q_bits), _p(k_bits), _p(v_bits), hq, hkv, d, smax, s, _p(out)), "sdpa")
+    return out
+
+
+def fexp_u20(x: np.ndarray) -> np.ndarray:
+    """torch's Vectorized<float>::fexp_u20, element-wise (the oracle's restatement)."""
+    f = lib().orc_fexp_u20
+    return np.array([f(float(v)) for v in np.asarray(x, np.float32).ravel()], np.float32).reshape(np.shape(x))
+
+
 def e4m3_decode_table() -> np.ndarray:
     """float32 value of every OCP e4m3fn code (the oracle's decoder)."""
     return np.array([lib().orc_e4m3_to_f32(c) for c in range(256)], dtype=np.float32)
@@ -269,15 +291,16 @@ class _Model(C.Structure):
                [(n, C.c_void_p) for n in ("embed", "final_norm", "rope_cos", "rope_sin", "ln_in", "ln_post",
                                           "attn_sub", "ffn_sub", "wq", "wk", "wv", "wo", "wg", "wu", "wd", "wscale",
                                           "k_cache", "v_cache")] + \
-               [("kv_fp8", C.c_int), ("kv_scale", C.c_void_p)]
+               [("kv_fp8", C.c_int), ("kv_scale", C.c_void_p), ("attn_mode", C.c_int)]
 
 
 class DecodeModel:
     """Holds a model's host arrays (dict of numpy arrays in the tests/golden/decode.npz layout) for
     orc_decode_step. K/V caches are [layers, n_kv_heads, max_seq, head_dim] bf16 bits."""
 
-    def __init__(self, arrays: dict, libname: str = "liborc.so", kv_fp8=False, kv_scale=None):
-        """kv_fp8: False / 0 bf16 K/V rows, True / 1 e4m3 rows, 2 int8 rows (orc_model.kv_fp8)."""
+    def __init__(self, arrays: dict, libname: str = "liborc.so", kv_fp8=False, kv_scale=None, attn_mode: int = 0):
+        """kv_fp8: False / 0 bf16 K/V rows, True / 1 e4m3 rows, 2 int8 rows (orc_model.kv_fp8).
+        attn_mode: 0 exact softmax (fp32-SDPA form), 1 the reference's CPU bf16 SDPA (orc_model)."""
         H, L, HQ, HKV, D, I, V, S = (int(x) for x in arrays["cfg"])
         self.cfg = (H, L, HQ, HKV, D, I, V, S)
         self.a = {k: np.ascontiguousarray(v) for k, v in arrays.items()}
@@ -294,6 +317,7 @@ class DecodeModel:
         self.kv_scale = np.ones((L, 2), np.float32) if kv_scale is None else np.ascontiguousarray(
             np.broadcast_to(np.asarray(kv_scale, dtype=np.float32), (L, 2)))
         m.kv_fp8, m.kv_scale = int(kv_fp8), _p(self.kv_scale)
+        m.attn_mode = int(attn_mode)
         self.m = m
 
     def step(self, token: int, pos: int, logits: bool = True):

@@ -52,13 +52,18 @@ def compare_position(g, i, krows, vrows, top_vals, layers):
     return ek, ev, el
 
 
-@pytest.mark.parametrize("fixture", ["decode_full", "decode_full_f32attn"])
-def test_oracle_full_width_vs_reference_decode_loop(orc, fixture):
+@pytest.mark.parametrize("fixture,attn_mode", [("decode_full", 1), ("decode_full_f32attn", 0)])
+def test_oracle_full_width_vs_reference_decode_loop(orc, fixture, attn_mode):
     """K / V rows of both layers and the top-64 logits of all 64 positions vs the reference, teacher
-    forced; layer 0's rows (computed from the token embedding alone) bit-exact; greedy token equal
-    wherever the reference's top-2 gap is clear. decode_full_f32attn (the reference's loop with its
-    SDPA evaluated in fp32): bit-exact everywhere. decode_full (its CPU bf16 SDPA): bounded drift
-    from layer 1 on, explained by the SDPA's bf16 probabilities (see the asserts)."""
+    forced (the token AND, for decode_full, the reference's K / V rows: each position then starts
+    from the reference's own state, so one position's flip does not follow every later position
+    through its cache row); layer 0's rows (computed from the token embedding alone) bit-exact;
+    greedy token equal wherever the reference's top-2 gap is clear.
+    decode_full (the reference exactly as it runs, CPU bf16 SDPA) against the oracle's restatement
+    of that SDPA (attn_mode 1): <= 3 flipped positions of 64 (measured 3: positions 0, 25, 63 --
+    summation-order ties of the SDPA's GEMMs, tests/golden/sdpa_probe.py).
+    decode_full_f32attn (the reference's loop with its SDPA evaluated in fp32) against the exact
+    softmax (attn_mode 0): bit-exact everywhere, cache not forced."""
     cfg, w, kh, vh, g = regenerate(fixture)
     import torch
     from wfamd.model import rope_tables
@@ -72,7 +77,7 @@ def test_oracle_full_width_vs_reference_decode_loop(orc, fixture):
         a[n] = w[n].numpy()
     for n in ("embed", "final_norm", "ln_in", "ln_post", "attn_sub", "ffn_sub"):
         a[n] = bits(w[n])
-    m = orc.DecodeModel(a)
+    m = orc.DecodeModel(a, attn_mode=attn_mode)
     ctx0 = int(g["ctx0"])
     m.k_cache[:, :, :ctx0] = bits(kh)
     m.v_cache[:, :, :ctx0] = bits(vh)
@@ -87,21 +92,23 @@ def test_oracle_full_width_vs_reference_decode_loop(orc, fixture):
         assert ek[0] == 0.0 and ev[0] == 0.0, (i, ek, ev)  # layer 0: bit-exact
         if max(ek + ev + [el]) >= FLIP:
             flips.append((i, [round(e, 4) for e in ek + ev], round(el, 4)))
+        if attn_mode == 1:
+            L, HKV, D = cfg.layers, cfg.n_kv_heads, cfg.head_dim
+            m.k_cache[:, :, pos] = g["k_rows"][i].reshape(L, HKV, D)
+            m.v_cache[:, :, pos] = g["v_rows"][i].reshape(L, HKV, D)
+        if flips and flips[-1][0] == i:
             continue
         worst = max(worst, el)
         ref = orc.bf16_to_f32(g["top_val"][i])
         if ref[0] - ref[1] > 1e-2 * abs(ref[0]):
             assert nxt == int(g["next"][i]), i
-    print(f"oracle vs reference ({fixture}), {P} positions: worst clean top-64 logits rel-L2 {worst:.2e}; "
+    print(f"oracle (attn_mode {attn_mode}) vs reference ({fixture}), {P} positions: worst clean top-64 logits rel-L2 {worst:.2e}; "
           f"flips {len(flips)}: {flips}")
     if fixture == "decode_full_f32attn":
         # the reference's loop with its SDPA evaluated in fp32 and rounded once: the oracle IS that
         # computation -- every K / V row and every top-64 logit bit-identical, every greedy token equal
         assert not flips and worst == 0.0, flips
     else:
-        # the reference's CPU bf16 SDPA rounds the softmax probabilities to bf16 before P.V, so ~20-40 %
-        # of its attention-output elements sit >= 1 bf16 ulp from the exactly rounded value; that flips
-        # int8 codes of attn_sub_norm's quantization and the random-init model carries one code flip to
-        # ~2-4 % of the next layer's K / V (measured: 63 of 64 positions, layer-1 rows 2.2-4.2 %, top-64
-        # logits 1-2.6 %). Layer 0's rows (no attention upstream) stay bit-exact (asserted above).
-        assert all(e < 6e-2 for _, es, el in flips for e in es + [el]), flips
+        # a flip is one bf16 attention element on the other side of a rounding boundary (an fp32
+        # summation-order tie) turned into an int8 code step by attn_sub_norm's quantization
+        assert len(flips) <= 3 and all(e < 3e-2 for _, es, el in flips for e in es + [el]), flips

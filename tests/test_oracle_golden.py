@@ -227,3 +227,42 @@ class TestActivationSparsity:
         assert np.array_equal(y.numpy(), g["sp_topk"]) and cfg.get_average_sparsity() == pytest.approx(0.6)
         y, r = sp.apply_sparsity(x, sp.get_default_config())
         assert y is x and r == 0.0
+
+
+def test_sdpa_cpu_bf16_restatement_vs_torch(orc):
+    """The reference's attention call (scripts/direct_inference_full.py:241) as it runs: torch
+    2.10's CPU flash SDPA on bf16 (a third-party dependency; tests/golden/sdpa_probe.py). The
+    oracle's restatement (orc_attention_sdpa_cpu_bf16: 512-key blocks, running max, fexp_u20,
+    bf16 probabilities, unrounded sums) against torch's own outputs over block edges (1, 15-17,
+    511-513, 527 keys), the decode_full geometry (961 keys, 20 / 5 heads), 1024-4096 keys and
+    peaky / flat scores: <= 0.1 % of the bf16 elements differ, each head within 2e-3 rel-L2 (the
+    QK / P.V GEMM summation order of oneDNN is unpublished; those elements are fp32-order ties).
+    The exact softmax rounded once differs in > 20 % of them, so the fixture discriminates."""
+    import sys
+    sys.path.insert(0, str(GOLDEN))
+    import sdpa_probe as sp
+    z = load_golden("sdpa_cpu_bf16")
+    assert str(z["input_sha256"]) == sp.digest(), "regenerated SDPA inputs differ from the fixture's"
+    assert int(z["backend"]) == 1  # torch._fused_sdp_choice: FLASH_ATTENTION
+    mis = tot = mis_exact = 0
+    for c in sp.CASES:
+        q, k, v = sp.inputs(*c)
+        qb, kb, vb = sp.bits(q[0, :, 0]), sp.bits(k[0]), sp.bits(v[0])
+        o = orc.attention_sdpa_cpu_bf16(qb, kb, vb, c[1])
+        ref = z[f"out_{c[0]}"]
+        of, rf = orc.bf16_to_f32(o), orc.bf16_to_f32(ref)
+        for h in range(c[2]):
+            err = np.linalg.norm(of[h] - rf[h]) / np.linalg.norm(rf[h])
+            assert err <= 2e-3, (c, h, err)
+        mis += int((o != ref).sum())
+        tot += o.size
+        mis_exact += int((orc.attention_gqa_bf16(qb, kb, vb, c[1]) != ref).sum())
+    print(f"SDPA restatement: {mis} / {tot} bf16 elements differ from torch; exact softmax: {mis_exact}")
+    assert mis <= 1e-3 * tot, (mis, tot)
+    assert mis_exact >= 0.2 * tot, (mis_exact, tot)
+    # fexp_u20 is a ~1e-4-accurate exponential: fexp_u20(0) = 0.9999466 (the row maximum's own term
+    # of the sum; its bf16 P rounds to 1.0), flushed to 0 below ln(FLT_MIN)
+    x = np.array([0.0, -1.0, -2.5, -10.0, -87.0, -88.0, -200.0], np.float32)
+    e = orc.fexp_u20(x)
+    assert e[0] == np.float32(0.9999466) and e[-1] == 0.0 and e[-2] == 0.0
+    assert np.allclose(e[:5], np.exp(x[:5].astype(np.float64)), rtol=1.5e-4, atol=0)
