@@ -103,3 +103,27 @@ def test_vnni_baseline_build_equals_checker():
         assert orc.lib().orc_bitnet_linear_bf16(x.ctypes.data, p.ctypes.data, 1.5, n, k, l0.ctypes.data) == 0
         assert fast.orc_bitnet_linear_bf16(x.ctypes.data, p.ctypes.data, 1.5, n, k, l1.ctypes.data) == 0
         assert np.array_equal(l0, l1), (n, k)
+
+
+def test_host_cores_respect_the_cgroup_quota(monkeypatch):
+    """A GPU box may show every CPU of the machine in the affinity mask while its cgroup quota is a
+    slice of them: the replicas' core slices come from the mask capped at the quota."""
+    import os
+    from wfamd import replicas
+    mask = sorted(os.sched_getaffinity(0))
+    monkeypatch.setattr(replicas.os, "sched_getaffinity", lambda pid: set(range(128)))
+    monkeypatch.setattr(replicas, "cgroup_cpu_quota", lambda: 16.0)
+    assert replicas.host_cores() == list(range(16))
+    sl = [replicas.core_slice(r, 8) for r in range(8)]
+    assert sl == [[2 * r, 2 * r + 1] for r in range(8)]  # 8 replicas x 2 cores, all within the quota
+    monkeypatch.setattr(replicas, "cgroup_cpu_quota", lambda: None)
+    assert replicas.host_cores() == list(range(128))
+    assert mask  # (the real mask is untouched)
+
+
+def test_timed_window_single_rank():
+    from wfamd.replicas import timed_steps, timed_window
+    calls = []
+    tw = timed_window(lambda: calls.append(1), 5, lambda: None)
+    assert len(calls) == 5 and tw["max_s"] == tw["local_s"] >= 0 and tw["t_end"] >= tw["t_start"]
+    assert timed_steps(lambda: None, 3, lambda: None) >= 0

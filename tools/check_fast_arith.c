@@ -72,7 +72,7 @@ int main(int argc, char** argv) {
         else { // near a half-integer: (k + 0.5) * sf rounded to bf16 +- a few ulps
             float k = (float)((int)(xr() % 255) - 127);
             float t = (k + 0.5f) * sf;
-            x = u2f((f2u(t) & 0xffff0000u) + (uint32_t)(((int)(xr() % 5) - 2) << 16));
+            x = u2f((f2u(t) & 0xffff0000u) + ((uint32_t)((int)(xr() % 5) - 2) << 16));
             if (!(fabsf(x) <= m)) continue;
         }
         ++n;
@@ -83,5 +83,24 @@ int main(int argc, char** argv) {
     }
     printf("quantizer: %ld mismatches of %ld (inv +-1 ulp: %ld)\n", bad, n, bad2);
     total += bad + bad2;
+    // 4) exhaustive over x: EVERY bf16 x with |x| <= m, for a sweep of bf16 maxima m (every
+    //    1/scale-th one of 2^-31 .. 2^17), with the reciprocal RN(1/sf) and +-1 ulp -- the prologue
+    //    forms 1/sf as v_rcp_f32 + one Newton step, within 1 ulp of RN(1/sf) (wf_device.h rcp_1ulp)
+    long bad3 = 0, n3 = 0;
+    const uint32_t mstep = scale >= 1.0 ? 1u : (uint32_t)(1.0 / scale);
+    for (uint32_t hm = 0x3000u; hm < 0x4800u; hm += mstep) {
+        const float m = u2f(hm << 16), sf = act_scale_ref(m), inv = 1.0f / sf;
+        const float invs[3] = {inv, u2f(f2u(inv) + 1), u2f(f2u(inv) - 1)};
+        for (uint32_t hx = 0; hx <= hm; ++hx)
+            for (uint32_t sg = 0; sg <= 0x8000u; sg += 0x8000u) {
+                const float x = u2f((hx | sg) << 16);
+                const int8_t r = q_ref(x, sf);
+                for (int j = 0; j < 3; ++j)
+                    if (q_exact(x, sf, invs[j]) != r) { if (bad3 < 5) printf("qx x=%a sf=%a j=%d\n", x, sf, j); ++bad3; }
+                ++n3;
+            }
+    }
+    printf("quantizer, every bf16 x: %ld mismatches of %ld x 3 reciprocals\n", bad3, n3);
+    total += bad3;
     return total ? 1 : 0;
 }

@@ -58,7 +58,7 @@ def child(args):
     import torch
     import torch.distributed as dist
     from wfamd.model import BITNET_2B, BitNetDecoder, synthetic_weights
-    from wfamd.replicas import timed_steps
+    from wfamd.replicas import timed_window
     if args.replicas > 1:  # host-only rendezvous (gloo over 127.0.0.1): no RCCL communicator
         dist.init_process_group("gloo", rank=args.replica, world_size=args.replicas)
     cfg = dataclasses.replace(BITNET_2B, layers=args.layers)
@@ -107,12 +107,12 @@ def child(args):
     for _ in range(3):  # warm (graph capture)
         one()
     torch.cuda.synchronize()
-    t_start = time.time()
-    el = timed_steps(one, args.steps, torch.cuda.synchronize, dist if args.replicas > 1 else None)
-    t_end = time.time()
+    tw = timed_window(one, args.steps, torch.cuda.synchronize, dist if args.replicas > 1 else None)
+    el = tw["local_s"]  # this replica's own clock: its rate; the node line keeps the max and the union
     n1, n128 = (n_b1 * args.steps if d1 else 0), (args.steps if d128 else 0)
     r = {"replica": args.replica, "cores": len(cores), "core_range": [cores[0], cores[-1]],
-         "seed": args.seed + args.replica, "seconds": round(el, 4), "t_start": t_start, "t_end": t_end,
+         "seed": args.seed + args.replica, "seconds": round(el, 4), "max_seconds": round(tw["max_s"], 4),
+         "t_start": tw["t_start"], "t_end": tw["t_end"],
          "b1_steps": n1, "b128_steps": n128,
          "b1_tokens_per_s": round(n1 / el, 2), "b128_tokens_per_s": round(128 * n128 / el, 2)}
     r["tokens_per_s"] = round(r["b1_tokens_per_s"] + r["b128_tokens_per_s"], 2)

@@ -8,7 +8,8 @@ timed region, on the host.
   (the reference pins its CPU server to 8 cores, scripts/launch_sglang_bitnet.sh:61-67); set
   before the process touches the GPU.
 * `timed_steps` brackets K steps with barrier + device sync on both sides and returns the MAX
-  elapsed time over ranks; `replica_rate` turns that into the whole-job rate.
+  elapsed time over ranks (`timed_window` also returns each rank's own time and window);
+  `replica_rate` turns that into the whole-job rate.
 * `aggregate` sums per-replica results and reports the spread (BASELINE configs[4]).
 * `launch` starts N replica processes, process i with HIP_VISIBLE_DEVICES=i, and collects the one
   JSON line each prints (tools/replica_node.py); it hands them a host rendezvous (MASTER_ADDR
@@ -24,12 +25,42 @@ import time
 from typing import Callable, Dict, List, Optional, Sequence
 
 
+def cgroup_cpu_quota() -> Optional[float]:
+    """CPUs the cgroup allows (v2 cpu.max, or v1 cfs quota / period); None when unlimited. A GPU box
+    may show every CPU of the machine in the affinity mask while its quota is a slice of them."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        return None if q <= 0 else q / p
+    except (OSError, ValueError):
+        return None
+
+
+def host_cores() -> List[int]:
+    """The host cores this process may really use: its affinity mask, sorted, capped at the cgroup
+    CPU quota (the first floor(quota) CPUs of the mask)."""
+    mask = sorted(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    if quota is not None and int(quota) < len(mask):
+        return mask[:max(1, int(quota))]
+    return mask
+
+
 def core_slice(rank: int, world: int, cores: Optional[Sequence[int]] = None) -> List[int]:
-    """Disjoint, contiguous, near-equal slices of `cores` (default: this process's affinity mask,
-    sorted); slice `rank` of `world`. Every core belongs to exactly one slice when world <= cores."""
+    """Disjoint, contiguous, near-equal slices of `cores` (default: host_cores(), the affinity mask
+    within the cgroup quota); slice `rank` of `world`. Every core belongs to exactly one slice when
+    world <= cores."""
     if world <= 0 or not 0 <= rank < world:
         raise ValueError(f"rank {rank} out of range for world {world}")
-    cs = sorted(cores if cores is not None else os.sched_getaffinity(0))
+    cs = sorted(cores if cores is not None else host_cores())
     if not cs:
         raise ValueError("no host cores")
     if world > len(cs):  # more replicas than cores: share round-robin (never an empty slice)
@@ -53,29 +84,38 @@ def pin_host_cores(rank: int, world: int, cores: Optional[Sequence[int]] = None)
     return sl
 
 
-def timed_steps(step: Callable[[], None], steps: int, sync: Callable[[], None], dist=None,
-                device: Optional[str] = None) -> float:
-    """Run `step` `steps` times between synchronised barriers; return max-over-ranks seconds.
-    `dist` is torch.distributed initialised with a host backend (gloo): the barrier and the
-    max-reduce of one scalar run on the host, outside the timed device work."""
+def timed_window(step: Callable[[], None], steps: int, sync: Callable[[], None], dist=None,
+                 device: Optional[str] = None) -> Dict[str, float]:
+    """Run `step` `steps` times between synchronised barriers. Returns this rank's own elapsed time
+    (`local_s`, measured from after the start barrier to the device sync after its last step), the
+    max of that over ranks (`max_s`) and this rank's wall-clock window (`t_start`, `t_end`, stamped
+    inside the barriers, so the window holds no barrier wait). `dist` is torch.distributed
+    initialised with a host backend (gloo): the barriers and the max-reduce of one scalar run on the
+    host, outside the timed device work."""
     import torch
     on = dist is not None and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
     sync()
     if on:
         dist.barrier()
     sync()
-    t0 = time.perf_counter()
+    w0, t0 = time.time(), time.perf_counter()
     for _ in range(steps):
         step()
     sync()
+    local, w1 = time.perf_counter() - t0, time.time()
+    el = local
     if on:
         dist.barrier()
-    el = time.perf_counter() - t0
-    if on:
-        t = torch.tensor([el], dtype=torch.float64, device=device or "cpu")
+        t = torch.tensor([local], dtype=torch.float64, device=device or "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    return el
+    return {"max_s": el, "local_s": local, "t_start": w0, "t_end": w1}
+
+
+def timed_steps(step: Callable[[], None], steps: int, sync: Callable[[], None], dist=None,
+                device: Optional[str] = None) -> float:
+    """timed_window's max-over-ranks seconds (the whole-job clock of bench.py's contract)."""
+    return timed_window(step, steps, sync, dist, device)["max_s"]
 
 
 def replica_rate(units_per_step_per_rank: int, steps: int, world: int, elapsed_s: float) -> float:
