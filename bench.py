@@ -51,6 +51,10 @@ def parse():
                          "config 4), on paged KV")
     ap.add_argument("--paged", action="store_true", help="paged KV (32-token pages; batch >= 16)")
     ap.add_argument("--no-gemv", action="store_true", help="skip the standalone GEMV benchmark")
+    ap.add_argument("--no-sub", action="store_true",
+                    help="skip the sub-records (batch 128 at ctx 1024 and at config-4 contexts, prefill 8 x 2048) "
+                         "that the default N = 1 batch-1 run appends")
+    ap.add_argument("--sub-steps", type=int, default=10, help="timed steps of each batch-128 sub-record")
     ap.add_argument("--kv", choices=["bf16", "fp8", "int8"], default="bf16",
                     help="K/V cache element type (batch >= 16): fp8 = OCP e4m3fn, scale 1.0; int8 = the "
                          "reference's INT8 KVCacheDtype, scale 4/127 (unit-variance synthetic K/V)")
@@ -147,6 +151,92 @@ def gemv_bench(rotate_bytes: float = 1.2e9, reps: int = 3):
                      "calls_per_replay": nbuf}
         del w, graph
         torch.cuda.empty_cache()
+    return out
+
+
+INT8_DENSE_PEAK_TOPS = 5000.0  # MI355X dense int8 MFMA (MI355X_MICROARCH.md; no 2:1 sparsity)
+
+
+def sub_records(cfg, steps: int, warmup: int = 3) -> dict:
+    """BASELINE's other single-GPU configurations under the same clock, each
+    with its own roofline:
+      b128      -- decode batch 128, every sequence at ctx 1024 (configs[3] at a fixed context);
+      b128_cfg4 -- decode batch 128 on paged KV, contexts U[1, max_seq - steps) seed 0 (configs[3]);
+      prefill   -- 8 sequences x 2048 tokens through wf_model_prefill (configs[2]).
+    Decode records: tokens/s over `steps` graph-replayed steps (barrier + sync both sides), the
+    per-op HIP-event timing and the dominant op's HBM fraction as in the headline line; prefill: the
+    median of 3 HIP-event-timed calls, int8 GEMM tera-ops (2 M N K summed over the 4 GEMMs x 30
+    layers, as scripts/benchmark_kernels.py:99) per second against the dense int8 peak."""
+    import numpy as np
+    import torch
+    from wfamd.model import BitNetDecoder, synthetic_weights
+    out = {}
+    st = torch.cuda.current_stream()
+    w = synthetic_weights(cfg, seed=0, device="cuda")
+    for name, dist_ in (("b128", "fixed"), ("b128_cfg4", "uniform")):
+        B, total = 128, warmup + steps
+        if dist_ == "uniform":
+            ctxs = np.random.default_rng(0).integers(1, cfg.max_seq - total - 1, size=B)
+        else:
+            ctxs = np.full(B, 1024, dtype=np.int64)
+        paged = dist_ == "uniform"
+        pages = int(sum((c + total + 1 + 31) // 32 for c in ctxs)) if paged else 0
+        dec = BitNetDecoder(cfg, w, batch=B, num_pages=pages, page_seed=0 if paged else None)
+        if paged:
+            for b in range(B):
+                dec.reserve(b, int(ctxs[b]) + total + 1)
+        dec.fill_kv_random(int(ctxs.max()), seed=1)
+        dec.set_state([1] * B, [int(c) for c in ctxs])
+        for _ in range(warmup):
+            dec.step(graph=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            dec.step(graph=True)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        ctx = int(round(float(ctxs.mean()))) + total // 2
+        kern = op_timing(dec, ctx, reps=3)
+        att = kern["attn"]
+        out[name] = {"workload": f"decode batch 128, ctx {'1024' if dist_ == 'fixed' else 'U[1, max_seq)'}, "
+                                 f"kv bf16{', paged' if paged else ''} (BASELINE configs[3])",
+                     "tokens_per_s": round(B * steps / el, 1), "ms_per_step": round(1000.0 * el / steps, 4),
+                     "steps": steps, "ctx_mean": int(round(float(ctxs.mean()))),
+                     "roofline": {"bound": "hbm", "kernel": "attn", "achieved": att["gbs"], "peak": HBM_PEAK_GBS,
+                                  "unit": "GB/s", "frac": round(att["gbs"] / HBM_PEAK_GBS, 4),
+                                  "bytes_per_launch": att["bytes"], "us_per_launch": att["us"],
+                                  "ops": {k: {"us": v["us"], "gbs": v["gbs"], "frac": round(v["gbs"] / HBM_PEAK_GBS, 4)}
+                                          for k, v in kern.items()}}}
+        del dec
+        torch.cuda.empty_cache()
+    # prefill 8 x 2048 (the batched decoder owns the KV slots)
+    seqs_n, seq_len = 8, 2048
+    dec = BitNetDecoder(cfg, w, batch=16)
+    rng = np.random.default_rng(0)
+    seqs = [(b, rng.integers(0, cfg.vocab, size=seq_len).tolist(), 0) for b in range(seqs_n)]
+    n_rows = seqs_n * seq_len  # one 16384-row chunk (tools/prefill_bench.py's default)
+    dec.prefill(seqs, chunk_rows=n_rows)
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        dec.prefill(seqs, chunk_rows=n_rows)
+        e1.record(st)
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1))
+    ms = sorted(times)[1]
+    n = seqs_n * seq_len
+    h, i, kv = cfg.hidden, cfg.inter, cfg.kv_dim
+    gemm_ops = 2.0 * n * cfg.layers * ((h + 2 * kv) * h + h * h + 2 * i * h + h * i)
+    tops = gemm_ops / (ms / 1000.0) / 1e12
+    out["prefill"] = {"workload": f"prefill {seqs_n} x {seq_len} tokens (BASELINE configs[2])", "ms": round(ms, 2),
+                      "tokens_per_s": round(n / (ms / 1000.0), 1), "gemm_tera_ops": round(gemm_ops / 1e12, 2),
+                      "roofline": {"bound": "mfma", "kernel": "whole prefill (GEMM ops over the end-to-end time)",
+                                   "achieved": round(tops, 1), "peak": INT8_DENSE_PEAK_TOPS, "unit": "TOPS",
+                                   "frac": round(tops / INT8_DENSE_PEAK_TOPS, 4)}}
+    del dec, w
+    torch.cuda.empty_cache()
     return out
 
 
@@ -285,6 +375,11 @@ def main():
     step_gbs = step_bytes / (ms_step / 1000.0) / 1e9
     roof = roofline(kern, B, args, step_gbs) if kern else None
     gemv = None if (args.no_gemv or B != 1) else gemv_bench()
+    sub = None
+    if rank == 0 and world == 1 and B == 1 and not args.no_sub and args.ctx_dist == "fixed":
+        del dec
+        torch.cuda.empty_cache()
+        sub = sub_records(cfg, args.sub_steps)
     if cpu:
         cpu_gemv = cpu.pop("gemv")
         if gemv:
@@ -309,7 +404,7 @@ def main():
             "step_hbm_gbs": round(step_gbs, 1),
             "gemv_hbm_gbs": kern.get("gate_up", {}).get("gbs") if kern else None,
             "gemv": gemv,
-            "roofline": roof, "cpu_baseline": cpu, "kernels": kern,
+            "roofline": roof, "cpu_baseline": cpu, "kernels": kern, "sub_records": sub,
         }
         print(json.dumps(line))
     if world > 1:

@@ -255,12 +255,16 @@ int wf_model_launch_op(wf_model* m, int layer, int op, void* stream);
  * (running max m, sum l) and the unnormalised output o[d] at part_o[((b n_heads + h) records + s) *
  * 128 + ((d >> 2) & 1) * 64 + (d >> 3) * 4 + (d & 3)] (head_dim 128); the attention output is
  * sum_s e^(m_s - M) o_s / sum_s e^(m_s - M) l_s, M = max_s m_s (records with l = 0 are empty).
- * Device pointers owned by the model; valid until wf_model_destroy. */
+ * Batch < 16 and untiled caches (the reference's SDPA semantics, records already in one frame:
+ * m = 0): attn_row is the merged bf16 attention output [batch, n_heads * head_dim] the O projection
+ * reads; NULL on the batched tile-layout path. Device pointers owned by the model; valid until
+ * wf_model_destroy. */
 typedef struct {
     const uint16_t* q;
     const float* part_ml;
     const float* part_o;
     int records;
+    const uint16_t* attn_row;
 } wf_attn_records;
 int wf_model_attn_view(const wf_model* m, wf_attn_records* out);
 /* Which batched GEMM ops (flags[0..3] = QKV, O, gate|up, down) run their input row norm inside the

@@ -61,6 +61,7 @@ def _load(path: Path):
         "orc_attention_gqa_bf16": [vp, vp, vp, i32, i32, i32, i32, i32, f32, vp],
         "orc_attention_gqa_f32": [vp, vp, vp, i32, i32, i32, i32, i32, f32, vp],
         "orc_attention_sdpa_cpu_bf16": [vp, vp, vp, i32, i32, i32, i32, i32, vp],
+        "orc_attention_sdpa_cpu_f32": [vp, vp, vp, i32, i32, i32, i32, i32, vp],
         "orc_decode_step": [vp, i32, i32, vp, vp],
         "orc_msb_ternarize": [vp, i32, i32, i32, f32, vp], "orc_msb_dequant": [vp, i32, i32, f32, vp],
         "orc_msb_linear": [vp, f32, vp, vp, i32, i32, i32, i32, vp],
@@ -258,6 +259,18 @@ def attention_sdpa_cpu_bf16(q_bits, k_bits, v_bits, s: int) -> np.ndarray:
     hkv, smax, _ = k_bits.shape
     out = np.zeros((hq, d), np.uint16)
     _ck(lib().orc_attention_sdpa_cpu_bf16(_p(q_bits), _p(k_bits), _p(v_bits), hq, hkv, d, smax, s, _p(out)), "sdpa")
+    return out
+
+
+def attention_sdpa_cpu_f32(q_bits, k_bits, v_bits, s: int) -> np.ndarray:
+    """attention_sdpa_cpu_bf16 before the output's bf16 rounding (float32 [Hq, D])."""
+    q_bits = np.ascontiguousarray(q_bits, dtype=np.uint16)
+    k_bits = np.ascontiguousarray(k_bits, dtype=np.uint16)
+    v_bits = np.ascontiguousarray(v_bits, dtype=np.uint16)
+    hq, d = q_bits.shape
+    hkv, smax, _ = k_bits.shape
+    out = np.zeros((hq, d), np.float32)
+    _ck(lib().orc_attention_sdpa_cpu_f32(_p(q_bits), _p(k_bits), _p(v_bits), hq, hkv, d, smax, s, _p(out)), "sdpa32")
     return out
 
 

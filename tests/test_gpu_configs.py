@@ -127,7 +127,7 @@ def test_decode_batch1_full_width_vs_oracle(orc, ctx, trained):
     cfg = make_cfg(2, 128256, 4128)
     w = make_weights(cfg, seed=1, trained_like=trained)
     dec = BitNetDecoder(cfg, w, batch=1)
-    m = orc.DecodeModel(oracle_arrays(cfg, w))
+    m = orc.DecodeModel(oracle_arrays(cfg, w), attn_mode=1)  # batch 1: the reference's SDPA (k_attn_sdpa)
     del w
     gen = torch.Generator(device="cuda").manual_seed(ctx)
     for l in range(cfg.layers):
@@ -190,7 +190,7 @@ def test_decode_batch128_paged_full_width_vs_oracle(orc, kv, B):
     rows = sorted({int(np.argmin(ctxs)), int(np.argmax(ctxs))} | {r for r in (0, 1, 17, 33, 39, 64, 100, 127) if r < B})
     gen = torch.Generator(device="cuda").manual_seed(77)
     cmax = int(ctxs.max())
-    models = {b: orc.DecodeModel(a, kv_fp8=quant, kv_scale=scale if fp8 else None) for b in rows}
+    models = {b: orc.DecodeModel(a, kv_fp8=quant, kv_scale=scale if fp8 else None, attn_mode=1) for b in rows}
     for l in range(cfg.layers):
         k = torch.randn(B, cfg.n_kv_heads, cmax, cfg.head_dim, generator=gen, device="cuda").to(torch.bfloat16)
         v = torch.randn(B, cfg.n_kv_heads, cmax, cfg.head_dim, generator=gen, device="cuda").to(torch.bfloat16)
@@ -252,12 +252,12 @@ def _attn_case(variant):
     """(decoder kwargs, batch, max_seq) of each attention code path of the decode step."""
     from wfamd._lib import WF_FMT_TQ
     return {
-        "b1": (dict(), 1, 4096),                                     # k_attn_part<1, 8>
+        "b1": (dict(), 1, 4096),                                     # k_attn_sdpa
         "b128_paged_bf16": (dict(kv_dtype="bf16"), 128, 4096),       # k_attn_mfma (double-buffered), pages
         "b128_paged_fp8": (dict(kv_dtype="fp8", kv_scale=(0.5, 0.25)), 128, 4096),  # k_attn_mfma FP8
         "b16_dense_tiled": (dict(), 16, 4096),                       # k_attn_mfma on dense tile planes
-        "b16_tq_untiled": (dict(wfmt=WF_FMT_TQ), 16, 4096),         # k_attn_part<4, 4> (untiled fallback)
-        "b16_seq4100_untiled": (dict(), 16, 4100),                   # max_seq % 32 != 0: untiled fallback
+        "b16_tq_untiled": (dict(wfmt=WF_FMT_TQ), 16, 4096),         # k_attn_sdpa (untiled caches)
+        "b16_seq4100_untiled": (dict(), 16, 4100),                   # max_seq % 32 != 0: k_attn_sdpa
     }[variant]
 
 
@@ -265,13 +265,15 @@ def _attn_case(variant):
                                      "b16_tq_untiled", "b16_seq4100_untiled"])
 def test_step_attention_kernels_vs_oracle(orc, variant):
     """WF_OP_QKV then WF_OP_ATTN of layer 0 on a full-geometry model (20 / 5 heads x 128), every
-    row at its own context S (the list ATTN_S, then random lengths): the attention output merged
-    from the partial records (include/wf_bitnet.h wf_model_attn_view: exactly what the O
-    projection's input stage reads) against orc_attention_gqa_f32 on the step's own q and the K/V
-    the cache holds (the row the QKV epilogue appended included), rel-L2 <= 2e-4 per (row, head)."""
+    row at its own context S (the list ATTN_S, then random lengths): the bf16 attention row the O
+    projection reads (include/wf_bitnet.h wf_model_attn_view attn_row) against the reference's SDPA
+    (orc_attention_sdpa_cpu_bf16) on the step's own q and the K/V the cache holds (the row the QKV
+    epilogue appended included): at most 0.1 % of the elements differ, by 1 ulp (fp32
+    summation-order ties); the batch < 16 / untiled kernel's fp32 split records within 1e-5."""
     from wfamd import _lib
     from wfamd.model import BitNetDecoder
     kw, B, smax = _attn_case(variant)
+    recs = variant in ("b1", "b16_tq_untiled", "b16_seq4100_untiled")  # k_attn_sdpa: fp32 split records too
     cfg = make_cfg(1, 1024, smax)
     w = make_weights(cfg, seed=3, trained_like=True)
     rng = np.random.default_rng(5)
@@ -280,7 +282,7 @@ def test_step_attention_kernels_vs_oracle(orc, variant):
         cases = [np.array([s]) for s in ATTN_S_B1]
     else:
         cases = [S]
-    worst = 0.0
+    worst, mism_tot, elems, rows = 0.0, 0, 0, []
     for S in cases:
         paged = variant.startswith("b128")
         pages = int(sum((s + 31) // 32 for s in S)) if paged else 0
@@ -300,18 +302,37 @@ def test_step_attention_kernels_vs_oracle(orc, variant):
             dec.launch_op(0, op)
         torch.cuda.synchronize()
         q, ml, o = dec.attention_records()
-        got = merge_records(ml, o)
+        got = merge_records(ml, o) if recs else None
+        row = dec.attention_row()
+        assert row is not None and (ml.shape[2] > 0) == recs, variant
         check = range(len(S)) if len(S) <= 16 else list(range(12)) + [40, 77, 100, 127]
         for b in check:
             s = int(S[b])
             kb, vb = logical_kv(dec, 0, b, s)
-            ref = orc.attention_gqa_f32(bits(q[b]), kv_bits(dec, kb, 0, 0), kv_bits(dec, vb, 0, 1), s)
-            for h in range(cfg.n_heads):
-                e = rel_l2(got[b, h], ref[h])
-                worst = max(worst, e)
-                assert e < 2e-4, (variant, b, s, h, e)
+            qb, kbb, vbb = bits(q[b]), kv_bits(dec, kb, 0, 0), kv_bits(dec, vb, 0, 1)
+            # the reference's SDPA (orc_attention_sdpa_cpu_*): the merged bf16 row the O projection
+            # reads bit-exact but for summation-order ties; fp32 split records within 1e-5
+            rb = orc.attention_sdpa_cpu_bf16(qb, kbb, vbb, s)
+            gb = bits(row[b])
+            mism = int((gb != rb).sum())
+            ulps = int(np.abs(gb.astype(np.int32) - rb.astype(np.int32)).max())
+            mism_tot += mism
+            elems += gb.size
+            e = rel_l2(orc.bf16_to_f32(gb), orc.bf16_to_f32(rb))
+            worst = max(worst, e)
+            rows.append((b, s, mism, ulps, round(e, 6)))
+            if recs:
+                ref = orc.attention_sdpa_cpu_f32(qb, kbb, vbb, s)
+                for h in range(cfg.n_heads):
+                    eh = rel_l2(got[b, h], ref[h])
+                    assert eh < 1e-5, (variant, b, s, h, eh)
         del dec
-    print(f"attention {variant}: worst rel-L2 {worst:.2e}")
+    print(f"attention {variant}: worst rel-L2 {worst:.2e}; merged bf16 row: {mism_tot} of {elems} elements off the "
+          f"oracle; per row (b, S, mismatches, max ulps, rel-L2): {rows}")
+    # the reference's own GEMM order is unpublished: the oracle itself differs from torch in 0.05-0.09 %
+    # of these elements (test_sdpa_cpu_bf16_restatement_vs_torch); a kernel may add as many again
+    assert worst < 1e-4, rows
+    assert mism_tot <= max(2, elems // 1000), (mism_tot, elems)
 
 
 def _kv_quality(orc, ctx, kvd):
@@ -342,8 +363,9 @@ def _kv_quality(orc, ctx, kvd):
         dec.load_attention_q(q)
         dec.launch_op(0, _lib.WF_OP_ATTN)
         torch.cuda.synchronize()
-        qa, ml, o = dec.attention_records()
+        qa, _, _ = dec.attention_records()
         assert torch.equal(qa, q)
+        row = dec.attention_row().double().cpu().numpy()  # the bf16 rows the O projection reads
         # the exact attention (float64) over the K/V this decoder holds (one-byte: the decoded codes)
         qf = q.double().cpu().numpy()
         exact = np.zeros((B, cfg.n_heads, 128))
@@ -357,7 +379,7 @@ def _kv_quality(orc, ctx, kvd):
                 pr = np.exp(sc - sc.max())
                 exact[b, h] = (pr / pr.sum()) @ vf[g]
         del dec
-        return merge_records(ml, o), exact
+        return row, exact
 
     (g16, e16), (g8, e8) = run("bf16"), run(kvd)
 

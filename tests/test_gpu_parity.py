@@ -334,7 +334,7 @@ def test_decode_steps_match_reference(orc, wfmt):
     (scripts/direct_inference_full.py:267-302 run on the reference's functions) and vs the oracle.
     Tolerance: rel-L2 of bf16 logits <= 1e-3; greedy token identical when the top-2 gap is clear."""
     g, dec = _small_decoder(wfmt)
-    m = orc.DecodeModel(g)
+    m = orc.DecodeModel(g, attn_mode=1)  # batch 1: the reference's SDPA (k_attn_sdpa)
     for pos, tok in enumerate(g["tokens"]):
         dec.set_state([int(tok)], [pos])
         dec.step(graph=True)

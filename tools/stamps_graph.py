@@ -33,7 +33,7 @@ from wfamd.model import BITNET_2B, BitNetDecoder, synthetic_weights  # noqa: E40
 SLOTS, NBLK = 80, 16384
 GEMV_NAMES = {0: "entry", 1: "image", 2: "dot", 3: "out", 7: "qkv_out", 8: "p_ss", 9: "p_r", 10: "p_y", 11: "p_sf",
               12: "p_q", 13: "w_landed"}
-ATTN_NAMES = {0: "entry", 1: "kv_done", 2: "out"}
+ATTN_NAMES = {0: "entry", 1: "qk_done", 2: "exchanged", 3: "records"}
 LM_NAMES = {0: "entry", 1: "staged", 2: "dot", 3: "ticket", 4: "argmax"}
 GEMM_NAMES = {0: "entry", 14: "norm_published", 15: "rows_ready", 1: "issued", 2: "first_mma", 3: "mma_done",
               4: "combined", 5: "epilogue"}

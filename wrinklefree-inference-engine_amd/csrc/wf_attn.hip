@@ -587,6 +587,364 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
 }
 
 // ---------------------------------------------------------------------------------------------
+// The reference's attention AS IT RUNS (scripts/direct_inference_full.py:241: torch 2.10's CPU
+// flash SDPA on bf16; restated in oracle/wf_oracle.c orc_attention_sdpa_cpu_bf16 and pinned by
+// tests/golden/sdpa_cpu_bf16.npz): keys in 512-key blocks with a RUNNING max M_c (max over blocks
+// <= c), probabilities e = fexp_u20(s - M_c) on the 16-key vector part of a block and expf on its
+// tail, P = bf16(e) into P.V, the UNROUNDED e into the row sum, blocks combined by
+// r_c = expf(M_{c-1} - M_c), out = bf16(dst * (1 / sum)).
+//
+// Decode step, batch < 16 and untiled caches: block (split s, query head, sequence) as
+// k_attn_part (kAttnPartSplits1 splits of T = round_up(ceil(S / NS), 16) keys, 16-lane groups),
+// in two phases around an in-launch exchange of the 512-key block maxima:
+//   1. q.k of the split's keys (products exact in fp32, summed in f64 and rounded once -- torch's
+//      oneDNN GEMM is that close to exact, tests/golden/sdpa_probe.py), the split's per-block maxima
+//      published write-through; one lane polls the head's arrival counter (all NS splits);
+//   2. wave 0 folds the NS x 4 published maxima into M_c, r_c and the suffix products R, every
+//      lane forms P and e of its keys, scales by the product of the r's after the key's block
+//      (1.0 exactly inside the split's last block), and accumulates l = sum e and o = sum P v.
+// Every record is then in the frame of the head's last block; the head's last block (ticket)
+// sums the NS records and writes out = bf16(O * (1 / L)) into the bf16 attention row.
+// Residency: every split of a head must be resident while its siblings poll: the host launches
+// at most kSdpaMaxBlocks blocks per launch (B = 1: 160), below the chip's resident count.
+// ---------------------------------------------------------------------------------------------
+constexpr int kSdpaMaxT = 1024;      // split length bound (max_seq <= 8192): a split spans <= 3 blocks
+constexpr int kSdpaMaxSeq = kAttnPartSplits1 * kSdpaMaxT;
+
+// torch Vectorized<float>::fexp_u20 (AVX512), bit for bit (x <= 0 here: no overflow branch)
+__device__ __forceinline__ float fexp_u20(float x) {
+    const float src = x * __uint_as_float(0x3fb8aa3bu);  // x * log2(e)
+    const float fr = src - floorf(src);
+    float r = fmaf(fr, -0.079204240219773236f, -0.22433836478672356f);
+    r = fmaf(fr, r, 0.30354260500649682f);
+    r = fmaf(fr, r, 0.00010703434948458272f);
+    const float t = fmaf(8388608.0f, src - r, 1065353216.0f);
+    const int ci = (int)t;  // v_cvt_i32_f32 truncates, as _mm512_cvttps_epi32
+    return __int_as_float(x < __uint_as_float(0xc2aeac50u) ? 0 : ci);
+}
+// glibc expf (the scalar tail and the block rescale), within ~1 ulp: x = k ln2 + r (two-constant
+// reduction, exact for |k| < 2^11), 2^(r log2 e) on v_exp_f32, scaled by 2^k (x <= 0 here). A 1-ulp
+// difference moves a bf16 P once in ~2^15 keys; the f64 exp it replaced cost ~0.5 us per launch.
+__device__ __forceinline__ float expf_rn(float x) {
+    if (!(x > -104.0f)) return 0.0f;  // below the smallest subnormal (and -inf)
+    const float k = rintf(x * 1.44269504f);
+    float r = fmaf(-k, 0.693145752f, x);  // ln 2 high part (16 bits): k * hi exact
+    r = fmaf(-k, 1.42860677e-06f, r);     // ln 2 low part
+    return ldexpf(__builtin_amdgcn_exp2f(r * 1.44269504f), (int)k);
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)dpp_i<CTRL>((int)(uint32_t)u), hi = (uint32_t)dpp_i<CTRL>((int)(uint32_t)(u >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ double group16_sum_d(double v) {
+    v += dpp_d<DPP_QP_1032>(v);
+    v += dpp_d<DPP_QP_2301>(v);
+    v += dpp_d<DPP_HALF_MIRROR>(v);
+    v += dpp_d<DPP_MIRROR>(v);
+    return v;
+}
+
+// k_attn_sdpa's per-chunk steps as plain functions: lambdas capturing the kernel's locals by reference
+// left their closure objects (pointers to the locals) in scratch
+template <int U>
+__device__ __forceinline__ void sdpa_load(uint4 (&r)[U], const uint16_t* __restrict__ base, int64_t kvb, int c0, int gid,
+                                          int t1) {
+    constexpr int NG = kAttnPartThreads / 16;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int t = min(c0 + gid + NG * u, max(t1 - 1, 0));
+        r[u] = *reinterpret_cast<const uint4*>(base + kvb + (int64_t)t * 128);
+    }
+}
+// q.k of the chunk's keys (products exact in fp32, summed in f64, rounded once), the split's per-block
+// maxima; the scores into sc (one-chunk splits) or the LDS score buffer
+template <int U, bool ONE>
+__device__ __forceinline__ void sdpa_scores(const uint4 (&kr)[U], const uint32_t (&qw)[4], int c0, int gid, int li, int t0,
+                                            int t1, int cb0, float sm_scale, float (&mx)[3], float (&sc)[ONE ? U : 1],
+                                            float* sc_lds) {
+    constexpr int NG = kAttnPartThreads / 16;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t w[4] = {kr[u].x, kr[u].y, kr[u].z, kr[u].w};
+        double dd = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            dd += (double)(bf_lo(qw[i]) * bf_lo(w[i]));  // bf16 x bf16: exact in fp32
+            dd += (double)(bf_hi(qw[i]) * bf_hi(w[i]));
+        }
+        const float sv = (float)group16_sum_d(dd) * sm_scale;
+        const int t = c0 + gid + NG * u;
+        const bool valid = t < t1;
+        const bool in0 = t < 512 * (cb0 + 1), in1 = t < 512 * (cb0 + 2);
+        mx[0] = (valid && in0) ? fmaxf(mx[0], sv) : mx[0];
+        mx[1] = (valid && !in0 && in1) ? fmaxf(mx[1], sv) : mx[1];
+        mx[2] = (valid && !in1) ? fmaxf(mx[2], sv) : mx[2];
+        if constexpr (ONE) sc[u] = sv;
+        else if (valid && li == 0) sc_lds[t - t0] = sv;
+    }
+}
+// probabilities of the chunk's keys and their P.V: e = fexp_u20 / expf of (s - M_c) (vector part /
+// tail of the key's 512-key block), l += e R, o += bf16(e) R v, R = the product of the block
+// rescale factors between the key's block and the split's last one (1.0 in the last block)
+struct SdpaBlocks {
+    float m0, m1, m2, r0, r1, r2;
+};
+template <int U, bool ONE>
+__device__ __forceinline__ void sdpa_pv(const uint4 (&vr)[U], const float (&sc)[ONE ? U : 1], const float* sc_lds, int c0,
+                                        int gid, int t0, int t1, int cb0, int Sb, const SdpaBlocks& bk, float& l,
+                                        float (&o)[8]) {
+    constexpr int NG = kAttnPartThreads / 16;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int t = c0 + gid + NG * u;
+        if (t < t1) {
+            float sv;
+            if constexpr (ONE) sv = sc[u];
+            else sv = sc_lds[t - t0];
+            const bool in0 = t < 512 * (cb0 + 1), in1 = t < 512 * (cb0 + 2);
+            const float Mc = in0 ? bk.m0 : (in1 ? bk.m1 : bk.m2);
+            const float Rc = in0 ? bk.r0 : (in1 ? bk.r1 : bk.r2);
+            const int blk0 = t & ~511;
+            const int vbnd = min(512, Sb - blk0) & ~15;  // the 16-wide vector part of the block
+            const float x = sv - Mc;
+            const float e = ((t - blk0) < vbnd) ? fexp_u20(x) : expf_rn(x);
+            const float p = rbf(e) * Rc;
+            l = fmaf(e, Rc, l);
+            const uint32_t w[4] = {vr[u].x, vr[u].y, vr[u].z, vr[u].w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                o[2 * i] = fmaf(p, bf_lo(w[i]), o[2 * i]);
+                o[2 * i + 1] = fmaf(p, bf_hi(w[i]), o[2 * i + 1]);
+            }
+        }
+    }
+}
+
+template <int U, bool ONE>
+__device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, int64_t q_sb, const uint16_t* __restrict__ K,
+                                               const uint16_t* __restrict__ V, int64_t kv_sb, int64_t kv_sh, int Hq,
+                                               int Hkv, int S, const int32_t* __restrict__ seq_lens, float sm_scale,
+                                               int b0, uint64_t* __restrict__ xg, float2* __restrict__ ml_out,
+                                               float* __restrict__ o_out, uint16_t* __restrict__ row_out,
+                                               unsigned* __restrict__ cnt, unsigned* __restrict__ xep) {
+    constexpr int NS = kAttnPartSplits1, D = 128, LP = 16, NG = kAttnPartThreads / LP, CH = U * NG;
+    constexpr int NWV = kAttnPartThreads / 64;
+    const int s = blockIdx.x, hq = blockIdx.y, b = b0 + (int)blockIdx.z;
+    const int g = hq / (Hq / Hkv);
+    const int gid = threadIdx.x / LP, li = threadIdx.x % LP, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int Sb = min(seq_lens[b], S);
+    const int T = ((Sb + NS - 1) / NS + 15) / 16 * 16;
+    const int t0 = s * T, t1 = min(t0 + T, Sb);
+    const int cb0 = t0 >> 9;
+    const int64_t bh = (int64_t)b * Hq + hq;
+    WF_STAMP(0);
+    __shared__ float sc_lds[ONE ? 1 : kSdpaMaxT];
+    __shared__ float red[NWV][3];
+    __shared__ float blk_m[3], blk_r[3], fin_r;
+    __shared__ float sm_l[NWV];
+    __shared__ __attribute__((aligned(16))) float sm_o[NWV][D];
+    __shared__ int sh_last;
+
+    const int64_t kvb = b * kv_sb + g * kv_sh + li * 8;
+    const uint4 qv = *reinterpret_cast<const uint4*>(q + b * q_sb + (int64_t)hq * D + li * 8);
+    const uint32_t qw[4] = {qv.x, qv.y, qv.z, qv.w};
+    float mx[3] = {-INFINITY, -INFINITY, -INFINITY};  // per 512-key block of the split (<= 3)
+    float sc[ONE ? U : 1];
+    uint4 vA[U], vB[ONE ? 1 : U];
+    if (t0 < t1) {
+        uint4 kA[U];
+        sdpa_load<U>(kA, K, kvb, t0, gid, t1);
+        if constexpr (ONE) {
+            sdpa_load<U>(vA, V, kvb, t0, gid, t1);
+            sdpa_scores<U, ONE>(kA, qw, t0, gid, li, t0, t1, cb0, sm_scale, mx, sc, sc_lds);
+        } else {
+            uint4 kB[U];
+            for (int c0 = t0; c0 < t1; c0 += 2 * CH) {
+                if (c0 + CH < t1) sdpa_load<U>(kB, K, kvb, c0 + CH, gid, t1);
+                sdpa_scores<U, ONE>(kA, qw, c0, gid, li, t0, t1, cb0, sm_scale, mx, sc, sc_lds);
+                if (c0 + 2 * CH < t1) sdpa_load<U>(kA, K, kvb, c0 + 2 * CH, gid, t1);
+                if (c0 + CH < t1) sdpa_scores<U, ONE>(kB, qw, c0 + CH, gid, li, t0, t1, cb0, sm_scale, mx, sc, sc_lds);
+            }
+            sdpa_load<U>(vA, V, kvb, t0, gid, t1);  // V chunks 0 and 1 in flight across the exchange
+            if (t0 + CH < t1) sdpa_load<U>(vB, V, kvb, t0 + CH, gid, t1);
+        }
+    }
+    WF_STAMP(1);
+    // ---- the exchange: per-block maxima of every split of this head ----
+    // Each split publishes one 8-byte granule {max, epoch} per 512-key block it covers (a split spans
+    // <= 3 blocks at T <= 1024) with an sc1 store; wave 0 polls the head's 3 NS granules with sc1
+    // loads until every tag is this launch's epoch (MI355X_MICROARCH.md handoff-1to1: data-tagged
+    // granules, no counter round trip). The epoch is the head's launch count, advanced by the
+    // head's merging block after every split has passed its poll.
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+        const float w = wave_max(mx[jj]);
+        if (lane == 0) red[wv][jj] = w;
+    }
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(wv) == 0) {  // wave 0 (a scalar branch: no exec-masked loop)
+        const unsigned ep = ld_sc1(xep + bh * kTailLine) + 1u;  // this launch's tag
+        float bmx[3];  // the block's maxima (constant LDS indices: uniform scalars)
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) {
+            bmx[jj] = red[0][jj];
+#pragma unroll
+            for (int w = 1; w < NWV; ++w) bmx[jj] = fmaxf(bmx[jj], red[w][jj]);
+        }
+        if (lane < 3) {
+            const float m = lane == 0 ? bmx[0] : (lane == 1 ? bmx[1] : bmx[2]);
+            st_sc1(xg + (bh * NS + s) * 3 + lane, ((uint64_t)ep << 32) | __float_as_uint(m));
+        }
+        // lanes 0 .. 3 NS - 1: split lane / 3, block cb0(split) + lane % 3
+        const int sp = lane / 3, ent = lane - 3 * sp;
+        uint64_t gv = ((uint64_t)ep << 32) | 0xff800000u;  // lanes past the granules: -inf, tagged
+        int ok = 1;
+        for (int it = 0;; ++it) {
+            if (lane < 3 * NS) gv = ld_sc1(xg + bh * NS * 3 + lane);
+            if (__all((unsigned)(gv >> 32) == ep)) break;
+            if (it > (1 << 20)) { ok = 0; break; }  // a missing sibling ends in NaN outputs, never a hang
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const float val = __uint_as_float((uint32_t)gv);
+        const int blk = lane < 3 * NS ? ((sp * T) >> 9) + ent : -1;
+        const int NB = (Sb + 511) >> 9;
+        const int cb1 = max(t1 - 1, t0) >> 9;
+        // prefix maxima, rescale factors and, for this split, the products of the factors after each
+        // of its blocks up to its last one (blk_r) and after its last block (fin_r): uniform loop
+        float M = -INFINITY, rr[3] = {1.f, 1.f, 1.f}, fin = 1.f;
+        for (int c = 0; c < NB; ++c) {
+            const float bmc = wave_max((blk == c) ? val : -INFINITY);
+            const float Mn = fmaxf(M, bmc);
+            const float r = (c == 0) ? 1.f : expf_rn(M - Mn);
+            M = Mn;
+            if (c > cb1) fin *= r;
+#pragma unroll
+            for (int jj = 0; jj < 3; ++jj)
+                if (c > cb0 + jj && c <= cb1) rr[jj] *= r;
+            if (lane == 0 && c >= cb0 && c < cb0 + 3) blk_m[c - cb0] = ok ? M : __uint_as_float(0x7fc00000u);
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int jj = 0; jj < 3; ++jj) blk_r[jj] = rr[jj];
+            fin_r = fin;
+        }
+    }
+    __syncthreads();
+    WF_STAMP(2);
+    // ---- probabilities and P.V ----
+    // block-uniform values read once into scalar registers (hipcc otherwise sank the LDS loads into
+    // the per-key selects and built a table of LDS addresses in scratch)
+    auto sload = [](const float& v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+    const SdpaBlocks bk{sload(blk_m[0]), sload(blk_m[1]), sload(blk_m[2]), sload(blk_r[0]), sload(blk_r[1]), sload(blk_r[2])};
+    float l = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (t0 < t1) {
+        if constexpr (ONE) {
+            sdpa_pv<U, ONE>(vA, sc, sc_lds, t0, gid, t0, t1, cb0, Sb, bk, l, o);
+        } else {
+            for (int c0 = t0; c0 < t1; c0 += 2 * CH) {
+                sdpa_pv<U, ONE>(vA, sc, sc_lds, c0, gid, t0, t1, cb0, Sb, bk, l, o);
+                if (c0 + 2 * CH < t1) sdpa_load<U>(vA, V, kvb, c0 + 2 * CH, gid, t1);
+                if (c0 + CH < t1) {
+                    sdpa_pv<U, ONE>(vB, sc, sc_lds, c0 + CH, gid, t0, t1, cb0, Sb, bk, l, o);
+                    if (c0 + 3 * CH < t1) sdpa_load<U>(vB, V, kvb, c0 + 3 * CH, gid, t1);
+                }
+            }
+        }
+    }
+    // ---- sum the lane groups (every record is in one frame: plain sums) ----
+    auto sum16 = [](float v) __attribute__((always_inline)) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    };
+    auto sum32 = [](float v) __attribute__((always_inline)) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    };
+    l = sum32(sum16(l));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = sum32(sum16(o[j]));
+    if (lane < LP) {
+        if (li == 0) sm_l[wv] = l;
+        *reinterpret_cast<float4*>(&sm_o[wv][li * 8]) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(&sm_o[wv][li * 8 + 4]) = make_float4(o[4], o[5], o[6], o[7]);
+    }
+    __syncthreads();
+    const float fr = sload(fin_r);
+    if (threadIdx.x < D / 4) {
+        const int d = 4 * threadIdx.x;
+        float ls = 0.f, os[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) {
+            ls += sm_l[w];
+            const float4 ov = *reinterpret_cast<const float4*>(&sm_o[w][d]);
+            os[0] += ov.x; os[1] += ov.y; os[2] += ov.z; os[3] += ov.w;
+        }
+        const int64_t rec = bh * NS + s;
+        st16_sc1(make_rsrc(o_out), (int)(4 * part_o_off<NS>(bh, s, d)),
+                 __builtin_bit_cast(uint4, make_float4(os[0] * fr, os[1] * fr, os[2] * fr, os[3] * fr)));
+        if (d == 0) st_sc1(reinterpret_cast<uint64_t*>(ml_out) + rec, __builtin_bit_cast(uint64_t, make_float2(0.f, ls * fr)));
+    }
+    WF_STAMP(3);
+    // ---- the head's last block sums the NS records into the bf16 attention row ----
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned* c = cnt + bh * kTailLine;
+        const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sh_last = (old == (unsigned)NS - 1u);
+        if (old == (unsigned)NS - 1u) {  // every split is past its poll: re-arm, advance the epoch
+            st_sc1(c, 0u);
+            st_sc1(xep + bh * kTailLine, ld_sc1(xep + bh * kTailLine) + 1u);
+        }
+    }
+    __syncthreads();
+    if (!sh_last || threadIdx.x >= D / 4) return;
+    const int d = 4 * threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rml = make_rsrc(ml_out), ro = make_rsrc(o_out);
+    float ll[NS];
+    float4 ov[NS];
+#pragma unroll
+    for (int u = 0; u < NS / 2; ++u) {
+        const float4 v = __builtin_bit_cast(float4, ld16_sc1(rml, (int)(8 * (bh * NS) + 16 * u)));
+        ll[2 * u] = v.y; ll[2 * u + 1] = v.w;
+    }
+#pragma unroll
+    for (int u = 0; u < NS; ++u) ov[u] = __builtin_bit_cast(float4, ld16_sc1(ro, (int)(4 * part_o_off<NS>(bh, u, d))));
+    float L = 0.f, O[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+        L += ll[u];
+        O[0] += ov[u].x; O[1] += ov[u].y; O[2] += ov[u].z; O[3] += ov[u].w;
+    }
+    const float inv = 1.0f / L;
+    *reinterpret_cast<uint2*>(row_out + bh * D + d) =
+        make_uint2(pk_bf16(O[0] * inv, O[1] * inv), pk_bf16(O[2] * inv, O[3] * inv));
+}
+
+__global__ __launch_bounds__(kAttnPartThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_attn_sdpa(const uint16_t* __restrict__ q, int64_t q_sb,
+                                                                const uint16_t* __restrict__ K,
+                                                                const uint16_t* __restrict__ V, int64_t kv_sb,
+                                                                int64_t kv_sh, int Hq, int Hkv, int S,
+                                                                const int32_t* __restrict__ seq_lens, float sm_scale,
+                                                                int b0, uint64_t* __restrict__ xg,
+                                                                float2* __restrict__ ml_out, float* __restrict__ o_out,
+                                                                uint16_t* __restrict__ row_out, unsigned* __restrict__ cnt,
+                                                                unsigned* __restrict__ xep) {
+    constexpr int NS = kAttnPartSplits1, NG = kAttnPartThreads / 16;
+    const int Sb = min(seq_lens[b0 + (int)blockIdx.z], S);
+    const int T = ((Sb + NS - 1) / NS + 15) / 16 * 16;
+    if (T <= kApUShort * NG)  // block-uniform: one load round holds the split
+        attn_sdpa_body<kApUShort, true>(q, q_sb, K, V, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, b0, xg, ml_out,
+                                        o_out, row_out, cnt, xep);
+    else
+        attn_sdpa_body<kApULong, false>(q, q_sb, K, V, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, b0, xg, ml_out,
+                                        o_out, row_out, cnt, xep);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Batched decode attention partials on the bf16 matrix cores (v_mfma_f32_16x16x32_bf16), on the
 // K / V caches in their tile layouts (wf_norm.h k_tile_off / v_tile_off; S % 32 == 0): every
 // fragment load is one contiguous KiB per wave. Same partial records as k_attn_part (a record holds
@@ -917,6 +1275,230 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
         }
         WF_STAMP(3);
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Batched decode attention (batch >= 16, tile-layout K/V) with the reference's SDPA arithmetic
+// (k_attn_sdpa's comment; oracle/wf_oracle.c orc_attention_sdpa_cpu_bf16): one block per (kv head
+// g, sequence b) walks the sequence's 512-key blocks in order, exactly the CPU kernel's loop, so
+// the running max needs no exchange between blocks of the launch. 4 waves; wave w takes tiles
+// w, w + 4, w + 8, w + 12 (32 keys each) of every 512-key block, in two passes:
+//   pass 1: K fragments -> QK on the bf16 matrix cores (k_attn_mfma's layouts: lane (head l16,
+//     quarter q4) holds the scores of keys base + 8 q4 + 0..7), the wave's per-head maximum;
+//     the four waves' maxima meet in LDS (one barrier per block) -> M_c, r_c = expf(M_{c-1} - M_c);
+//   pass 2: V fragments -> e = fexp_u20 / expf of (s - M_c) (vector part / tail of the block),
+//     l = l r_c + sum e (unrounded), acc = acc r_c + bf16(e) . V (ONE bf16 MFMA term: P IS bf16).
+// The fragment stream K(c, 0..3), V(c, 0..3), K(c + 1, 0..3) ... is double-buffered one tile ahead
+// (a tile past the sequence loads nothing and computes nothing). The block writes the normalised
+// bf16 attention row bf16(o * (1 / l)) of its group's heads into `row` [B][Hq * 128].
+// ---------------------------------------------------------------------------------------------
+template <int KV8>
+__global__ __launch_bounds__(256, 3) void k_attn_sdpa_mfma(const uint16_t* __restrict__ q, int64_t q_sb,
+                                                          const uint16_t* __restrict__ K, const uint16_t* __restrict__ Vt,
+                                                          int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv, int S,
+                                                          const int32_t* __restrict__ seq_lens, float sm_scale,
+                                                          const int32_t* __restrict__ pt, int pps, int npages,
+                                                          int64_t kv_pgs, float v_scale, uint16_t* __restrict__ row,
+                                                          const int32_t* __restrict__ order) {
+    constexpr int D = 128;
+    using KF = KvFrag<KV8>;
+    using FT = typename KF::T;
+    // blocks in longest-context-first order (k_seq_order; any permutation is correct, the order only
+    // balances ragged contexts over the CUs)
+    const int g = blockIdx.x, b = order ? min(max(order[blockIdx.y], 0), (int)gridDim.y - 1) : (int)blockIdx.y;
+    const int grp = Hq / Hkv, hq0 = g * grp;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
+    const int Sb = min(seq_lens[b], S);
+    const int NB = (Sb + 511) >> 9;
+    __shared__ float sm_mx[2][4][16];
+    // the wave's scores of its 4 tiles of the block (LDS, not registers: three blocks per CU instead
+    // of two); after the last block the same bytes hold the waves' output partials
+    __shared__ __attribute__((aligned(16))) union {
+        float x[4][4][8][64];
+        float o[4][kAttnMfmaMaxGrp][D];
+    } sm_u;
+    __shared__ float sm_l[4][kAttnMfmaMaxGrp];
+    const int64_t kvo = b * kv_sb + g * kv_sh + lane * 8;
+    const int32_t* ptb = pt ? pt + (int64_t)b * pps : nullptr;
+    WF_STAMP(0);
+
+    // the q fragments (B operand: column = query head of the group) live in LDS, read per tile: 16
+    // VGPRs fewer, three blocks per CU
+    __shared__ __attribute__((aligned(16))) uint4 sm_q[4][64];
+    {
+        const uint16_t* qp = q + b * q_sb + (int64_t)(hq0 + min(l16, grp - 1)) * D + 8 * q4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            uint4 t = *reinterpret_cast<const uint4*>(qp + 32 * c);
+            if (l16 >= grp) t = make_uint4(0, 0, 0, 0);
+            if (wave == 0) sm_q[c][lane] = t;
+        }
+    }
+    __syncthreads();
+    // step s of block c: pass s >> 2 (0 = K, 1 = V), tile base 512 c + 32 (wave + 4 (s & 3))
+    auto tbase = [&](int c, int s) { return 512 * c + 32 * (wave + 4 * (s & 3)); };
+    auto load = [&](FT (&f)[8], int c, int s) {
+        const int bs = tbase(c, s);
+        const int64_t blk = ptb ? (int64_t)min(max(ptb[__builtin_amdgcn_readfirstlane(bs) >> 5], 0), npages - 1) * kv_pgs
+                                : (int64_t)(bs >> 5) * 4096;
+        const uint16_t* base = (s >> 2) ? Vt : K;
+#pragma unroll
+        for (int n = 0; n < 8; ++n) f[n] = KF::ld(base, kvo + blk + n * 512);
+    };
+    float m_run = -INFINITY, l_run = 0.f;  // per lane: head l16 (m), the lane's quarter of the sum (l)
+    v4f_t acc[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[n] = v4f_t{0.f, 0.f, 0.f, 0.f};
+    FT fa[8], fb[8];
+    if (NB > 0 && tbase(0, 0) < Sb) load(fa, 0, 0);
+    for (int c = 0; c < NB; ++c) {
+        const int nb = min(512, Sb - 512 * c), vbnd = nb & ~15;
+        float wmx = -INFINITY;
+        float mblk = -INFINITY, r = 0.f;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            // the next step's fragments first (one tile ahead), into the other buffer
+            {
+                const int cn = s == 7 ? c + 1 : c, sn = (s + 1) & 7;
+                if (cn < NB && tbase(cn, sn) < Sb) {
+                    if (s & 1) load(fa, cn, sn);
+                    else load(fb, cn, sn);
+                }
+            }
+            if (s == 4) {  // the block's maxima: every wave's pass 1 is done
+                if (q4 == 0 && l16 < 16) sm_mx[c & 1][wave][l16] = wmx;
+                __syncthreads();
+                mblk = fmaxf(fmaxf(sm_mx[c & 1][0][l16], sm_mx[c & 1][1][l16]), fmaxf(sm_mx[c & 1][2][l16], sm_mx[c & 1][3][l16]));
+                const float mn = fmaxf(m_run, mblk);
+                r = (c == 0) ? 0.f : expf_rn(m_run - mn);
+                m_run = mn;
+                l_run *= r;
+                if (c > 0) {
+                    float ar[4];  // rescale of output row (head) 4 q4 + rr
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) ar[rr] = __shfl(r, 4 * q4 + rr, 64);
+#pragma unroll
+                    for (int n = 0; n < 8; ++n)
+#pragma unroll
+                        for (int rr = 0; rr < 4; ++rr) acc[n][rr] *= ar[rr];
+                }
+            }
+            const int bs = tbase(c, s);
+            if (bs >= Sb) continue;  // wave-uniform
+            const FT (&f)[8] = (s & 1) ? fb : fa;
+            const int i = s & 3;
+            const int lim = Sb - bs - 8 * q4;  // valid keys among this lane's 8
+            if (s < 4) {  // pass 1: scores
+                // the four 32-dim partial dots in separate accumulators, summed in f64 and rounded
+                // once: close to the exactly rounded dot of the reference's GEMM (one fp32
+                // accumulator chained through the four MFMAs moved 1.6 % of the outputs at 4096 keys;
+                // eight 16-dim partials (v_mfma_f32_16x16x16_bf16) measured 5 vs 9 of 40960 outputs off
+                // the oracle, but 20 bytes of scratch at three blocks per CU)
+#pragma unroll
+                for (int tau = 0; tau < 2; ++tau) {
+                    double dd[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int cc = 0; cc < 4; ++cc) {
+                        const v4f_t pr = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(v8s_t, KF::bf(f[tau * 4 + cc])), __builtin_bit_cast(v8s_t, sm_q[cc][lane]),
+                            v4f_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+                        for (int r4 = 0; r4 < 4; ++r4) dd[r4] += (double)pr[r4];
+                    }
+#pragma unroll
+                    for (int r4 = 0; r4 < 4; ++r4) {
+                        const int e = 4 * tau + r4;
+                        const float xv = e < lim ? (float)dd[r4] * sm_scale : -INFINITY;
+                        sm_u.x[wave][i][e][lane] = xv;
+                        wmx = fmaxf(wmx, xv);
+                    }
+                }
+                if (i == 3 || tbase(c, s + 1) >= Sb) {  // the wave's last tile of the block: its head maxima
+                    wmx = fmaxf(wmx, __shfl_xor(wmx, 16, 64));
+                    wmx = fmaxf(wmx, __shfl_xor(wmx, 32, 64));
+                }
+            } else {  // pass 2: probabilities and P.V
+                const int j0 = bs - 512 * c + 8 * q4;  // the lane's first key within the block
+                float p[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float xv = sm_u.x[wave][i][e][lane] - m_run;
+                    const float ev = e < lim ? ((j0 + e) < vbnd ? fexp_u20(xv) : expf_rn(xv)) : 0.f;
+                    l_run += ev;
+                    p[e] = ev;
+                }
+                const v8s_t ph = __builtin_bit_cast(v8s_t, make_uint4(pk_bf16(p[0], p[1]), pk_bf16(p[2], p[3]),
+                                                                      pk_bf16(p[4], p[5]), pk_bf16(p[6], p[7])));
+#pragma unroll
+                for (int n = 0; n < 8; ++n) {
+                    const v8s_t vf = __builtin_bit_cast(v8s_t, KF::bf(KF::mask(f[n], lim)));
+                    acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vf, acc[n], 0, 0, 0);
+                }
+            }
+        }
+    }
+    WF_STAMP(1);
+    __syncthreads();  // every wave is past its last score read: sm_u becomes the output partials
+    l_run += __shfl_xor(l_run, 16, 64);
+    l_run += __shfl_xor(l_run, 32, 64);
+    if (q4 == 0 && l16 < grp) sm_l[wave][l16] = l_run;
+#pragma unroll
+    for (int n = 0; n < 8; ++n)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+            if (4 * q4 + rr < grp) sm_u.o[wave][4 * q4 + rr][16 * n + l16] = acc[n][rr];
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < grp * (D / 4); idx += 256) {
+        const int h = idx / (D / 4), d = (idx % (D / 4)) * 4;
+        float ls = 0.f, os[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            ls += sm_l[w][h];
+            const float4 ov = *reinterpret_cast<const float4*>(&sm_u.o[w][h][d]);
+            os[0] += ov.x; os[1] += ov.y; os[2] += ov.z; os[3] += ov.w;
+        }
+        const float inv = 1.0f / ls;
+        float o4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o4[k] = KV8 ? (os[k] * v_scale) * inv : os[k] * inv;
+        *reinterpret_cast<uint2*>(row + (int64_t)b * Hq * D + (int64_t)(hq0 + h) * D + d) =
+            make_uint2(pk_bf16(o4[0], o4[1]), pk_bf16(o4[2], o4[3]));
+    }
+    WF_STAMP(2);
+}
+
+// The sequences of a batch by decreasing context (ties by index): one 1024-thread block, bitonic sort
+// of (length, index) keys in LDS, B <= 2048 (longer batches keep the identity order). Launched once
+// per decode step before the first layer's batched attention; every layer uses the order.
+__global__ __launch_bounds__(1024) void k_seq_order(const int32_t* __restrict__ seq_lens, int B, int S,
+                                                    int32_t* __restrict__ order) {
+    __shared__ uint32_t key[2048];
+    const int n = B <= 1024 ? 1024 : 2048;
+    for (int i = threadIdx.x; i < n; i += 1024) {
+        const uint32_t len = i < B ? (uint32_t)min(max(seq_lens[i], 0), S) : 0u;
+        // descending length = ascending (~len); pads (len 0, index >= B) sort last
+        key[i] = i < B ? ((~len & 0xffffu) << 16) | (uint32_t)i : 0xffff0000u | (uint32_t)i;
+    }
+    __syncthreads();
+    for (int k = 2; k <= n; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < n; i += 1024) {
+                const int p = i ^ j;
+                if (p > i) {
+                    const uint32_t a = key[i], c = key[p];
+                    const bool up = (i & k) == 0;
+                    if ((a > c) == up) { key[i] = c; key[p] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    for (int i = threadIdx.x; i < B; i += 1024) order[i] = (int32_t)(key[i] & 0xffffu);
+}
+
+int seq_order(const int32_t* seq_lens, int B, int S, int32_t* order, hipStream_t st) {
+    if (B > 2048 || S > 65535) return WF_OK;  // identity order stays (set at model creation)
+    hipLaunchKernelGGL(k_seq_order, dim3(1), dim3(1024), 0, st, seq_lens, B, S, order);
+    return check_launch("seq_order");
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1378,62 +1960,72 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
                               float2* ml, float* o, hipStream_t st, bool kv_tiled, const int32_t* pt, int pps,
                               int npages, int64_t kv_pgs, int kv8, float k_scale, float v_scale, const AttnTail* tail,
-                              uint16_t* merged_row, unsigned* merge_cnt) {
+                              uint16_t* merged_row, unsigned* merge_cnt, uint64_t* xmax, const int32_t* order) {
     const int grp = Hq / Hkv;
     if (grp > 8) {
         set_error("decode_attention_partials: GQA group %d > 8", grp);
         return WF_EINVAL;
     }
-    if (B < 16) {
-        // one block per query head (G = 1): 4x the blocks of one per kv head at Hq/Hkv = 4, a quarter
-        // of the per-lane arithmetic (at batch 1 the kernel is latency-bound on its score/softmax
-        // chain; the K/V re-reads of the group's heads hit L2)
-        hipLaunchKernelGGL((k_attn_part<1, kAttnPartSplits1>), dim3(kAttnPartSplits1, Hq, B), dim3(kAttnPartThreads), 0, st, q, q_sb, k, v,
-                           kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, ml, o, merged_row, merge_cnt);
-        return check_launch("decode_attention_partials");
-    }
-    // batched: one block per kv head, the group's query heads share every K/V load (KV-bound)
-    const dim3 grid(kAttnPartSplits, Hkv, B);
-    if (kv_tiled) {  // tile-layout caches: matrix-core kernel
-        if (S % 32 != 0) {
-            set_error("decode_attention_partials: tiled K/V need S %% 32 == 0 (S=%d)", S);
+    if (B < 16 || !kv_tiled) {
+        // the reference's SDPA semantics (k_attn_sdpa): one block per (split, query head, sequence),
+        // the head's records merged into the bf16 row merged_row in the launch
+        if (!merged_row || !merge_cnt || !xmax || pt) {
+            set_error("decode_attention_partials: batch < 16 / untiled caches need the merged-row buffers, no page table");
             return WF_EINVAL;
         }
-        if (tail && Hq * 128 > 4096) {
-            set_error("decode_attention_partials: the fused row norm handles Hq * 128 <= 4096 (Hq=%d)", Hq);
+        if (S > kSdpaMaxSeq) {
+            set_error("decode_attention_partials: max_seq %d > %d at batch < 16 / untiled caches", S, kSdpaMaxSeq);
             return WF_EINVAL;
         }
-        const AttnTail tl = tail ? *tail : AttnTail{};
-#ifndef WF_KV8_DB  // study: 1 = double-buffered tiles (2 waves per SIMD) for the FP8 / INT8 caches too
-#define WF_KV8_DB 0
-#endif
-        constexpr bool kKv8Db = WF_KV8_DB;
-#define WF_AM(DBV, KV8V, TAILV, SCALE, VSC)                                                                        \
-    hipLaunchKernelGGL((k_attn_mfma<DBV, false, false, KV8V, false, TAILV>), grid, dim3(256), 0, st, q, q_sb, k, v, \
-                       kv_sb, kv_sh, Hq, Hkv, S, seq_lens, SCALE, ml, o, pt, pps, npages, kv_pgs, VSC, tl)
-        if (kv8 == 2) {  // int8 caches: as FP8, a wider in-register decode
-            if (tail) WF_AM(false, 2, true, sm_scale * k_scale, v_scale);
-            else WF_AM(kKv8Db, 2, false, sm_scale * k_scale, v_scale);
-        } else if (kv8) {  // FP8 caches: K scale folded into the score scale; one tile in flight per wave, 4 waves per SIMD
-            if (tail) WF_AM(false, 1, true, sm_scale * k_scale, v_scale);
-            else WF_AM(kKv8Db, 1, false, sm_scale * k_scale, v_scale);
-        } else {  // bf16: double-buffered tiles, 2 waves per SIMD (at 4 splits a wave takes >= 2 tiles at ctx >= 1024)
-            if (tail) WF_AM(true, 0, true, sm_scale, 1.0f);
-            else WF_AM(true, 0, false, sm_scale, 1.0f);
+        // every split of a head polls its siblings: a launch holds only blocks the chip keeps resident
+        // at once (half the occupancy API's count), whole sequences per launch
+        static int cap = 0;
+        if (!cap) {
+            int dev = 0, ncu = 0, per = 0;
+            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_attn_sdpa, kAttnPartThreads, 0) != hipSuccess) {
+                set_error("decode_attention_partials: occupancy query failed");
+                return WF_EHIP;
+            }
+            cap = std::max(1, per * ncu / 2);
         }
-#undef WF_AM
-        return check_launch("decode_attention_partials");
+        const int per_seq = kAttnPartSplits1 * Hq;
+        if (per_seq > cap) {
+            set_error("decode_attention_partials: %d blocks per sequence exceed the resident bound %d", per_seq, cap);
+            return WF_EINVAL;
+        }
+        const int chunk = std::max(1, cap / per_seq);
+        unsigned* xep = merge_cnt + (int64_t)B * Hq * kTailLine;  // per-head launch epochs
+        for (int b0 = 0; b0 < B; b0 += chunk) {
+            hipLaunchKernelGGL(k_attn_sdpa, dim3(kAttnPartSplits1, Hq, std::min(chunk, B - b0)), dim3(kAttnPartThreads), 0, st,
+                               q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, b0, xmax, ml, o, merged_row,
+                               merge_cnt, xep);
+            if (int rc = check_launch("decode_attention_partials")) return rc;
+        }
+        return WF_OK;
     }
-    // batch >= 16 on untiled caches (TQ weights, or max_seq % 32 != 0): the VALU kernel, one block per
-    // kv head, with the batched record count (the reader, k_rownorm_attn, merges kAttnPartSplits)
-#define WF_AP(GV)                                                                                                   \
-    hipLaunchKernelGGL((k_attn_part<GV, kAttnPartSplits>), grid, dim3(kAttnPartThreads), 0, st, q, q_sb, k, v, kv_sb,  \
-                       kv_sh, Hq, Hkv, S, seq_lens, sm_scale, ml, o, nullptr, nullptr)
-    if (grp == 1) WF_AP(1);
-    else if (grp == 2) WF_AP(2);
-    else if (grp <= 4) WF_AP(4);
-    else WF_AP(8);
-#undef WF_AP
+    // batched, tile-layout caches: one block per (kv head, sequence) walking its 512-key blocks in
+    // order (k_attn_sdpa_mfma), the normalised bf16 rows into merged_row
+    if (S % 32 != 0) {
+        set_error("decode_attention_partials: tiled K/V need S %% 32 == 0 (S=%d)", S);
+        return WF_EINVAL;
+    }
+    if (!merged_row || grp > kAttnMfmaMaxGrp) {
+        set_error("decode_attention_partials: batched attention needs the merged-row buffer and a GQA group <= %d",
+                  kAttnMfmaMaxGrp);
+        return WF_EINVAL;
+    }
+    (void)tail;
+    const dim3 grid(Hkv, B);
+    if (kv8 == 2)
+        hipLaunchKernelGGL(k_attn_sdpa_mfma<2>, grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, seq_lens,
+                           sm_scale * k_scale, pt, pps, npages, kv_pgs, v_scale, merged_row, order);
+    else if (kv8)
+        hipLaunchKernelGGL(k_attn_sdpa_mfma<1>, grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, seq_lens,
+                           sm_scale * k_scale, pt, pps, npages, kv_pgs, v_scale, merged_row, order);
+    else
+        hipLaunchKernelGGL(k_attn_sdpa_mfma<0>, grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, seq_lens,
+                           sm_scale, pt, pps, npages, kv_pgs, 1.0f, merged_row, order);
     return check_launch("decode_attention_partials");
 }
 

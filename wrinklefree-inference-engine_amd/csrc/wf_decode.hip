@@ -38,7 +38,9 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
                               float2* ml, float* o, hipStream_t st, bool kv_tiled, const int32_t* pt = nullptr,
                               int pps = 0, int npages = 0, int64_t kv_pgs = 0, int kv8 = 0, float k_scale = 1.f,
                               float v_scale = 1.f, const AttnTail* tail = nullptr, uint16_t* merged_row = nullptr,
-                              unsigned* merge_cnt = nullptr);
+                              unsigned* merge_cnt = nullptr, uint64_t* xmax = nullptr,
+                              const int32_t* order = nullptr);
+int seq_order(const int32_t* seq_lens, int B, int S, int32_t* order, hipStream_t st);
 
 // study switches (same-box A/B builds, tools/build_var.sh; measured r04, profiles/ab_r04.txt):
 // WF_NO_XTOK restores the batch-1 embed launch (-0.5 %); WF_OLD_EPI the LDS-round O/DN epilogue
@@ -2157,7 +2159,9 @@ struct wf_model {
     unsigned* tickets = nullptr;
     unsigned* seam = nullptr;  // fused row-norm hand-off words (k_dec_gemm_t PRO), zero between launches
     unsigned* attn_cnt = nullptr;  // batched attention tail: one arrival counter per sequence (kTailLine apart)
-    uint16_t* attn_row = nullptr;  // batch < 16: the merged bf16 attention rows [B][H] (kMerge1)
+    uint16_t* attn_row = nullptr;  // batch < 16 / untiled caches: the merged bf16 attention rows [B][H] (kMerge1)
+    uint64_t* attn_xmax = nullptr;  // k_attn_sdpa's exchange: {max, epoch} granules [B][Hq][splits][3]
+    int32_t* attn_order = nullptr;  // batched attention: sequences by decreasing context (k_seq_order)
     int fuse[4] = {0, 0, 0, 0};  // per GEMM op (QKV, O, GU, DN): row norm fused into the GEMM launch
     uint2* am_part = nullptr;
     int lm_blocks = 0;
@@ -2453,6 +2457,12 @@ bool attn_tail_on(const wf_model* m) {
     return kAttnTail && m->d.batch >= 16 && m->kv_tiled && m->attn_cnt && m->d.n_heads * m->d.head_dim <= 4096 && !m->fuse[1];
 }
 
+// the attention merges each head's records into the bf16 row m->attn_row (k_attn_sdpa: batch < 16 and
+// untiled caches); the O input then reads that row
+bool attn_merged(const wf_model* m) { (void)m; return true; }
+// the attention also leaves per-split (m, l, o) records (k_attn_sdpa; include/wf_bitnet.h attn view)
+bool attn_records(const wf_model* m) { return m->d.batch < 16 || !m->kv_tiled; }
+
 // One op of the decode step (WF_OP_* in include/wf_bitnet.h).
 int run_op(wf_model* m, int l, int op, hipStream_t st) {
     const wf_model_desc& d = m->d;
@@ -2476,33 +2486,38 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             }
             return launch_gemv_fmt<MODE_QKV, kLprQKV>(d.wfmt, a, st);
         case WF_OP_ATTN: {  // split partials; merged by the O projection's input stage or the tail
+            if (m->kv_tiled && B >= 16 && l == 0 && (rc = seq_order(m->seq_lens, B, S, m->attn_order, st))) return rc;
             // batch >= 16 on tile-layout caches: the attention's last block per sequence forms the O
             // input row (AttnTail) instead of a k_rownorm_attn launch
             AttnTail tail{d.attn_sub + (int64_t)l * H, d.eps, m->q8, m->act_sf, m->act_sum, m->attn_cnt};
             const AttnTail* tp = attn_tail_on(m) ? &tail : nullptr;
-            uint16_t* mrow = (kMerge1 && B < 16) ? m->attn_row : nullptr;
+            uint16_t* mrow = attn_merged(m) ? m->attn_row : nullptr;
             unsigned* mcnt = mrow ? m->attn_cnt : nullptr;
             if (a.pt)  // paged pool: kv head stride 32 * D inside a page
                 return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, 0, 32 * D, B, d.n_heads,
                                                  d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D), m->part_ml,
                                                  m->part_o, st, true, a.pt, a.pps, a.npages, a.kv_pgs, d.kv_quant,
-                                                 m->kv_scale[2 * l], m->kv_scale[2 * l + 1], tp, mrow, mcnt);
+                                                 m->kv_scale[2 * l], m->kv_scale[2 * l + 1], tp, mrow, mcnt, m->attn_xmax,
+                                                 m->attn_order);
             return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, a.kv_b_stride, (int64_t)S * D,
                                              B, d.n_heads, d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D),
                                              m->part_ml, m->part_o, st, m->kv_tiled != 0, nullptr, 0, 0, 0, d.kv_quant,
                                              d.kv_quant ? m->kv_scale[2 * l] : 1.f, d.kv_quant ? m->kv_scale[2 * l + 1] : 1.f,
-                                             tp, mrow, mcnt);
+                                             tp, mrow, mcnt, m->attn_xmax, m->attn_order);
         }
         case WF_OP_O:  // h_b = h_a + o_proj(rms_norm(attn_sub_norm)(attn))
             a.w = d.w_o + (int64_t)l * H * wrow_bytes(d.wfmt, H); a.N = H; a.K = H; a.ws0 = wsh[3];
             a.resid = m->h_a; a.out = m->h_b; a.out_stride = H;
             if (kXTok && B == 1 && l == 0) { a.resid = d.embed; a.x_tok = m->tokens; a.vocab = d.vocab; }
-            if (kMerge1 && B < 16) { a.x = m->attn_row; a.x_stride = H; }
+            if (attn_merged(m)) { a.x = m->attn_row; a.x_stride = H; }
             a.nw = d.attn_sub + (int64_t)l * H;
             a.part_ml = m->part_ml;
             a.part_o = m->part_o;
             if (m->fuse[1]) return launch_gemv_fmt<MODE_O, kLprO>(d.wfmt, a, st, 2);
-            if (B > 1 && !attn_tail_on(m)) {
+            if (B > 1 && attn_merged(m)) {  // the merged bf16 rows: the plain row norm
+                launch_rownorm(m, m->attn_row, H, a.nw, H, nullptr, st);
+                if ((rc = check_launch("rownorm_attn_row"))) return rc;
+            } else if (B > 1 && !attn_tail_on(m)) {
 // the records of decode_attention_partials: kAttnPartSplits1 per head below batch 16, else kAttnPartSplits
 #define WF_RA(PPTV, TL, NS)                                                                                                 \
     hipLaunchKernelGGL((k_rownorm_attn<PPTV, TL, NS>), dim3(B), dim3(kNT), 0, st, m->part_ml, m->part_o, d.n_heads, a.nw, \
@@ -2675,14 +2690,25 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_ALLOC(m->tickets, sizeof(unsigned) * kTicketWords * TK_COUNT);
     WF_ALLOC(m->seam, sizeof(unsigned) * 2 * kSeamTiles * kSeamLine);
     // arrival lines: one per sequence (batched tail) or per (sequence, head) (kMerge1)
-    WF_ALLOC(m->attn_cnt, sizeof(unsigned) * (size_t)B * d.n_heads * kTailLine);
-    if (kMerge1) WF_ALLOC(m->attn_row, 2 * (size_t)B * d.hidden);
+    // (the second half: k_attn_sdpa's exchange counters)
+    WF_ALLOC(m->attn_cnt, 2 * sizeof(unsigned) * (size_t)B * d.n_heads * kTailLine);
+    WF_ALLOC(m->attn_row, 2 * (size_t)B * d.hidden);
+    WF_ALLOC(m->attn_xmax, sizeof(uint64_t) * 3 * (size_t)B * d.n_heads * kAttnPartSplits1);
+    WF_ALLOC(m->attn_order, sizeof(int32_t) * (size_t)B);
+    {  // identity order until the first step sorts the batch
+        std::vector<int32_t> id(B);
+        for (int b = 0; b < B; ++b) id[b] = b;
+        if ((e = hipMemcpy(m->attn_order, id.data(), sizeof(int32_t) * B, hipMemcpyHostToDevice)) != hipSuccess) return fail(e);
+    }
     WF_ALLOC(m->am_part, sizeof(uint2) * B * m->lm_blocks);
 #undef WF_ALLOC
     // tickets start at zero; every launch re-arms the ones it uses
     if ((e = hipMemset(m->tickets, 0, sizeof(unsigned) * kTicketWords * TK_COUNT)) != hipSuccess) return fail(e);
     if ((e = hipMemset(m->seam, 0, sizeof(unsigned) * 2 * kSeamTiles * kSeamLine)) != hipSuccess) return fail(e);
-    if ((e = hipMemset(m->attn_cnt, 0, sizeof(unsigned) * (size_t)B * d.n_heads * kTailLine)) != hipSuccess) return fail(e);
+    if ((e = hipMemset(m->attn_cnt, 0, 2 * sizeof(unsigned) * (size_t)B * d.n_heads * kTailLine)) != hipSuccess) return fail(e);
+    // granule tags start at 0; the first launch's epoch is 1
+    if ((e = hipMemset(m->attn_xmax, 0, sizeof(uint64_t) * 3 * (size_t)B * d.n_heads * kAttnPartSplits1)) != hipSuccess)
+        return fail(e);
     fused_norm_plan(m);
     if ((e = hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking)) != hipSuccess) return fail(e);
     *out = m;
@@ -2694,7 +2720,7 @@ int wf_model_destroy(wf_model* m) {
     if (m->exec) (void)hipGraphExecDestroy(m->exec);
     if (m->graph) (void)hipGraphDestroy(m->graph);
     if (m->cap) (void)hipStreamDestroy(m->cap);
-    void* ptrs[] = {m->attn_cnt, m->attn_row, m->seq_lens, m->h_a, m->h_b, m->qbuf, m->part_ml, m->part_o, m->hn, m->act, m->q8, m->dec_ws,
+    void* ptrs[] = {m->attn_cnt, m->attn_row, m->attn_xmax, m->attn_order, m->seq_lens, m->h_a, m->h_b, m->qbuf, m->part_ml, m->part_o, m->hn, m->act, m->q8, m->dec_ws,
                     m->act_sf, m->act_sum, m->tickets, m->seam, m->am_part, m->embed_t, m->pf_h_a, m->pf_h_b, m->pf_q,
                     m->pf_attn, m->pf_act, m->pf_q8, m->pf_sf, m->pf_asum, m->pf_seq};
     for (void* p : ptrs)
@@ -2727,7 +2753,8 @@ int wf_model_attn_view(const wf_model* m, wf_attn_records* out) {
     out->q = m->qbuf;
     out->part_ml = reinterpret_cast<const float*>(m->part_ml);
     out->part_o = m->part_o;
-    out->records = m->d.batch < 16 ? kAttnPartSplits1 : kAttnPartSplits;
+    out->records = attn_records(m) ? kAttnPartSplits1 : 0;
+    out->attn_row = attn_merged(m) ? m->attn_row : nullptr;
     return WF_OK;
 }
 

@@ -86,7 +86,8 @@ class WFModelDesc(C.Structure):
 
 class WFAttnView(C.Structure):
     """Mirror of wf_attn_records (include/wf_bitnet.h wf_model_attn_view)."""
-    _fields_ = [("q", C.c_void_p), ("part_ml", C.c_void_p), ("part_o", C.c_void_p), ("records", C.c_int)]
+    _fields_ = [("q", C.c_void_p), ("part_ml", C.c_void_p), ("part_o", C.c_void_p), ("records", C.c_int),
+                ("attn_row", C.c_void_p)]
 
 
 class KernelError(RuntimeError):

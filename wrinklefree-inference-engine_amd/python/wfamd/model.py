@@ -499,6 +499,19 @@ class BitNetDecoder:
         o = o.view(B, Hq, R, D)[..., idx]
         return q, ml, o
 
+    def attention_row(self):
+        """The merged bf16 attention output the O projection reads after WF_OP_ATTN ([B, Hq, D]), on
+        the paths whose attention merges its records in the launch (batch < 16, untiled caches:
+        include/wf_bitnet.h wf_attn_records.attn_row); None on the batched tile-layout path."""
+        v = _lib.WFAttnView()
+        call("wf_model_attn_view", self._h, C.addressof(v))
+        if not v.attn_row:
+            return None
+        cfg = self.cfg
+        row = torch.empty(self.batch, cfg.n_heads, cfg.head_dim, dtype=torch.bfloat16, device=self.dev)
+        ops.device_copy(row.data_ptr(), v.attn_row, row.numel() * 2)
+        return row
+
     @property
     def fused_norm(self) -> tuple:
         """(QKV, O, gate|up, down): which batched GEMMs normalise their input rows inside the GEMM
