@@ -435,9 +435,10 @@ def test_prefill_8x2048_full_width_vs_oracle(orc):
     within an fp32 rounding of a bf16 boundary the two round apart, the int8 requantisation
     downstream (attn_sub_norm, ffn_sub_norm) turns that into whole code steps, and that one
     position's layer-1 K/V moves by ~1e-2 while its neighbours stay bit-exact. Measured at 2048
-    positions (tools/diag_prefill.py --n 2048 --oracle --trained --batch 1): batch-1 decode 32
-    positions, rel-L2 2.95e-3; prefill 41, 3.29e-3 (with P.V in two bf16 terms instead of three:
-    71, 4.28e-3)."""
+    positions (tools/diag_prefill.py --n 2048 --oracle --trained --batch 1; round 3, exact-softmax
+    attention): batch-1 decode 32 positions, rel-L2 2.95e-3; prefill 41, 3.29e-3. Since round 5 the
+    oracle and every GPU attention follow the reference's CPU bf16 SDPA (orc_attention_sdpa_cpu_bf16,
+    k_attn_prefill_sdpa)."""
     from wfamd.model import BitNetDecoder
     cfg = make_cfg(2, 128256, 2080)
     w = make_weights(cfg, seed=6, trained_like=True)
@@ -465,7 +466,7 @@ def test_prefill_8x2048_full_width_vs_oracle(orc):
         return int((per > 1e-3).sum()), max(rel_l2(kg, kr), rel_l2(vg, vr)), per.max()
 
     for b, npos in ((0, n), (5, 512)):
-        m = orc.DecodeModel(a)
+        m = orc.DecodeModel(a, attn_mode=1)  # the reference's SDPA, as every GPU attention path
         for t in range(npos):
             m.step(prompts[b][t], t, logits=False)
         for l in range(cfg.layers):

@@ -1917,6 +1917,226 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __re
     }
 }
 
+// Prefill attention with the reference's SDPA arithmetic (k_attn_sdpa's comment): the decode loop
+// the reference runs for a prompt computes each position's attention over keys [0, pos] in 512-key
+// blocks with a running max. Same block / wave / lane layout, LDS-DMA ring and XCD-chunked order as
+// k_attn_prefill_fa, but per 512-key block two passes over its tiles:
+//   pass 1 (ring stages of TWO tiles' K): S^T = K . Q^T (two 64-dim partial MFMA chains summed in f64
+//     and rounded once), the column's block maximum (causal limit per column);
+//   then M_c = max(M_{c-1}, block max), r = expf(M_{c-1} - M_c) rescales the column's O^T and l;
+//   pass 2 (stages of one tile's K + V): the same S^T again, e = fexp_u20 / expf of (s - M_c) (the
+//     16-key vector part / the tail of the column's block), l += e, O^T += V^T . bf16(e)^T (one MFMA
+//     term per k-step: P is bf16, 24 instead of 32 MFMAs per tile).
+// Every stage is 16 KiB and four 1-KiB DMAs per wave, so the ring's vmcnt accounting is unchanged.
+__global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __restrict__ q, int64_t q_rs,
+                                                              const uint16_t* __restrict__ K,
+                                                              const uint16_t* __restrict__ Vt, int64_t kv_sb,
+                                                              int64_t kv_sh, const int32_t* __restrict__ row_pos,
+                                                              const int32_t* __restrict__ row_slot, int M,
+                                                              float scale, const int32_t* __restrict__ pt, int pps,
+                                                              int npages, int64_t kv_pgs, uint16_t* __restrict__ out,
+                                                              int64_t o_rs, int xchunk) {
+    constexpr int D = 128, P = kFaStages;
+    constexpr int kSlot = 16384;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[P * kSlot];
+    __shared__ int s_page[kPfMaxTiles];
+    const int nrb = M / 32;
+    int g, rbi;
+    if (xchunk > 0) {
+        const int b = blockIdx.x, item = (b & 7) * xchunk + (xchunk - 1 - (b >> 3));
+        g = item / nrb;
+        rbi = item - g * nrb;
+    } else {
+        g = blockIdx.y;
+        rbi = nrb - 1 - (int)blockIdx.x;
+    }
+    const int hq0 = g * 4;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
+    const int rb = rbi * 32;
+    const int slot = __builtin_amdgcn_readfirstlane(row_slot[rb]);
+    const int qrow = rb + 8 * wave + (c >> 2);
+    const int lim_q = row_pos[qrow] + 1;  // keys [0, lim_q) of column c
+    int lim_b = 0;
+    for (int t = 0; t < 32; ++t) lim_b = max(lim_b, row_pos[rb + t] + 1);
+    lim_b = __builtin_amdgcn_readfirstlane(min(lim_b, 32 * min(pps, kPfMaxTiles)));
+    v8bf_t qf[8];  // Q^T fragments: column c, dims 16 s + 8 h .. + 7
+    {
+        const uint16_t* qp = q + (int64_t)qrow * q_rs + (int64_t)(hq0 + (c & 3)) * D + 8 * h;
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2) qf[s2] = __builtin_bit_cast(v8bf_t, *reinterpret_cast<const uint4*>(qp + 16 * s2));
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 8; ++s2) asm volatile("" : "+v"(qf[s2]));
+    const int ntiles = (lim_b + 31) >> 5;
+    const int NB = (ntiles + 15) >> 4;
+    const uint16_t* Kg = K + (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;
+    const uint16_t* Vg = Vt + (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;
+    if (pt) {
+        for (int t = threadIdx.x; t < ntiles; t += 256) s_page[t] = min(max(pt[(int64_t)slot * pps + t], 0), npages - 1);
+        __syncthreads();
+    }
+    // stage i -> (block, pass, tiles): a full block has 8 pass-1 stages (two tiles' K each) then 16
+    // pass-2 stages (one tile's K + V); the last block s1 = ceil(nt / 2) + nt
+    const int nt_last = ntiles - 16 * (NB - 1), s1_last = (nt_last + 1) >> 1;
+    const int nstages = 24 * (NB - 1) + s1_last + nt_last;
+    auto stage_of = [=](int i, int& cb, int& pass, int& ta, int& tb) __attribute__((always_inline)) {
+        cb = min(i / 24, NB - 1);
+        const int j = i - 24 * cb;
+        const int nt = cb == NB - 1 ? nt_last : 16, s1 = (nt + 1) >> 1;
+        if (j < s1) {
+            pass = 1;
+            ta = 16 * cb + 2 * j;
+            tb = min(ta + 1, 16 * cb + nt - 1);
+        } else {
+            pass = 2;
+            ta = tb = 16 * cb + (j - s1);
+        }
+    };
+    auto issue = [=](int i) __attribute__((always_inline)) {
+        int cb, pass, ta, tb;
+        stage_of(i, cb, pass, ta, tb);
+        const int64_t ba = pt ? (int64_t)s_page[ta] * kv_pgs : (int64_t)ta * 4096;
+        const int64_t bb = pt ? (int64_t)s_page[tb] * kv_pgs : (int64_t)tb * 4096;
+        uint8_t* st = ring + (i % P) * kSlot;
+        const uint16_t* second = pass == 1 ? Kg + bb : Vg + bb;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int j = wave * 4 + jj;
+            glds16_asm(j < 8 ? Kg + ba + j * 512 : second + (j - 8) * 512, st + j * 1024);
+        }
+    };
+    const int o = (c & ~12) | ((c & 4) << 1) | ((c & 8) >> 1);
+    const int koff = ((((o >> 2) & 1) * 16 + h) * 16 + 4 * (o >> 3) + (o & 3)) * 16;
+    // S^T of one tile in natural units: two 64-dim partial MFMA chains, summed in f64, rounded once
+    auto qk = [=](const uint8_t* st, float (&x)[16]) __attribute__((always_inline)) {
+        uint4 kf[8];
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2) kf[s2] = *reinterpret_cast<const uint4*>(st + koff + s2 * 512);
+        v16f_t a0, a1;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) { a0[e] = 0.f; a1[e] = 0.f; }
+#pragma unroll
+        for (int s2 = 0; s2 < 8; s2 += 2) {
+            a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf_t, kf[s2]), qf[s2], a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf_t, kf[s2 + 1]), qf[s2 + 1], a1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) x[e] = (float)((double)a0[e] + (double)a1[e]) * scale;
+    };
+    float m_run = -INFINITY, l_run = 0.f, bmax = -INFINITY;
+    v16f_t oacc[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) oacc[mt][e] = 0.f;
+#pragma unroll
+    for (int i = 0; i < P - 1; ++i)
+        if (i < nstages) issue(i);
+    auto wait_through = [=](int i, int last_issued) __attribute__((always_inline)) {
+        const int pending = min(nstages - 1, last_issued) - i;
+        if (pending <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (pending == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if (pending == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    };
+    for (int i = 0; i < nstages; ++i) {
+        wait_through(i, i + P - 2);  // stage i landed, and everyone is done with stage i - 1's slot
+        if (i + P - 1 < nstages) issue(i + P - 1);
+        int cb, pass, ta, tb;
+        stage_of(i, cb, pass, ta, tb);
+        const uint8_t* st = ring + (i % P) * kSlot;
+        const int blk0 = 512 * cb;
+        if (pass == 1) {
+            // this column's maximum over its keys of the stage's tiles
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int t = u ? tb : ta;
+                if (u && tb == ta) break;  // wave-uniform
+                if (32 * t >= lim_b) break;
+                float x[16];
+                qk(st + u * 8192, x);
+                const int lim = lim_q - 32 * t - 8 * h;
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if ((j & 7) + 16 * (j >> 3) < lim) bmax = fmaxf(bmax, x[j]);
+            }
+            const int nt = cb == NB - 1 ? nt_last : 16, s1 = (nt + 1) >> 1;
+            if (i - 24 * cb == s1 - 1) {  // the block's last pass-1 stage: M_c, rescale O and l
+                const float mn = fmaxf(m_run, swap32_max(bmax));
+                const float r = expf_rn(m_run - mn);  // 0 before the first block, 1 if no key of it
+                m_run = mn;
+                bmax = -INFINITY;
+                l_run *= r;
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) oacc[mt][e] *= r;
+            }
+        } else {
+            const int bs = 32 * ta;
+            if (bs >= lim_b) continue;  // wave-uniform (the block's tiles past the group's last row)
+            uint4 vv[4][2];  // V^T fragments (dim 32 mt + c, keys 16 s + 8 h + 0..7): issued first
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const int d = 32 * mt + c, n = d >> 4, l = d & 15;
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2)
+                    vv[mt][s2] = *reinterpret_cast<const uint4*>(st + 8192 + ((n * 4 + 2 * s2 + h) * 16 + l) * 16);
+            }
+            float x[16];
+            qk(st, x);
+            const int lim = lim_q - bs - 8 * h;
+            const int nbc = min(512, lim_q - blk0), vbnd = nbc & ~15;  // the column's block: vector part
+            uint32_t pk[8];
+#pragma unroll
+            for (int j = 0; j < 16; j += 2) {
+                float e2[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int kk = (j + u & 7) + 8 * h + 16 * ((j + u) >> 3);  // key within the tile
+                    const int kb = bs - blk0 + kk;                             // key within the block
+                    const float xv = x[j + u] - m_run;
+                    const float ev = kk < lim + 8 * h ? (kb < vbnd ? fexp_u20(xv) : expf_rn(xv)) : 0.f;
+                    l_run += ev;
+                    e2[u] = ev;
+                }
+                pk[j >> 1] = pk_bf16(e2[0], e2[1]);
+            }
+            const v8bf_t pb0 = __builtin_bit_cast(v8bf_t, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+            const v8bf_t pb1 = __builtin_bit_cast(v8bf_t, make_uint4(pk[4], pk[5], pk[6], pk[7]));
+            const int limv = lim_b - bs - 8 * h;  // V keys past the block's last position: zero (stale)
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    uint4 a = vv[mt][s2];
+                    if (limv < 32) {
+                        const int k0 = 16 * s2;
+                        a.x &= (k0 < limv ? 0xffffu : 0u) | (k0 + 1 < limv ? 0xffff0000u : 0u);
+                        a.y &= (k0 + 2 < limv ? 0xffffu : 0u) | (k0 + 3 < limv ? 0xffff0000u : 0u);
+                        a.z &= (k0 + 4 < limv ? 0xffffu : 0u) | (k0 + 5 < limv ? 0xffff0000u : 0u);
+                        a.w &= (k0 + 6 < limv ? 0xffffu : 0u) | (k0 + 7 < limv ? 0xffff0000u : 0u);
+                    }
+                    oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf_t, a), s2 ? pb1 : pb0,
+                                                                       oacc[mt], 0, 0, 0);
+                }
+            }
+        }
+    }
+    const float inv = 1.0f / swap32_sum(l_run);
+    if (qrow < M) {
+        uint16_t* orow = out + (int64_t)qrow * o_rs + (int64_t)(hq0 + (c & 3)) * D;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)  // dims 32 mt + 8 u + 4 h .. + 3
+                *reinterpret_cast<uint2*>(orow + 32 * mt + 8 * u + 4 * h) =
+                    make_uint2(pk_bf16(oacc[mt][4 * u] * inv, oacc[mt][4 * u + 1] * inv),
+                               pk_bf16(oacc[mt][4 * u + 2] * inv, oacc[mt][4 * u + 3] * inv));
+    }
+}
+
 // Contract of prefill_attention, checked by wf_model_prefill before its first launch (so a refused
 // call leaves the cache untouched).
 int prefill_attention_check(int Hq, int Hkv, int pps) {
@@ -1939,9 +2159,8 @@ int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const 
     if (!kv8 && pps <= kPfMaxTiles && M % 32 == 0) {
         const int items = (M / 32) * Hkv, xchunk = items % 8 == 0 ? items / 8 : 0;
         const dim3 grid = xchunk ? dim3(items) : dim3(M / 32, Hkv);
-        const float sl2 = sm_scale * 1.4426950408889634f;
-        hipLaunchKernelGGL(k_attn_prefill_fa, grid, dim3(256), 0, st, q, q_rs, k, v, kv_sb, kv_sh, row_pos, row_slot, M,
-                           sl2, pt, pps, npages, kv_pgs, out, o_rs, xchunk);
+        hipLaunchKernelGGL(k_attn_prefill_sdpa, grid, dim3(256), 0, st, q, q_rs, k, v, kv_sb, kv_sh, row_pos, row_slot, M,
+                           sm_scale, pt, pps, npages, kv_pgs, out, o_rs, xchunk);
     } else if (kv8 == 2)
         hipLaunchKernelGGL((k_attn_prefill<1, 2, 2>), dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v, kv_sb,
                            kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale * k_scale, pt, pps, npages, kv_pgs, out, o_rs,
