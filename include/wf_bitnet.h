@@ -247,6 +247,9 @@ enum {
     WF_OP_DOWN = 5,       /* down_proj + residual; last block: next input norm or final norm    */
     WF_OP_LM_HEAD = 6     /* tied bf16 LM head + greedy argmax + position advance (layer ignored) */
 };
+/* Batch 1: wf_model_step skips WF_OP_EMBED and layer 0's WF_OP_QKV / WF_OP_O read the token's
+ * embedding row (embed[token], the residual) themselves, so wf_model_launch_op(m, 0, WF_OP_QKV or
+ * WF_OP_O) at batch 1 takes its input from tokens[0] (wf_model_desc.tokens), not from h. */
 int wf_model_launch_op(wf_model* m, int layer, int op, void* stream);
 /* Read-only view of the step's attention hand-off, for kernel-level checks (tests/, profiling):
  * after WF_OP_QKV and WF_OP_ATTN of a layer, q holds that layer's query rows after RoPE
@@ -256,9 +259,9 @@ int wf_model_launch_op(wf_model* m, int layer, int op, void* stream);
  * 128 + ((d >> 2) & 1) * 64 + (d >> 3) * 4 + (d & 3)] (head_dim 128); the attention output is
  * sum_s e^(m_s - M) o_s / sum_s e^(m_s - M) l_s, M = max_s m_s (records with l = 0 are empty).
  * Batch < 16 and untiled caches (the reference's SDPA semantics, records already in one frame:
- * m = 0): attn_row is the merged bf16 attention output [batch, n_heads * head_dim] the O projection
- * reads; NULL on the batched tile-layout path. Device pointers owned by the model; valid until
- * wf_model_destroy. */
+ * m = 0). attn_row is the bf16 attention output [batch, n_heads * head_dim] the O projection reads,
+ * on every path (the batched tile-layout kernel writes it directly and keeps no records:
+ * records = 0). Device pointers owned by the model; valid until wf_model_destroy. */
 typedef struct {
     const uint16_t* q;
     const float* part_ml;

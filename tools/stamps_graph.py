@@ -119,11 +119,17 @@ def main():
             res[name]["gap_from_prev_last_exit"] = round(res[name]["entry_first"] - res[prev]["exit_last"], 2)
         prev = name
     res["step_ms"] = round(e0.elapsed_time(e1), 4)
+    # per-block timeline of the attention (block index, then each named stamp in us from t0)
+    ar = ops["attn"][0]
+    live = np.nonzero(ar[:, 0] > 0)[0]
+    raw = [[int(i)] + [round(float((ar[i, sl] - t0) * 0.01), 2) if ar[i, sl] > 0 else None for sl in ATTN_NAMES]
+           for i in live]
     for k, v in res.items():
         print(k, json.dumps(v), flush=True)
     out = ROOT / "gpurun_out" / f"stamps_graph_b{B}.json"
     out.parent.mkdir(exist_ok=True)
     out.write_text(json.dumps(res, indent=1))
+    (out.parent / f"stamps_graph_b{B}_attn_raw.json").write_text(json.dumps(raw))
 
 
 if __name__ == "__main__":

@@ -608,6 +608,12 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
 // Residency: every split of a head must be resident while its siblings poll: the host launches
 // at most kSdpaMaxBlocks blocks per launch (B = 1: 160), below the chip's resident count.
 // ---------------------------------------------------------------------------------------------
+#ifndef WF_SDPA_SLEEP
+#define WF_SDPA_SLEEP 1
+#endif
+#ifndef WF_SDPA_WPE
+#define WF_SDPA_WPE __attribute__((amdgpu_waves_per_eu(1, 2)))
+#endif
 constexpr int kSdpaMaxT = 1024;      // split length bound (max_seq <= 8192): a split spans <= 3 blocks
 constexpr int kSdpaMaxSeq = kAttnPartSplits1 * kSdpaMaxT;
 
@@ -803,10 +809,12 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
         uint64_t gv = ((uint64_t)ep << 32) | 0xff800000u;  // lanes past the granules: -inf, tagged
         int ok = 1;
         for (int it = 0;; ++it) {
+#ifndef WF_SDPA_NOPOLL
             if (lane < 3 * NS) gv = ld_sc1(xg + bh * NS * 3 + lane);
+#endif
             if (__all((unsigned)(gv >> 32) == ep)) break;
             if (it > (1 << 20)) { ok = 0; break; }  // a missing sibling ends in NaN outputs, never a hang
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(WF_SDPA_SLEEP);
         }
         const float val = __uint_as_float((uint32_t)gv);
         const int blk = lane < 3 * NS ? ((sp * T) >> 9) + ent : -1;
@@ -924,7 +932,7 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
         make_uint2(pk_bf16(O[0] * inv, O[1] * inv), pk_bf16(O[2] * inv, O[3] * inv));
 }
 
-__global__ __launch_bounds__(kAttnPartThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_attn_sdpa(const uint16_t* __restrict__ q, int64_t q_sb,
+__global__ __launch_bounds__(kAttnPartThreads) WF_SDPA_WPE void k_attn_sdpa(const uint16_t* __restrict__ q, int64_t q_sb,
                                                                 const uint16_t* __restrict__ K,
                                                                 const uint16_t* __restrict__ V, int64_t kv_sb,
                                                                 int64_t kv_sh, int Hq, int Hkv, int S,
@@ -1292,7 +1300,7 @@ __global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* _
 // (a tile past the sequence loads nothing and computes nothing). The block writes the normalised
 // bf16 attention row bf16(o * (1 / l)) of its group's heads into `row` [B][Hq * 128].
 // ---------------------------------------------------------------------------------------------
-template <int KV8>
+template <int KV8, int GQ>
 __global__ __launch_bounds__(256, 3) void k_attn_sdpa_mfma(const uint16_t* __restrict__ q, int64_t q_sb,
                                                           const uint16_t* __restrict__ K, const uint16_t* __restrict__ Vt,
                                                           int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv, int S,
@@ -1326,11 +1334,15 @@ __global__ __launch_bounds__(256, 3) void k_attn_sdpa_mfma(const uint16_t* __res
     // VGPRs fewer, three blocks per CU
     __shared__ __attribute__((aligned(16))) uint4 sm_q[4][64];
     {
-        const uint16_t* qp = q + b * q_sb + (int64_t)(hq0 + min(l16, grp - 1)) * D + 8 * q4;
+        // GQ = 4: column l16 = head (l16 & 3) restricted to the lane quarter l16 >> 2 of every 32
+        // dims, so each MFMA output is a sum of 8 products (below)
+        const int hh = GQ == 4 ? (l16 & 3) : min(l16, grp - 1);
+        const bool live = GQ == 4 ? (l16 >> 2) == q4 : l16 < grp;
+        const uint16_t* qp = q + b * q_sb + (int64_t)(hq0 + hh) * D + 8 * q4;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             uint4 t = *reinterpret_cast<const uint4*>(qp + 32 * c);
-            if (l16 >= grp) t = make_uint4(0, 0, 0, 0);
+            if (!live) t = make_uint4(0, 0, 0, 0);
             if (wave == 0) sm_q[c][lane] = t;
         }
     }
@@ -1389,11 +1401,13 @@ __global__ __launch_bounds__(256, 3) void k_attn_sdpa_mfma(const uint16_t* __res
             const int i = s & 3;
             const int lim = Sb - bs - 8 * q4;  // valid keys among this lane's 8
             if (s < 4) {  // pass 1: scores
-                // the four 32-dim partial dots in separate accumulators, summed in f64 and rounded
-                // once: close to the exactly rounded dot of the reference's GEMM (one fp32
-                // accumulator chained through the four MFMAs moved 1.6 % of the outputs at 4096 keys;
-                // eight 16-dim partials (v_mfma_f32_16x16x16_bf16) measured 5 vs 9 of 40960 outputs off
-                // the oracle, but 20 bytes of scratch at three blocks per CU)
+                // partial dots in separate accumulators, summed in f64 and rounded once: close to the
+                // exactly rounded dot of the reference's GEMM. GQ = 4 (4 query heads per kv head) puts
+                // the 12 idle B columns to work: column 4 c + h holds head h on dims 8 c .. 8 c + 7 of
+                // each 32, so every MFMA output sums 8 products and the 16 partials of a score meet
+                // in f64 (two row rotations); one fp32 accumulator chained through the four MFMAs
+                // moved 1.6 % of the outputs at 4096 keys, four 32-product partials ~0.1 % on peaky
+                // rows (tests/test_gpu_configs.py attention kernels)
 #pragma unroll
                 for (int tau = 0; tau < 2; ++tau) {
                     double dd[4] = {0.0, 0.0, 0.0, 0.0};
@@ -1404,6 +1418,13 @@ __global__ __launch_bounds__(256, 3) void k_attn_sdpa_mfma(const uint16_t* __res
                             v4f_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
 #pragma unroll
                         for (int r4 = 0; r4 < 4; ++r4) dd[r4] += (double)pr[r4];
+                    }
+                    if constexpr (GQ == 4) {  // lane l16 < 4: the sum of columns l16, +4, +8, +12
+#pragma unroll
+                        for (int r4 = 0; r4 < 4; ++r4) {
+                            dd[r4] += dpp_d<DPP_ROW_ROR8>(dd[r4]);
+                            dd[r4] += dpp_d<DPP_ROW_ROR4>(dd[r4]);
+                        }
                     }
 #pragma unroll
                     for (int r4 = 0; r4 < 4; ++r4) {
@@ -2236,15 +2257,13 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
     }
     (void)tail;
     const dim3 grid(Hkv, B);
-    if (kv8 == 2)
-        hipLaunchKernelGGL(k_attn_sdpa_mfma<2>, grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, seq_lens,
-                           sm_scale * k_scale, pt, pps, npages, kv_pgs, v_scale, merged_row, order);
-    else if (kv8)
-        hipLaunchKernelGGL(k_attn_sdpa_mfma<1>, grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, seq_lens,
-                           sm_scale * k_scale, pt, pps, npages, kv_pgs, v_scale, merged_row, order);
-    else
-        hipLaunchKernelGGL(k_attn_sdpa_mfma<0>, grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, seq_lens,
-                           sm_scale, pt, pps, npages, kv_pgs, 1.0f, merged_row, order);
+    const bool g4 = Hq == 4 * Hkv;
+    const float ss = kv8 ? sm_scale * k_scale : sm_scale, vs = kv8 ? v_scale : 1.0f;
+    auto kern = kv8 == 2 ? (g4 ? k_attn_sdpa_mfma<2, 4> : k_attn_sdpa_mfma<2, 0>)
+              : kv8      ? (g4 ? k_attn_sdpa_mfma<1, 4> : k_attn_sdpa_mfma<1, 0>)
+                         : (g4 ? k_attn_sdpa_mfma<0, 4> : k_attn_sdpa_mfma<0, 0>);
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, ss, pt, pps,
+                       npages, kv_pgs, vs, merged_row, order);
     return check_launch("decode_attention_partials");
 }
 

@@ -2843,10 +2843,13 @@ static bool pf_staged_ok(const GemvArgs& a, bool wide) {
 #define WF_PG_PERSIST 1  // (ab_prefill_persist_r04.txt)
 #endif
 constexpr bool kPgPersist = WF_PG_PERSIST;
-[[maybe_unused]] static int pg_cu_count() {
+[[maybe_unused]] static int pg_cu_count() {  // queried once per device (every gate|up launch asks)
+    static int cached[64] = {};
     int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (dev >= 0 && dev < 64 && cached[dev]) return cached[dev];
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (dev >= 0 && dev < 64) cached[dev] = n;
     return n;
 }
 template <int MODE, int TNW, int ALG>

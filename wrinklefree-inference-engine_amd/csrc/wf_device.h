@@ -55,7 +55,7 @@ __device__ __forceinline__ void store_from_f32(void* p, int64_t i, int dt, float
 // ~8 cycles per step instead of an LDS-latency ds_bpermute per step.
 // ---------------------------------------------------------------------------------------------
 enum : int { DPP_QP_1032 = 0xB1, DPP_QP_2301 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140,
-             DPP_BCAST15 = 0x142, DPP_BCAST31 = 0x143, DPP_ROW_ROR8 = 0x128 };
+             DPP_BCAST15 = 0x142, DPP_BCAST31 = 0x143, DPP_ROW_ROR8 = 0x128, DPP_ROW_ROR4 = 0x124 };
 template <int CTRL, int ROW_MASK = 0xF>
 __device__ __forceinline__ int dpp_i(int v, int old = 0) {
     return __builtin_amdgcn_update_dpp(old, v, CTRL, ROW_MASK, 0xF, false);
