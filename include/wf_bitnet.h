@@ -270,6 +270,11 @@ typedef struct {
     const uint16_t* attn_row;
 } wf_attn_records;
 int wf_model_attn_view(const wf_model* m, wf_attn_records* out);
+/* Read-only view of the last wf_model_prefill call's last layer, for kernel-level checks (tests/):
+ * q = its query rows after RoPE and attn = its causal attention output rows, both [rows][n_heads *
+ * head_dim] bf16 in the call's row order. Device pointers owned by the model; valid until the next
+ * prefill or wf_model_destroy. WF_EINVAL before any prefill reservation. */
+int wf_model_prefill_view(const wf_model* m, const uint16_t** q, const uint16_t** attn);
 /* Which batched GEMM ops (flags[0..3] = QKV, O, gate|up, down) run their input row norm inside the
  * GEMM launch instead of a separate row-norm launch (batch >= 16 on WF_FMT_I2S_MFMA weights, when
  * the whole grid fits the device at once; decided at wf_model_create). Diagnostic / bench query:

@@ -7,3 +7,4 @@ for n in base sleep20 nopoll nowpe; do
   WF_STAMPS_LIB=$lib timeout -k 10 200 python -u tools/stamps_graph.py --ctx 1024 --reps 20 > gpurun_out/stamps_$n.txt 2>&1 || exit 1
   echo "== $n"; grep "^attn\|step_ms" gpurun_out/stamps_$n.txt | cut -c1-300
 done
+bash tools/prof_prefill.sh r05a

@@ -612,7 +612,7 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
 #define WF_SDPA_SLEEP 1
 #endif
 #ifndef WF_SDPA_WPE
-#define WF_SDPA_WPE __attribute__((amdgpu_waves_per_eu(1, 2)))
+#define WF_SDPA_WPE
 #endif
 constexpr int kSdpaMaxT = 1024;      // split length bound (max_seq <= 8192): a split spans <= 3 blocks
 constexpr int kSdpaMaxSeq = kAttnPartSplits1 * kSdpaMaxT;
@@ -627,6 +627,20 @@ __device__ __forceinline__ float fexp_u20(float x) {
     const float t = fmaf(8388608.0f, src - r, 1065353216.0f);
     const int ci = (int)t;  // v_cvt_i32_f32 truncates, as _mm512_cvttps_epi32
     return __int_as_float(x < __uint_as_float(0xc2aeac50u) ? 0 : ci);
+}
+// fexp_u20 on a packed pair: the same operations, two lanes per instruction where the VALU has
+// packed fp32 forms (each lane rounds as the scalar op)
+__device__ __forceinline__ f32x2_t fexp_u20_pk(f32x2_t x) {
+    const f32x2_t src = x * __uint_as_float(0x3fb8aa3bu);
+    const f32x2_t fr = src - f32x2_t{floorf(src.x), floorf(src.y)};
+    f32x2_t r = __builtin_elementwise_fma(fr, f32x2_t{-0.079204240219773236f, -0.079204240219773236f},
+                                          f32x2_t{-0.22433836478672356f, -0.22433836478672356f});
+    r = __builtin_elementwise_fma(fr, r, f32x2_t{0.30354260500649682f, 0.30354260500649682f});
+    r = __builtin_elementwise_fma(fr, r, f32x2_t{0.00010703434948458272f, 0.00010703434948458272f});
+    const f32x2_t t = __builtin_elementwise_fma(f32x2_t{8388608.0f, 8388608.0f}, src - r,
+                                                f32x2_t{1065353216.0f, 1065353216.0f});
+    const float lo = __uint_as_float(0xc2aeac50u);
+    return f32x2_t{__int_as_float(x.x < lo ? 0 : (int)t.x), __int_as_float(x.y < lo ? 0 : (int)t.y)};
 }
 // glibc expf (the scalar tail and the block rescale), within ~1 ulp: x = k ln2 + r (two-constant
 // reduction, exact for |k| < 2^11), 2^(r log2 e) on v_exp_f32, scaled by 2^k (x <= 0 here). A 1-ulp
@@ -695,13 +709,13 @@ __device__ __forceinline__ void sdpa_scores(const uint4 (&kr)[U], const uint32_t
 // probabilities of the chunk's keys and their P.V: e = fexp_u20 / expf of (s - M_c) (vector part /
 // tail of the key's 512-key block), l += e R, o += bf16(e) R v, R = the product of the block
 // rescale factors between the key's block and the split's last one (1.0 in the last block)
-struct SdpaBlocks {
-    float m0, m1, m2, r0, r1, r2;
-};
+// (the six block values by value: a struct passed by reference became a private array that the
+// per-key selects indexed, in scratch -- or, under an occupancy attribute, in LDS, which stretched
+// the launch's block dispatch over ~9 us)
 template <int U, bool ONE>
 __device__ __forceinline__ void sdpa_pv(const uint4 (&vr)[U], const float (&sc)[ONE ? U : 1], const float* sc_lds, int c0,
-                                        int gid, int t0, int t1, int cb0, int Sb, const SdpaBlocks& bk, float& l,
-                                        float (&o)[8]) {
+                                        int gid, int t0, int t1, int cb0, int Sb, float bm0, float bm1, float bm2,
+                                        float br0, float br1, float br2, float& l, float (&o)[8]) {
     constexpr int NG = kAttnPartThreads / 16;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -711,8 +725,8 @@ __device__ __forceinline__ void sdpa_pv(const uint4 (&vr)[U], const float (&sc)[
             if constexpr (ONE) sv = sc[u];
             else sv = sc_lds[t - t0];
             const bool in0 = t < 512 * (cb0 + 1), in1 = t < 512 * (cb0 + 2);
-            const float Mc = in0 ? bk.m0 : (in1 ? bk.m1 : bk.m2);
-            const float Rc = in0 ? bk.r0 : (in1 ? bk.r1 : bk.r2);
+            const float Mc = in0 ? bm0 : (in1 ? bm1 : bm2);
+            const float Rc = in0 ? br0 : (in1 ? br1 : br2);
             const int blk0 = t & ~511;
             const int vbnd = min(512, Sb - blk0) & ~15;  // the 16-wide vector part of the block
             const float x = sv - Mc;
@@ -846,17 +860,18 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
     // block-uniform values read once into scalar registers (hipcc otherwise sank the LDS loads into
     // the per-key selects and built a table of LDS addresses in scratch)
     auto sload = [](const float& v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
-    const SdpaBlocks bk{sload(blk_m[0]), sload(blk_m[1]), sload(blk_m[2]), sload(blk_r[0]), sload(blk_r[1]), sload(blk_r[2])};
+    const float bm0 = sload(blk_m[0]), bm1 = sload(blk_m[1]), bm2 = sload(blk_m[2]);
+    const float br0 = sload(blk_r[0]), br1 = sload(blk_r[1]), br2 = sload(blk_r[2]);
     float l = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (t0 < t1) {
         if constexpr (ONE) {
-            sdpa_pv<U, ONE>(vA, sc, sc_lds, t0, gid, t0, t1, cb0, Sb, bk, l, o);
+            sdpa_pv<U, ONE>(vA, sc, sc_lds, t0, gid, t0, t1, cb0, Sb, bm0, bm1, bm2, br0, br1, br2, l, o);
         } else {
             for (int c0 = t0; c0 < t1; c0 += 2 * CH) {
-                sdpa_pv<U, ONE>(vA, sc, sc_lds, c0, gid, t0, t1, cb0, Sb, bk, l, o);
+                sdpa_pv<U, ONE>(vA, sc, sc_lds, c0, gid, t0, t1, cb0, Sb, bm0, bm1, bm2, br0, br1, br2, l, o);
                 if (c0 + 2 * CH < t1) sdpa_load<U>(vA, V, kvb, c0 + 2 * CH, gid, t1);
                 if (c0 + CH < t1) {
-                    sdpa_pv<U, ONE>(vB, sc, sc_lds, c0 + CH, gid, t0, t1, cb0, Sb, bk, l, o);
+                    sdpa_pv<U, ONE>(vB, sc, sc_lds, c0 + CH, gid, t0, t1, cb0, Sb, bm0, bm1, bm2, br0, br1, br2, l, o);
                     if (c0 + 3 * CH < t1) sdpa_load<U>(vB, V, kvb, c0 + 3 * CH, gid, t1);
                 }
             }
@@ -2028,23 +2043,32 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
     };
     const int o = (c & ~12) | ((c & 4) << 1) | ((c & 8) >> 1);
     const int koff = ((((o >> 2) & 1) * 16 + h) * 16 + 4 * (o >> 3) + (o & 3)) * 16;
-    // S^T of one tile in natural units: two 64-dim partial MFMA chains, summed in f64, rounded once
+    // S^T of one tile, raw dots (unscaled): two 64-dim MFMA accumulator chains and one fp32 add.
+    // Measured against the oracle on the same caches (tests/test_gpu_configs.py
+    // test_prefill_attention_vs_oracle_sdpa; 2 x 2048 rows, 911360 sampled outputs): these chains
+    // 307 off and 54 of 2048 layer-1 positions > 1e-3 in test_prefill_8x2048_full_width_vs_oracle;
+    // 8 zero-C partials in a pairwise fp32 tree 292 (+80 us per layer); the 8 partials summed in f64
+    // in pass 2 only 274 / 54, in pass 1 only 192 / 58, in both passes 109 / 27 (the batched decode
+    // kernel's level: 11 positions) at +30 % kernel time and 216 B of scratch. The matrix cores align
+    // each 8-product group to its largest product and truncate (tools/ubench/mfma_round.hip), and
+    // every fp32 partial sum rounds; the block max M_c enters every probability (l is summed from
+    // the unrounded e, P.V from the rounded P), so pass 1 needs the precision as much as pass 2.
     auto qk = [=](const uint8_t* st, float (&x)[16]) __attribute__((always_inline)) {
         uint4 kf[8];
 #pragma unroll
         for (int s2 = 0; s2 < 8; ++s2) kf[s2] = *reinterpret_cast<const uint4*>(st + koff + s2 * 512);
-        v16f_t a0, a1;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) { a0[e] = 0.f; a1[e] = 0.f; }
+        v16f_t a0 = {}, a1 = {};
 #pragma unroll
         for (int s2 = 0; s2 < 8; s2 += 2) {
             a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf_t, kf[s2]), qf[s2], a0, 0, 0, 0);
             a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf_t, kf[s2 + 1]), qf[s2 + 1], a1, 0, 0, 0);
         }
+        const v16f_t t = a0 + a1;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) x[e] = (float)((double)a0[e] + (double)a1[e]) * scale;
+        for (int e = 0; e < 16; ++e) x[e] = t[e];
     };
     float m_run = -INFINITY, l_run = 0.f, bmax = -INFINITY;
+    int vmin = 0;
     v16f_t oacc[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
@@ -2061,14 +2085,16 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
         else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
         __builtin_amdgcn_s_barrier();
     };
-    for (int i = 0; i < nstages; ++i) {
-        wait_through(i, i + P - 2);  // stage i landed, and everyone is done with stage i - 1's slot
-        if (i + P - 1 < nstages) issue(i + P - 1);
-        int cb, pass, ta, tb;
-        stage_of(i, cb, pass, ta, tb);
-        const uint8_t* st = ring + (i % P) * kSlot;
-        const int blk0 = 512 * cb;
-        if (pass == 1) {
+    // one loop per pass of each block (a single stage loop with a pass switch made the register
+    // allocator copy the 64 O accumulators at every stage)
+    int i = 0;
+    for (int cb = 0; cb < NB; ++cb) {
+        const int nt = cb == NB - 1 ? nt_last : 16, s1 = (nt + 1) >> 1, blk0 = 512 * cb;
+        for (int jj = 0; jj < s1; ++jj, ++i) {
+            wait_through(i, i + P - 2);  // stage i landed, and everyone is done with stage i - 1's slot
+            if (i + P - 1 < nstages) issue(i + P - 1);
+            const uint8_t* st = ring + (i % P) * kSlot;
+            const int ta = 16 * cb + 2 * jj, tb = min(ta + 1, 16 * cb + nt - 1);
             // this column's maximum over its keys of the stage's tiles
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
@@ -2082,67 +2108,88 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
                 for (int j = 0; j < 16; ++j)
                     if ((j & 7) + 16 * (j >> 3) < lim) bmax = fmaxf(bmax, x[j]);
             }
-            const int nt = cb == NB - 1 ? nt_last : 16, s1 = (nt + 1) >> 1;
-            if (i - 24 * cb == s1 - 1) {  // the block's last pass-1 stage: M_c, rescale O and l
-                const float mn = fmaxf(m_run, swap32_max(bmax));
-                const float r = expf_rn(m_run - mn);  // 0 before the first block, 1 if no key of it
-                m_run = mn;
-                bmax = -INFINITY;
-                l_run *= r;
+        }
+        {  // M_c, rescale O and l (the max of the raw dots, scaled once: rounding a product is monotone)
+            const float mn = fmaxf(m_run, swap32_max(bmax) * scale);
+            vmin = (int)-wave_max((float)-(min(512, lim_q - blk0) & ~15));  // the wave's smallest vector part
+            const float r = expf_rn(m_run - mn);  // 0 before the first block, 1 if no key of it
+            m_run = mn;
+            bmax = -INFINITY;
+            l_run *= r;
 #pragma unroll
-                for (int mt = 0; mt < 4; ++mt)
+            for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-                    for (int e = 0; e < 16; ++e) oacc[mt][e] *= r;
-            }
-        } else {
-            const int bs = 32 * ta;
+                for (int e = 0; e < 16; ++e) oacc[mt][e] *= r;
+        }
+        for (int jj = 0; jj < nt; ++jj, ++i) {
+            wait_through(i, i + P - 2);
+            if (i + P - 1 < nstages) issue(i + P - 1);
+            const uint8_t* st = ring + (i % P) * kSlot;
+            const int bs = 32 * (16 * cb + jj);
             if (bs >= lim_b) continue;  // wave-uniform (the block's tiles past the group's last row)
-            uint4 vv[4][2];  // V^T fragments (dim 32 mt + c, keys 16 s + 8 h + 0..7): issued first
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
-                const int d = 32 * mt + c, n = d >> 4, l = d & 15;
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2)
-                    vv[mt][s2] = *reinterpret_cast<const uint4*>(st + 8192 + ((n * 4 + 2 * s2 + h) * 16 + l) * 16);
-            }
-            float x[16];
-            qk(st, x);
-            const int lim = lim_q - bs - 8 * h;
-            const int nbc = min(512, lim_q - blk0), vbnd = nbc & ~15;  // the column's block: vector part
-            uint32_t pk[8];
-#pragma unroll
-            for (int j = 0; j < 16; j += 2) {
-                float e2[2];
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const int kk = (j + u & 7) + 8 * h + 16 * ((j + u) >> 3);  // key within the tile
-                    const int kb = bs - blk0 + kk;                             // key within the block
-                    const float xv = x[j + u] - m_run;
-                    const float ev = kk < lim + 8 * h ? (kb < vbnd ? fexp_u20(xv) : expf_rn(xv)) : 0.f;
-                    l_run += ev;
-                    e2[u] = ev;
+                uint4 vv[4][2];  // V^T fragments (dim 32 mt + c, keys 16 s + 8 h + 0..7): issued first
+    #pragma unroll
+                for (int mt = 0; mt < 4; ++mt) {
+                    const int d = 32 * mt + c, n = d >> 4, l = d & 15;
+    #pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2)
+                        vv[mt][s2] = *reinterpret_cast<const uint4*>(st + 8192 + ((n * 4 + 2 * s2 + h) * 16 + l) * 16);
                 }
-                pk[j >> 1] = pk_bf16(e2[0], e2[1]);
-            }
-            const v8bf_t pb0 = __builtin_bit_cast(v8bf_t, make_uint4(pk[0], pk[1], pk[2], pk[3]));
-            const v8bf_t pb1 = __builtin_bit_cast(v8bf_t, make_uint4(pk[4], pk[5], pk[6], pk[7]));
-            const int limv = lim_b - bs - 8 * h;  // V keys past the block's last position: zero (stale)
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-                    uint4 a = vv[mt][s2];
-                    if (limv < 32) {
-                        const int k0 = 16 * s2;
-                        a.x &= (k0 < limv ? 0xffffu : 0u) | (k0 + 1 < limv ? 0xffff0000u : 0u);
-                        a.y &= (k0 + 2 < limv ? 0xffffu : 0u) | (k0 + 3 < limv ? 0xffff0000u : 0u);
-                        a.z &= (k0 + 4 < limv ? 0xffffu : 0u) | (k0 + 5 < limv ? 0xffff0000u : 0u);
-                        a.w &= (k0 + 6 < limv ? 0xffffu : 0u) | (k0 + 7 < limv ? 0xffff0000u : 0u);
+                float x[16];
+                qk(st, x);
+                const int lim = lim_q - bs - 8 * h;
+                const int nbc = min(512, lim_q - blk0), vbnd = nbc & ~15;  // the column's block: vector part
+                uint32_t pk[8];
+                // every key of the tile below every column's causal limit and inside its block's 16-wide
+                // vector part (the common case): fexp_u20 only, no per-key bounds
+                // the lane's 16 exponentials of the tile summed as a pairwise tree, then into l: 16
+                // sequential adds per 512-key block instead of 256 (the one long fp32 chain of the kernel;
+                // it moved 2x the decode kernel's share of outputs off the oracle)
+                float ee[16];
+                if (bs - blk0 + 32 <= vmin) {  // packed fp32 pairs (v_pk_mul / v_pk_add / v_pk_fma)
+                    const f32x2_t sc2 = {scale, scale}, m2 = {m_run, m_run};
+    #pragma unroll
+                    for (int j = 0; j < 16; j += 2) {
+                        const f32x2_t e2 = fexp_u20_pk(f32x2_t{x[j], x[j + 1]} * sc2 - m2);
+                        ee[j] = e2.x;
+                        ee[j + 1] = e2.y;
                     }
-                    oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf_t, a), s2 ? pb1 : pb0,
-                                                                       oacc[mt], 0, 0, 0);
+                } else {
+    #pragma unroll
+                    for (int j = 0; j < 16; ++j) {
+                        const int kk = (j & 7) + 8 * h + 16 * (j >> 3);  // key within the tile
+                        const int kb = bs - blk0 + kk;                   // key within the block
+                        const float xv = x[j] * scale - m_run;
+                        ee[j] = kk < lim + 8 * h ? (kb < vbnd ? fexp_u20(xv) : expf_rn(xv)) : 0.f;
+                    }
                 }
-            }
+    #pragma unroll
+                for (int j = 0; j < 16; j += 2) pk[j >> 1] = pk_bf16(ee[j], ee[j + 1]);
+    #pragma unroll
+                for (int w2 = 8; w2 >= 1; w2 >>= 1)
+    #pragma unroll
+                    for (int j = 0; j < w2; ++j) ee[j] += ee[j + w2];
+                l_run += ee[0];
+                const v8bf_t pb0 = __builtin_bit_cast(v8bf_t, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+                const v8bf_t pb1 = __builtin_bit_cast(v8bf_t, make_uint4(pk[4], pk[5], pk[6], pk[7]));
+                const int limv = lim_b - bs - 8 * h;  // V keys past the block's last position: zero (stale)
+    #pragma unroll
+                for (int mt = 0; mt < 4; ++mt) {
+    #pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        uint4 a = vv[mt][s2];
+                        if (limv < 32) {
+                            const int k0 = 16 * s2;
+                            a.x &= (k0 < limv ? 0xffffu : 0u) | (k0 + 1 < limv ? 0xffff0000u : 0u);
+                            a.y &= (k0 + 2 < limv ? 0xffffu : 0u) | (k0 + 3 < limv ? 0xffff0000u : 0u);
+                            a.z &= (k0 + 4 < limv ? 0xffffu : 0u) | (k0 + 5 < limv ? 0xffff0000u : 0u);
+                            a.w &= (k0 + 6 < limv ? 0xffffu : 0u) | (k0 + 7 < limv ? 0xffff0000u : 0u);
+                        }
+                        oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf_t, a), s2 ? pb1 : pb0,
+                                                                           oacc[mt], 0, 0, 0);
+                    }
+                }
+
         }
     }
     const float inv = 1.0f / swap32_sum(l_run);

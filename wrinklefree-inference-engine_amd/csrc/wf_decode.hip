@@ -2879,6 +2879,14 @@ static void prefill_gemm(const GemvArgs& a, hipStream_t st) {
 }
 }  // extern "C++"
 
+int wf_model_prefill_view(const wf_model* m, const uint16_t** q, const uint16_t** attn) {
+    WF_REQUIRE(m && q && attn, "model_prefill_view: null argument");
+    WF_REQUIRE(m->pf_rows > 0 && m->pf_q && m->pf_attn, "model_prefill_view: no prefill reservation");
+    *q = m->pf_q;
+    *attn = m->pf_attn;
+    return WF_OK;
+}
+
 int wf_model_prefill(wf_model* m, const int32_t* tokens, const int32_t* row_slot, const int32_t* row_pos, int rows,
                      void* stream) {
     WF_REQUIRE(m && tokens && row_slot && row_pos, "model_prefill: null argument");

@@ -69,6 +69,7 @@ SIGNATURES = {
     "wf_model_fused_norm": (i32, [vp, vp]),
     "wf_model_prefill_reserve": (i32, [vp, i32]),
     "wf_model_prefill": (i32, [vp, vp, vp, vp, i32, vp]),
+    "wf_model_prefill_view": (i32, [vp, vp, vp]),
 }
 
 

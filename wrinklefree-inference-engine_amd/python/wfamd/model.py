@@ -397,6 +397,19 @@ class BitNetDecoder:
             call("wf_model_prefill", self._h, t[r0:].data_ptr(), sl[r0:].data_ptr(), ps[r0:].data_ptr(), n, st)
         self._pf_keep = (t, sl, ps)  # alive until the stream has consumed them
 
+    def prefill_view(self, rows: int):
+        """The last prefill call's last layer (include/wf_bitnet.h wf_model_prefill_view): q rows
+        after RoPE and the causal attention output rows, [rows, Hq, D] bf16 copies on the device."""
+        qp, ap = C.c_void_p(), C.c_void_p()
+        call("wf_model_prefill_view", self._h, C.byref(qp), C.byref(ap))
+        cfg = self.cfg
+        out = []
+        for p in (qp, ap):
+            t = torch.empty(rows, cfg.n_heads, cfg.head_dim, dtype=torch.bfloat16, device=self.dev)
+            ops.device_copy(t.data_ptr(), p.value, t.numel() * 2)
+            out.append(t)
+        return out[0], out[1]
+
     def admit(self, b: int, prompt) -> None:
         """Start sequence `prompt` in slot b: prefill all but its last token, then the next decode
         step runs the last token at position len - 1 (scripts/direct_inference_full.py's loop)."""
