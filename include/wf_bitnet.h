@@ -258,10 +258,10 @@ int wf_model_launch_op(wf_model* m, int layer, int op, void* stream);
  * (running max m, sum l) and the unnormalised output o[d] at part_o[((b n_heads + h) records + s) *
  * 128 + ((d >> 2) & 1) * 64 + (d >> 3) * 4 + (d & 3)] (head_dim 128); the attention output is
  * sum_s e^(m_s - M) o_s / sum_s e^(m_s - M) l_s, M = max_s m_s (records with l = 0 are empty).
- * Batch < 16 and untiled caches (the reference's SDPA semantics, records already in one frame:
- * m = 0). attn_row is the bf16 attention output [batch, n_heads * head_dim] the O projection reads,
- * on every path (the batched tile-layout kernel writes it directly and keeps no records:
- * records = 0). Device pointers owned by the model; valid until wf_model_destroy. */
+ * Batch < 16 and untiled caches: records in one frame (m = 0; the reference's SDPA semantics), which
+ * each head's last attention block sums into attn_row. Batch >= 16 on tile-layout caches: no records
+ * (records = 0). attn_row is the bf16 attention output [batch, n_heads * head_dim] the O projection
+ * reads, on every path. Device pointers owned by the model; valid until wf_model_destroy. */
 typedef struct {
     const uint16_t* q;
     const float* part_ml;

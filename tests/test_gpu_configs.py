@@ -114,6 +114,23 @@ def merge_records(ml: torch.Tensor, o: torch.Tensor) -> np.ndarray:
     return (wgt[..., None] * o).sum(-2) / (wgt * l).sum(-1)[..., None]
 
 
+def merge_records_bf16(ml: torch.Tensor, o: torch.Tensor) -> np.ndarray:
+    """The bf16 attention row k_attn_sdpa's merging block forms from the head's records (one frame:
+    m = 0), in its float32 arithmetic: L = sum_s l_s and O = sum_s o_s in split order, out =
+    bf16(O * (1 / L)). Bit patterns [B, Hq, D]."""
+    ml = ml.float().cpu().numpy()
+    o = o.float().cpu().numpy()
+    assert np.all(ml[..., 0] == 0.0), "k_attn_sdpa records are in one frame"
+    L = np.zeros(ml.shape[:2], np.float32)
+    O = np.zeros(o.shape[:2] + o.shape[3:], np.float32)
+    for u in range(ml.shape[2]):
+        L = (L + ml[:, :, u, 1]).astype(np.float32)
+        O = (O + o[:, :, u]).astype(np.float32)
+    y = (O * (np.float32(1.0) / L)[..., None]).astype(np.float32)
+    b = y.view(np.uint32).astype(np.uint64)
+    return ((b + 0x7FFF + ((b >> 16) & 1)) >> 16).astype(np.uint16)
+
+
 # ------------------------------------------------------------------------------------------------
 # (a) batch 1, full width, contexts 1024 / 4096 (BASELINE configs[1])
 # ------------------------------------------------------------------------------------------------
@@ -305,6 +322,9 @@ def test_step_attention_kernels_vs_oracle(orc, variant):
         got = merge_records(ml, o) if recs else None
         row = dec.attention_row()
         assert row is not None and (ml.shape[2] > 0) == recs, variant
+        rowb = bits(row)
+        if recs:  # the head's merging block: the records summed in split order, bf16(O * (1 / L))
+            assert np.array_equal(merge_records_bf16(ml, o), rowb), variant
         check = range(len(S)) if len(S) <= 16 else list(range(12)) + [40, 77, 100, 127]
         for b in check:
             s = int(S[b])
@@ -313,7 +333,7 @@ def test_step_attention_kernels_vs_oracle(orc, variant):
             # the reference's SDPA (orc_attention_sdpa_cpu_*): the merged bf16 row the O projection
             # reads bit-exact but for summation-order ties; fp32 split records within 1e-5
             rb = orc.attention_sdpa_cpu_bf16(qb, kbb, vbb, s)
-            gb = bits(row[b])
+            gb = rowb[b]
             mism = int((gb != rb).sum())
             ulps = int(np.abs(gb.astype(np.int32) - rb.astype(np.int32)).max())
             mism_tot += mism

@@ -53,12 +53,20 @@ def op_summary(rows, names, last_slot, t0):
     out = {"blocks": int(len(live)), "entry_first": round(float(ent.min()), 2),
            "entry_med": round(float(np.median(ent)), 2), "exit_med": round(float(np.median(ex)), 2),
            "exit_last": round(float(ex.max()), 2)}
-    per = {}
+    per, foreign = {}, {}
     for sl, nm in names.items():
-        ok = live[:, sl] > 0
+        # a stamp counts only inside its own block's window [entry, exit + 20 us]: a slot another launch
+        # wrote (an earlier layer's op of the same region, a kernel that skips the stamp) is
+        # reported as foreign, not folded into the medians
+        ok = (live[:, sl] > 0) & (live[:, sl] >= live[:, 0]) & (live[:, sl] <= live[:, last_slot] + 2000)
+        bad = int(((live[:, sl] > 0) & ~ok).sum())
         if sl and ok.any():
             per[nm] = round(float(np.median((live[ok, sl] - live[ok, 0]) * 0.01)), 2)
+        if sl and bad:
+            foreign[nm] = bad
     out["per_block_med"] = per
+    if foreign:
+        out["foreign_stamps"] = foreign
     ok = (live[:, 64] > 0) & (live[:, 64 + last_slot] > 0)
     if ok.any():
         dt = (live[ok, last_slot] - live[ok, 0]).astype(np.float64)
@@ -101,7 +109,7 @@ def main():
     dc, at = read(lib, "wf_debug_stamps_decode"), read(lib, "wf_debug_stamps_attn")
     if B == 1:
         order = ("qkv", "attn", "o_proj", "gate_up", "down", "lm_head")
-        ops = {"qkv": (dc[0:512], GEMV_NAMES, 7), "attn": (at[0:2048], ATTN_NAMES, 2),
+        ops = {"qkv": (dc[0:512], GEMV_NAMES, 7), "attn": (at[0:2048], ATTN_NAMES, 3),
                "o_proj": (dc[512:1024], GEMV_NAMES, 3), "gate_up": (dc[1024:1536], GEMV_NAMES, 3),
                "down": (dc[1536:2048], GEMV_NAMES, 3), "lm_head": (dc[4096:4096 + 8016], LM_NAMES, 3)}
     else:

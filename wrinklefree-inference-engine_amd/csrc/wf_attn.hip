@@ -316,16 +316,8 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
 }
 
 // ---------------------------------------------------------------------------------------------
-// Decode-step attention partials: bf16 q/K/V, D = 128, kAttnPartSplits splits per (b, kv head)
-// whatever the context: split s of a sequence with Sb keys covers [s*T, min((s+1)*T, Sb)) with
-// T = round_up(ceil(Sb / kAttnPartSplits), 16), walked in chunks of 128 keys (16 lane groups x 8
-// keys) with an online softmax; chunk loads are double-buffered (the next chunk's loads are in
-// flight while the current one is computed; a split of up to 256 keys -- 2048 keys of context --
-// has all of its loads in flight at once). The block writes, per query head of its group, (m, l) to
-// ml[b][hq][s] and the unnormalised o to o[b][hq][s][D]; an empty split writes (-inf, 0) and
-// zeros. The consumer (wf_norm.h AttnRow, the O projection's prologue or k_rownorm_attn) reads a
-// fixed number of records, so it needs no sequence length and issues every load before its
-// weight stream.
+// Decode-step attention shared constants: k_attn_sdpa's block size and keys per lane group per chunk,
+// and the K/V load form.
 // ---------------------------------------------------------------------------------------------
 #ifndef WF_AP_THREADS  // study builds only (tools/build_variant.sh): threads per block
 #define WF_AP_THREADS 256
@@ -351,241 +343,6 @@ __device__ __forceinline__ uint4 kv_ld16(const uint16_t* p) {
 #define WF_KV_NT_B1 0
 #endif
 
-template <int G, int NS, int U>
-__device__ __forceinline__ void attn_part_body(const uint16_t* __restrict__ q, int64_t q_sb, const uint16_t* __restrict__ K,
-                                               const uint16_t* __restrict__ V, int64_t kv_sb, int64_t kv_sh, int Hq,
-                                               int Hkv, int S, const int32_t* __restrict__ seq_lens, float sm_scale,
-                                               float2* __restrict__ ml_out, float* __restrict__ o_out,
-                                               uint16_t* __restrict__ row_out, unsigned* __restrict__ cnt) {
-    constexpr int D = 128, LP = D / 8, NG = kAttnPartThreads / LP, CH = U * NG;
-    // block (s, y, b): query heads hq0 .. hq0 + G - 1 (G = whole GQA group, or 1: one block per query
-    // head, 4x the blocks for a group of 4 -- the K/V re-reads hit the caches)
-    const int s = blockIdx.x, b = blockIdx.z;
-    const int grp = Hq / Hkv;
-    const int hq0 = (G == 1) ? (int)blockIdx.y : (int)blockIdx.y * grp;
-    const int g = hq0 / grp;
-    const int nh = (G == 1) ? 1 : grp;  // query heads of this block
-    const int gid = threadIdx.x / LP, li = threadIdx.x % LP;
-    const int Sb = min(seq_lens[b], S);
-    const int T = ((Sb + NS - 1) / NS + 15) / 16 * 16;
-    const int t0 = s * T, t1 = min(t0 + T, Sb);
-    WF_STAMP(0);
-    __shared__ float sm_m[NG][G], sm_l[NG][G];
-    __shared__ __attribute__((aligned(16))) float sm_o[NG][G][D];
-
-    float m[G], l[G], o[G][8];
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-        m[h] = -INFINITY;
-        l[h] = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[h][j] = 0.f;
-    }
-    if (t0 < t1) {
-        const int64_t kvb = b * kv_sb + g * kv_sh + li * 8;
-        // chunk loads: clamped to the split (no branch around loads: hipcc counts vmcnt exactly)
-        auto load = [&](uint4 (&kr)[U], uint4 (&vr)[U], int c0) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int t = min(c0 + gid + NG * u, t1 - 1);
-                kr[u] = WF_KV_NT_B1 ? kv_ld16(K + kvb + (int64_t)t * D) : *reinterpret_cast<const uint4*>(K + kvb + (int64_t)t * D);
-                vr[u] = WF_KV_NT_B1 ? kv_ld16(V + kvb + (int64_t)t * D) : *reinterpret_cast<const uint4*>(V + kvb + (int64_t)t * D);
-            }
-        };
-        uint4 qv[G];  // bf16 pairs
-        uint4 kA[U], vA[U], kB[U], vB[U];
-#pragma unroll
-        for (int h = 0; h < G; ++h)
-            qv[h] = *reinterpret_cast<const uint4*>(q + b * q_sb + (int64_t)(hq0 + min(h, nh - 1)) * D + li * 8);
-        load(kA, vA, t0);
-        auto compute = [&](const uint4 (&kr)[U], const uint4 (&vr)[U], int c0) {
-            float sc[U][G];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t w[4] = {kr[u].x, kr[u].y, kr[u].z, kr[u].w};
-#pragma unroll
-                for (int h = 0; h < G; ++h) {
-                    const uint32_t qw[4] = {qv[h].x, qv[h].y, qv[h].z, qv[h].w};
-                    float d = 0.f;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        d = fmaf(bf_lo(qw[i]), bf_lo(w[i]), d);
-                        d = fmaf(bf_hi(qw[i]), bf_hi(w[i]), d);
-                    }
-                    d = group_reduce<LP>(d, OpAdd{});
-                    sc[u][h] = (c0 + gid + NG * u < t1) ? d * sm_scale : -INFINITY;
-                }
-            }
-#pragma unroll
-            for (int h = 0; h < G; ++h) {
-                float mx = m[h];
-#pragma unroll
-                for (int u = 0; u < U; ++u) mx = fmaxf(mx, sc[u][h]);
-                const float a = (mx == -INFINITY) ? 1.f : __expf(m[h] - mx);  // no key yet: nothing to rescale
-                l[h] *= a;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) o[h][j] *= a;
-                m[h] = mx;
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t w[4] = {vr[u].x, vr[u].y, vr[u].z, vr[u].w};
-                float vx[8];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) { vx[2 * i] = bf_lo(w[i]); vx[2 * i + 1] = bf_hi(w[i]); }
-#pragma unroll
-                for (int h = 0; h < G; ++h) {
-                    const float p = (sc[u][h] == -INFINITY) ? 0.f : __expf(sc[u][h] - m[h]);
-                    l[h] += p;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) o[h][j] = fmaf(p, vx[j], o[h][j]);
-                }
-            }
-        };
-        // block-uniform guards: only chunks that hold keys are loaded (a dead load still costs its
-        // latency where its destination registers are next written)
-        for (int c0 = t0; c0 < t1; c0 += 2 * CH) {
-            if (c0 + CH < t1) load(kB, vB, c0 + CH);  // next chunk in flight while this one is computed
-            compute(kA, vA, c0);
-            if (c0 + 2 * CH < t1) load(kA, vA, c0 + 2 * CH);
-            if (c0 + CH < t1) compute(kB, vB, c0 + CH);
-        }
-    }
-    WF_STAMP(1);
-    // merge the NG lane groups: first the four groups of each wave (lanes l, l ^ 16, l ^ 32 hold the
-    // same dims) by two shuffle steps, then the waves through LDS -- a 4-way merge per output instead
-    // of NG = 16 (the former all-LDS merge took ~1 us of a ~4.9 us launch, in-graph stamps r03)
-    // v_permlane16_swap / v_permlane32_swap on (v, v) hand every lane its (lower, upper) pair of
-    // lanes l, l ^ 16 (then l, l ^ 32) in the same order, so both partners compute the same merge
-    auto pair16 = [](float v) {
-        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-        return make_float2(__uint_as_float(r[0]), __uint_as_float(r[1]));
-    };
-    auto pair32 = [](float v) {
-        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-        return make_float2(__uint_as_float(r[0]), __uint_as_float(r[1]));
-    };
-    auto merge_step = [&](auto pair) {
-#pragma unroll
-        for (int h = 0; h < G; ++h) {
-            const float2 mm = pair(m[h]), ll = pair(l[h]);
-            const float M = fmaxf(mm.x, mm.y);
-            const float a = (mm.x == -INFINITY) ? 0.f : __expf(mm.x - M);
-            const float c = (mm.y == -INFINITY) ? 0.f : __expf(mm.y - M);
-            l[h] = ll.x * a + ll.y * c;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float2 oo = pair(o[h][j]);
-                o[h][j] = oo.x * a + oo.y * c;
-            }
-            m[h] = M;
-        }
-    };
-    merge_step(pair16);
-    merge_step(pair32);
-    constexpr int NWV = kAttnPartThreads / 64;
-    const int wv = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) < LP) {  // lane group 0 of each wave holds the wave's merge
-        if (li == 0) {
-#pragma unroll
-            for (int h = 0; h < G; ++h) { sm_m[wv][h] = m[h]; sm_l[wv][h] = l[h]; }
-        }
-#pragma unroll
-        for (int h = 0; h < G; ++h) {
-            *reinterpret_cast<float4*>(&sm_o[wv][h][li * 8]) = make_float4(o[h][0], o[h][1], o[h][2], o[h][3]);
-            *reinterpret_cast<float4*>(&sm_o[wv][h][li * 8 + 4]) = make_float4(o[h][4], o[h][5], o[h][6], o[h][7]);
-        }
-    }
-    __syncthreads();
-    constexpr int D4 = D / 4;
-    for (int idx = threadIdx.x; idx < nh * D4; idx += kAttnPartThreads) {
-        const int h = idx / D4, d = (idx - h * D4) * 4;
-        float mx = -INFINITY;
-#pragma unroll
-        for (int w = 0; w < NWV; ++w) mx = fmaxf(mx, sm_m[w][h]);
-        float ls = 0.f, os[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int w = 0; w < NWV; ++w) {
-            const float a = (sm_m[w][h] == -INFINITY) ? 0.f : __expf(sm_m[w][h] - mx);
-            ls += sm_l[w][h] * a;
-            const float4 ov = *reinterpret_cast<const float4*>(&sm_o[w][h][d]);
-            os[0] += ov.x * a; os[1] += ov.y * a; os[2] += ov.z * a; os[3] += ov.w * a;
-        }
-        const int64_t rec = (int64_t)(b * Hq + hq0 + h) * NS + s;
-        const int64_t oe = part_o_off<NS>(rec / NS, (int)(rec % NS), d);
-        if (row_out) {  // write-through: the head's last block merges them in this launch
-            st16_sc1(make_rsrc(o_out), (int)(4 * oe), __builtin_bit_cast(uint4, make_float4(os[0], os[1], os[2], os[3])));
-            if (d == 0) st_sc1(reinterpret_cast<uint64_t*>(ml_out) + rec, __builtin_bit_cast(uint64_t, make_float2(mx, ls)));
-        } else {
-            *reinterpret_cast<float4*>(o_out + oe) = make_float4(os[0], os[1], os[2], os[3]);
-            if (d == 0) ml_out[rec] = make_float2(mx, ls);
-        }
-    }
-    WF_STAMP(2);
-    if (G == 1 && row_out) {
-        // batch < 16: the head's last block merges its NS records into the bf16
-        // attention row (AttnRow::finish's arithmetic) so the O projection reads 256 B per head
-        // instead of every record: ticket per (sequence, head) (MI355X_MICROARCH.md Valid forms row 1)
-        __shared__ int sh_last;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned* c = cnt + (int64_t)(b * Hq + hq0) * 32;
-            const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sh_last = (old == (unsigned)NS - 1u);
-            if (old == (unsigned)NS - 1u) st_sc1(c, 0u);
-        }
-        __syncthreads();
-        if (!sh_last || threadIdx.x >= D / 4) return;
-        const int d = 4 * threadIdx.x;
-        const int64_t bh = (int64_t)b * Hq + hq0;
-        const __amdgpu_buffer_rsrc_t rml = make_rsrc(ml_out), ro = make_rsrc(o_out);
-        float mm[NS], ll[NS];
-        float4 ov[NS];
-#pragma unroll
-        for (int u = 0; u < NS / 2; ++u) {
-            const float4 v = __builtin_bit_cast(float4, ld16_sc1(rml, (int)(8 * (bh * NS) + 16 * u)));
-            mm[2 * u] = v.x; ll[2 * u] = v.y; mm[2 * u + 1] = v.z; ll[2 * u + 1] = v.w;
-        }
-#pragma unroll
-        for (int u = 0; u < NS; ++u) ov[u] = __builtin_bit_cast(float4, ld16_sc1(ro, (int)(4 * part_o_off<NS>(bh, u, d))));
-        float M = mm[0];
-#pragma unroll
-        for (int u = 1; u < NS; ++u) M = fmaxf(M, mm[u]);
-        float L = 0.f, O[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int u = 0; u < NS; ++u) {
-            const float w = (mm[u] == -INFINITY) ? 0.f : __expf(mm[u] - M);
-            L = fmaf(w, ll[u], L);
-            O[0] = fmaf(w, ov[u].x, O[0]); O[1] = fmaf(w, ov[u].y, O[1]);
-            O[2] = fmaf(w, ov[u].z, O[2]); O[3] = fmaf(w, ov[u].w, O[3]);
-        }
-        const float inv = 1.0f / L;
-        *reinterpret_cast<uint2*>(row_out + bh * D + d) =
-            make_uint2(pk_bf16(rbf(O[0] * inv), rbf(O[1] * inv)), pk_bf16(rbf(O[2] * inv), rbf(O[3] * inv)));
-    }
-}
-
-template <int G, int NS>
-__global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* __restrict__ q, int64_t q_sb,
-                                                                const uint16_t* __restrict__ K,
-                                                                const uint16_t* __restrict__ V, int64_t kv_sb,
-                                                                int64_t kv_sh, int Hq, int Hkv, int S,
-                                                                const int32_t* __restrict__ seq_lens, float sm_scale,
-                                                                float2* __restrict__ ml_out, float* __restrict__ o_out,
-                                                                uint16_t* __restrict__ row_out, unsigned* __restrict__ cnt) {
-    constexpr int NG = kAttnPartThreads / 16;
-    const int Sb = min(seq_lens[blockIdx.z], S);
-    const int T = ((Sb + NS - 1) / NS + 15) / 16 * 16;  // the body's split length
-    // (the batched untiled fallback, G > 1, keeps one body: two would double its LDS)
-    if (G == 1 && T <= kApUShort * NG)  // block-uniform
-        attn_part_body<G, NS, G == 1 ? kApUShort : kApULong>(q, q_sb, K, V, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale,
-                                                             ml_out, o_out, row_out, cnt);
-    else
-        attn_part_body<G, NS, kApULong>(q, q_sb, K, V, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, ml_out, o_out,
-                                        row_out, cnt);
-}
-
 // ---------------------------------------------------------------------------------------------
 // The reference's attention AS IT RUNS (scripts/direct_inference_full.py:241: torch 2.10's CPU
 // flash SDPA on bf16; restated in oracle/wf_oracle.c orc_attention_sdpa_cpu_bf16 and pinned by
@@ -594,17 +351,23 @@ __global__ __launch_bounds__(kAttnPartThreads) void k_attn_part(const uint16_t* 
 // tail, P = bf16(e) into P.V, the UNROUNDED e into the row sum, blocks combined by
 // r_c = expf(M_{c-1} - M_c), out = bf16(dst * (1 / sum)).
 //
-// Decode step, batch < 16 and untiled caches: block (split s, query head, sequence) as
-// k_attn_part (kAttnPartSplits1 splits of T = round_up(ceil(S / NS), 16) keys, 16-lane groups),
-// in two phases around an in-launch exchange of the 512-key block maxima:
+// Decode step, batch < 16 and untiled caches: block (split s, query head, sequence), kAttnPartSplits1
+// splits of T = round_up(ceil(S / NS), 16) keys read by 16-lane groups (8 dims per lane, a wave
+// reads 4 contiguous 256-byte key rows), in two phases around an in-launch exchange of the 512-key
+// block maxima:
 //   1. q.k of the split's keys (products exact in fp32, summed in f64 and rounded once -- torch's
 //      oneDNN GEMM is that close to exact, tests/golden/sdpa_probe.py), the split's per-block maxima
-//      published write-through; one lane polls the head's arrival counter (all NS splits);
-//   2. wave 0 folds the NS x 4 published maxima into M_c, r_c and the suffix products R, every
+//      published as epoch-tagged granules; wave 0 polls the head's granules (all NS splits);
+//   2. wave 0 folds the NS x 3 published maxima into M_c, r_c and the suffix products R, every
 //      lane forms P and e of its keys, scales by the product of the r's after the key's block
 //      (1.0 exactly inside the split's last block), and accumulates l = sum e and o = sum P v.
-// Every record is then in the frame of the head's last block; the head's last block (ticket)
-// sums the NS records and writes out = bf16(O * (1 / L)) into the bf16 attention row.
+// Every record (m = 0, l, o) is then in the frame of the head's last block; the head's last block
+// (merge ticket) sums the NS records and writes out = bf16(O * (1 / L)) into the bf16 attention row,
+// resets the ticket and stores this launch's tag as the head's epoch word (the next launch's tag is
+// that + 1). Merging in the O projection's input stage instead (round 5, same box): attention 10.4
+// -> 9.0 us, O 4.4 -> 6.0 us per layer (every O block reads all 83 KB of records), 1019 -> 1011
+// tok/s. Pipelined polls (four in flight, 256 clocks apart) did not shorten the exchange (2.2 ->
+// 2.6 us).
 // Residency: every split of a head must be resident while its siblings poll: the host launches
 // at most kSdpaMaxBlocks blocks per launch (B = 1: 160), below the chip's resident count.
 // ---------------------------------------------------------------------------------------------
@@ -968,27 +731,13 @@ __global__ __launch_bounds__(kAttnPartThreads) WF_SDPA_WPE void k_attn_sdpa(cons
 }
 
 // ---------------------------------------------------------------------------------------------
-// Batched decode attention partials on the bf16 matrix cores (v_mfma_f32_16x16x32_bf16), on the
-// K / V caches in their tile layouts (wf_norm.h k_tile_off / v_tile_off; S % 32 == 0): every
-// fragment load is one contiguous KiB per wave. Same partial records as k_attn_part (a record holds
-// the keys its block's waves took, not a contiguous range: the merge is order-free). Block
-// (split s, kv head g, sequence b) = 4 waves; wave w walks 32-key tiles base = 32 (4 s + w) + 1024 i
-// (round-robin over the 32 waves of (b, g)), online softmax per head.
-//   scores: two 16-key MFMA tiles, A = K rows (tile tau, row 4a + r <- key base + 8a + 4 tau + r),
-//     B = Q^T (column = query head of the group, rows >= grp zero; lane quarter q takes dims
-//     32c + 8q .. +8 of MFMA c = 0..3, the same for both operands). Lane (head h, q)
-//     then holds the scores of keys base + 8q + 0..7 -- exactly the A fragment (P rows = heads,
-//     k = keys) of the P.V MFMA, whose B fragment is V[base + 8q, +8)[16n + l16].
-//   P enters the MFMA as bf16 hi + lo (two MFMAs), so P.V keeps ~16 mantissa bits (the VALU path's
-//     fp32 p within ~1e-5 relative). Scores of keys past the split are masked to -inf (select, so a
-//     stale K row cannot leak a NaN), V entries past it zeroed (0 * stale = 0).
+// Fragment types and one-byte K/V widening shared by the batched decode attention
+// (k_attn_sdpa_mfma): K / V caches in their tile layouts (wf_norm.h k_tile_off / v_tile_off), every
+// fragment load one contiguous KiB per wave.
 // ---------------------------------------------------------------------------------------------
 typedef short v8s_t __attribute__((ext_vector_type(8)));
 typedef float v4f_t __attribute__((ext_vector_type(4)));
 constexpr int kAttnMfmaMaxGrp = 8;
-// WREC: one partial record per WAVE instead of per block -- grid.x = kAttnPartSplits / 4, the 8
-// waves of (b, g) take the 32-key tiles round-robin (wave r: tiles r, r + 8, ...) and each writes
-// its own (m, l, o) record: no LDS merge or barrier, and a wave streams several tiles per launch.
 // FP8 (OCP e4m3fn) K/V caches: a fragment is 8 one-byte keys / dims (8 bytes per lane, 512
 // contiguous bytes per wave-instruction), widened to bf16 in registers (exact: every e4m3 value is
 // a bf16 value). The per-layer scales are folded into the score scale (K) and the partial records
@@ -1057,257 +806,16 @@ struct KvFrag<1> : KvFrag8<1> {};
 template <>
 struct KvFrag<2> : KvFrag8<2> {};
 
-// PAIR: records of 2 waves -- grid.x = kAttnPartSplits / 2, the 16 waves of (b, g) take the
-// tiles round-robin and each block merges its wave pairs (0, 1) and (2, 3) into 2 records: half the
-// per-tile block overheads of the 4-wave records, twice the waves per sequence of WREC.
-// TAIL: the records are stored write-through and the last block of each sequence forms the O
-// projection's input row (wf_norm.h AttnTail) -- no k_rownorm_attn launch.
-template <bool DB, bool RR, bool WREC = false, int KV8 = 0, bool PAIR = false, bool TAIL = false>
-__global__ __launch_bounds__(256, DB ? 2 : 4) void k_attn_mfma(const uint16_t* __restrict__ q, int64_t q_sb,
-                                                   const uint16_t* __restrict__ K, const uint16_t* __restrict__ Vt,
-                                                   int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv, int S,
-                                                   const int32_t* __restrict__ seq_lens, float sm_scale,
-                                                   float2* __restrict__ ml_out, float* __restrict__ o_out,
-                                                   const int32_t* __restrict__ pt, int pps, int npages, int64_t kv_pgs,
-                                                   float v_scale, AttnTail tail) {
-    static_assert(!(TAIL && (WREC || PAIR)), "the tail follows the per-block records");
-    constexpr int D = 128;
-    using KF = KvFrag<KV8>;
-    using FT = typename KF::T;
-    const int s = WREC ? 4 * (int)blockIdx.x + (int)(threadIdx.x >> 6) : (int)blockIdx.x, g = blockIdx.y, b = blockIdx.z;
-    static_assert(!(PAIR && (WREC || RR)), "one schedule");
-    const int grp = Hq / Hkv, hq0 = g * grp;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
-    const int Sb = min(seq_lens[b], S);
-    // 32-key tiles dealt round-robin over the 4 * kAttnPartSplits waves of (b, g): wave (s, w)
-    // takes tiles 4 s + w + 32 i, so per-wave tile counts differ by at most one and a block's four
-    // waves finish together (a contiguous split per block left wave 0 with twice the tiles)
-    const int T = ((Sb + kAttnPartSplits - 1) / kAttnPartSplits + 31) / 32 * 32;
-    const int kStride = PAIR ? 32 * 2 * kAttnPartSplits
-                              : (WREC ? 32 * kAttnPartSplits : (RR ? 32 * 4 * kAttnPartSplits : 128));
-    const int t1 = (RR || WREC || PAIR) ? Sb : min(s * T + T, Sb);
-    __shared__ float sm_m[4][kAttnMfmaMaxGrp], sm_l[4][kAttnMfmaMaxGrp];
-    __shared__ __attribute__((aligned(16))) float sm_o[4][kAttnMfmaMaxGrp][D];
-    // dense: (sequence, kv head) slab of S / 32 blocks; paged: block j of sequence b in page
-    // pt[b][j] (kv_sb = 0, kv_sh = the kv head stride inside a page)
-    // (element offsets: the fragment loaders scale them by the element size)
-    const int64_t kvo = b * kv_sb + g * kv_sh + lane * 8;
-    const int32_t* ptb = pt ? pt + (int64_t)b * pps : nullptr;
-    WF_STAMP(0);
-
-    float m_run = -INFINITY, l_run = 0.f;
-    v4f_t acc[8];
-#pragma unroll
-    for (int n = 0; n < 8; ++n) acc[n] = v4f_t{0.f, 0.f, 0.f, 0.f};
-    int base = PAIR ? 32 * (4 * s + wave) : (WREC ? 32 * s : (RR ? 32 * (4 * s + wave) : s * T + 32 * wave));
-    if (base < t1) {
-        v8s_t qf[4];
-        {
-            const uint16_t* qp = q + b * q_sb + (int64_t)(hq0 + min(l16, grp - 1)) * D + 8 * q4;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                uint4 t = *reinterpret_cast<const uint4*>(qp + 32 * c);
-                if (l16 >= grp) t = make_uint4(0, 0, 0, 0);
-                qf[c] = __builtin_bit_cast(v8s_t, t);
-            }
-        }
-        auto load = [&](FT (&kr)[2][4], FT (&vr)[8], int bs) {
-            // 32 keys x 128 dims per tile block (bs is wave-uniform: the page id is a scalar load)
-            const int64_t blk = ptb ? (int64_t)min(max(ptb[__builtin_amdgcn_readfirstlane(bs) >> 5], 0), npages - 1) * kv_pgs
-                                    : (int64_t)(bs >> 5) * 4096;
-#pragma unroll
-            for (int tau = 0; tau < 2; ++tau)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) kr[tau][c] = KF::ld(K, kvo + blk + (tau * 4 + c) * 512);
-#pragma unroll
-            for (int n = 0; n < 8; ++n) vr[n] = KF::ld(Vt, kvo + blk + n * 512);
-        };
-        auto compute = [&](const FT (&kr)[2][4], const FT (&vr)[8], int bs) {
-            v4f_t sc[2];
-#pragma unroll
-            for (int tau = 0; tau < 2; ++tau) {
-                sc[tau] = v4f_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    sc[tau] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8s_t, KF::bf(kr[tau][c])),
-                                                                      qf[c], sc[tau], 0, 0, 0);
-            }
-            const int lim = t1 - bs - 8 * q4;  // valid keys among this lane's 8
-            float x[8], mx = -INFINITY;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                x[e] = e < lim ? sc[e >> 2][e & 3] * sm_scale : -INFINITY;
-                mx = fmaxf(mx, x[e]);
-            }
-            mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));  // the tile has >= 1 valid key: finite
-            const float mnew = fmaxf(m_run, mx);
-            const float alpha = __expf(m_run - mnew);  // 0 on the first tile
-            m_run = mnew;
-            float p[8], ps = 0.f;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                p[e] = __expf(x[e] - mnew);
-                ps += p[e];
-            }
-            l_run = l_run * alpha + ps;  // per-lane partial (summed over the quarters at the end)
-            uint32_t hi[4], lo[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                hi[j] = pk_bf16(p[2 * j], p[2 * j + 1]);
-                lo[j] = pk_bf16(p[2 * j] - bf_lo(hi[j]), p[2 * j + 1] - bf_hi(hi[j]));
-            }
-            const v8s_t ph = __builtin_bit_cast(v8s_t, make_uint4(hi[0], hi[1], hi[2], hi[3]));
-            const v8s_t pl = __builtin_bit_cast(v8s_t, make_uint4(lo[0], lo[1], lo[2], lo[3]));
-            float ar[4];  // rescale factor of output row (head) 4 q4 + r
-#pragma unroll
-            for (int r = 0; r < 4; ++r) ar[r] = __shfl(alpha, 4 * q4 + r, 64);
-#pragma unroll
-            for (int n = 0; n < 8; ++n) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) acc[n][r] *= ar[r];
-                const v8s_t vf = __builtin_bit_cast(v8s_t, KF::bf(KF::mask(vr[n], lim)));
-                acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vf, acc[n], 0, 0, 0);
-                acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vf, acc[n], 0, 0, 0);
-            }
-        };
-        FT kA[2][4], vA[8];
-        load(kA, vA, base);
-        if constexpr (DB) {
-            FT kB[2][4], vB[8];
-            for (; base < t1; base += 2 * kStride) {
-                const int nb = base + kStride;
-                if (nb < t1) load(kB, vB, nb);
-                compute(kA, vA, base);
-                if (nb >= t1) break;
-                if (nb + kStride < t1) load(kA, vA, nb + kStride);
-                compute(kB, vB, nb);
-            }
-        } else {
-            for (; base < t1; base += kStride) {
-                compute(kA, vA, base);
-                if (base + kStride < t1) load(kA, vA, base + kStride);
-            }
-        }
-    }
-    WF_STAMP(1);
-    l_run += __shfl_xor(l_run, 16, 64);
-    l_run += __shfl_xor(l_run, 32, 64);
-    if constexpr (KV8 != 0) {  // o = v_scale * sum p v8 (the partial records carry the V scale)
-#pragma unroll
-        for (int n = 0; n < 8; ++n)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) acc[n][r] *= v_scale;
-    }
-    if constexpr (WREC) {  // this wave's record s of each of its group's heads
-        const int64_t rec0 = (int64_t)(b * Hq + hq0) * kAttnPartSplits + s;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int h = 4 * q4 + r;
-            if (h < grp) {
-#pragma unroll
-                for (int n = 0; n < 8; ++n) o_out[part_o_off((int64_t)b * Hq + hq0 + h, s, 16 * n + l16)] = acc[n][r];
-            }
-        }
-        if (q4 == 0 && l16 < grp) ml_out[rec0 + (int64_t)l16 * kAttnPartSplits] = make_float2(m_run, l_run);
-        return;
-    }
-    if (q4 == 0 && l16 < grp) {
-        sm_m[wave][l16] = m_run;
-        sm_l[wave][l16] = l_run;
-    }
-#pragma unroll
-    for (int n = 0; n < 8; ++n)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            if (4 * q4 + r < grp) sm_o[wave][4 * q4 + r][16 * n + l16] = acc[n][r];
-    __syncthreads();
-    if constexpr (PAIR) {  // waves (2p, 2p + 1) -> record 2 blockIdx.x + p
-        for (int idx = threadIdx.x; idx < 2 * grp * (D / 4); idx += 256) {
-            const int p = idx / (grp * (D / 4)), hd = idx % (grp * (D / 4));
-            const int h = hd / (D / 4), d = (hd % (D / 4)) * 4;
-            const float m0 = sm_m[2 * p][h], m1 = sm_m[2 * p + 1][h], mx = fmaxf(m0, m1);
-            const float a0 = m0 == -INFINITY ? 0.f : __expf(m0 - mx), a1 = m1 == -INFINITY ? 0.f : __expf(m1 - mx);
-            const float ls = sm_l[2 * p][h] * a0 + sm_l[2 * p + 1][h] * a1;
-            const float4 o0 = *reinterpret_cast<const float4*>(&sm_o[2 * p][h][d]);
-            const float4 o1 = *reinterpret_cast<const float4*>(&sm_o[2 * p + 1][h][d]);
-            const int64_t rec = (int64_t)(b * Hq + hq0 + h) * kAttnPartSplits + 2 * s + p;
-            *reinterpret_cast<float4*>(o_out + part_o_off(rec / kAttnPartSplits, (int)(rec % kAttnPartSplits), d)) =
-                make_float4(o0.x * a0 + o1.x * a1, o0.y * a0 + o1.y * a1, o0.z * a0 + o1.z * a1, o0.w * a0 + o1.w * a1);
-            if (d == 0) ml_out[rec] = make_float2(mx, ls);
-        }
-        return;
-    }
-    for (int idx = threadIdx.x; idx < grp * (D / 4); idx += 256) {
-        const int h = idx / (D / 4), d = (idx % (D / 4)) * 4;
-        float mx = -INFINITY;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) mx = fmaxf(mx, sm_m[w][h]);
-        float ls = 0.f, os[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const float a = (sm_m[w][h] == -INFINITY) ? 0.f : __expf(sm_m[w][h] - mx);
-            ls += sm_l[w][h] * a;
-            const float4 ov = *reinterpret_cast<const float4*>(&sm_o[w][h][d]);
-            os[0] += ov.x * a; os[1] += ov.y * a; os[2] += ov.z * a; os[3] += ov.w * a;
-        }
-        const int64_t rec = (int64_t)(b * Hq + hq0 + h) * kAttnPartSplits + s;
-        const int64_t oe = part_o_off(rec / kAttnPartSplits, (int)(rec % kAttnPartSplits), d);
-        if constexpr (TAIL) {  // write-through: the sequence's last block reads them in this launch
-            st16_sc1(make_rsrc(o_out), (int)(4 * oe), __builtin_bit_cast(uint4, make_float4(os[0], os[1], os[2], os[3])));
-            if (d == 0) st_sc1(reinterpret_cast<uint64_t*>(ml_out) + rec, __builtin_bit_cast(uint64_t, make_float2(mx, ls)));
-        } else {
-            *reinterpret_cast<float4*>(o_out + oe) = make_float4(os[0], os[1], os[2], os[3]);
-            if (d == 0) ml_out[rec] = make_float2(mx, ls);
-        }
-    }
-    WF_STAMP(2);
-    if constexpr (TAIL) {
-        // ticket of sequence b (MI355X_MICROARCH.md Valid forms row 1): every storing wave drains its
-        // write-through stores, the block meets at a barrier, one lane adds; the block whose add
-        // returns n - 1 re-arms the counter and reads the records with sc1 loads
-        __shared__ int sh_last;
-        __shared__ float red[16];
-        __shared__ int red_i[4];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned* c = tail.cnt + (int64_t)b * kTailLine;
-            const unsigned n = gridDim.x * gridDim.y;
-            const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sh_last = (old == n - 1u);
-            if (old == n - 1u) st_sc1(c, 0u);
-        }
-        __syncthreads();
-        if (!sh_last) return;
-        const int Kr = Hq * D, nkb = Kr >> 7;
-        AttnRow<2, 256, kAttnPartSplits> ar;
-        ar.template issue<true>(ml_out, o_out, b, Hq, D);
-        NormRow<2, 256> nr;
-        nr.issue_w(tail.nw, Kr);
-        float y[2][8];
-        ar.finish(Hq, D, y);
-        const float sf = norm_core_e512(nr, Kr, tail.eps, y, red);
-        int as = quant_row_tiled<2, 256>(y, sf, Kr / 8, tail.q8, b, nkb);
-        as = wave_sum_i(as);
-        if ((threadIdx.x & 63) == 0) red_i[threadIdx.x >> 6] = as;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            tail.asum[b] = red_i[0] + red_i[1] + red_i[2] + red_i[3];
-            tail.sf[b] = sf;
-        }
-        WF_STAMP(3);
-    }
-}
-
 // ---------------------------------------------------------------------------------------------
 // Batched decode attention (batch >= 16, tile-layout K/V) with the reference's SDPA arithmetic
 // (k_attn_sdpa's comment; oracle/wf_oracle.c orc_attention_sdpa_cpu_bf16): one block per (kv head
 // g, sequence b) walks the sequence's 512-key blocks in order, exactly the CPU kernel's loop, so
 // the running max needs no exchange between blocks of the launch. 4 waves; wave w takes tiles
 // w, w + 4, w + 8, w + 12 (32 keys each) of every 512-key block, in two passes:
-//   pass 1: K fragments -> QK on the bf16 matrix cores (k_attn_mfma's layouts: lane (head l16,
-//     quarter q4) holds the scores of keys base + 8 q4 + 0..7), the wave's per-head maximum;
+//   pass 1: K fragments -> QK on the bf16 matrix cores (A = K rows: tile tau, row 4 a + r <- key
+//     base + 8 a + 4 tau + r; B = Q^T, lane quarter q4 takes dims 32 c + 8 q4 .. + 8 of MFMA c:
+//     lane (head l16, quarter q4) then holds the scores of keys base + 8 q4 + 0..7, exactly the A
+//     fragment of the P.V MFMA), the wave's per-head maximum;
 //     the four waves' maxima meet in LDS (one barrier per block) -> M_c, r_c = expf(M_{c-1} - M_c);
 //   pass 2: V fragments -> e = fexp_u20 / expf of (s - M_c) (vector part / tail of the block),
 //     l = l r_c + sum e (unrounded), acc = acc r_c + bf16(e) . V (ONE bf16 MFMA term: P IS bf16).
@@ -1699,22 +1207,21 @@ __global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __res
 
 constexpr int kPfMaxTiles = 256;  // 32-key tiles per sequence (max_seq <= 8192)
 
-// Prefill attention, flash style on 32 x 32 bf16 matrix cores (the default for bf16 K/V): block =
-// one row group of kPrefillRowGroup = 32 consecutive rows of one slot x kv head g; wave w takes
-// tokens 8 w .. 8 w + 7 x the group's 4 query heads = 32 query columns (column c = token 8 w + c / 4,
-// head c % 4). Per 32-key tile (staged once per block in a 4 x 16 KiB LDS ring by LDS-DMA, each
-// wave a quarter, P - 2 tiles in flight beyond the one being read):
-//   S^T (32 keys x 32 queries) = K . Q^T: 8 v_mfma_f32_32x32x16_bf16 (K fragments = 16 bytes of
-//       one key's 8 dims, ds_read_b128; Q^T fragments in registers for the whole key range);
-//   online softmax in log2 units: lane (c, h) holds keys j % 4 + 8 (j / 4) + 4 h of column c, so a
-//       column's max / sum needs one v_permlane32_swap, and the rescale factor is the lane's own;
-//   O^T (128 dims x 32 queries) += V^T . P^T: 8 MFMAs; P^T's fragments are the score lanes as they
-//       stand (the QK MFMA takes the keys permuted so that k-slot i of lane half h is key
-//       16 s + 8 h + i), V^T's fragments one 16-byte ds_read of the V tile layout each.
-// Per-column causal limit (masking only on diagonal tiles), P as three bf16 terms for the P.V MFMAs
-// (~24 mantissa bits: fp32 P), V rows past the block's last position zeroed. Heavy row groups
-// (late positions) are launched first. A column's result depends only on its own key range (tiles
-// past it add p = 0 at alpha = 1), so chunked prefill stays bit-exact.
+// Prefill attention on 32 x 32 bf16 matrix cores (k_attn_prefill_sdpa, the default for bf16 K/V):
+// block = one row group of kPrefillRowGroup = 32 consecutive rows of one slot x kv head g; wave w
+// takes tokens 8 w .. 8 w + 7 x the group's 4 query heads = 32 query columns (column c = token
+// 8 w + c / 4, head c % 4). K/V tiles (32 keys) are staged once per block in a 4 x 16 KiB LDS ring by
+// LDS-DMA, each wave a quarter, P - 2 stages in flight beyond the one being read:
+//   S^T (32 keys x 32 queries) = K . Q^T: 8 v_mfma_f32_32x32x16_bf16 (K fragments = 16 bytes of one
+//       key's 8 dims, ds_read_b128; Q^T fragments in registers for the whole key range); lane (c, h)
+//       holds keys (j & 7) + 8 h + 16 (j >> 3) of column c, so a column's max / sum needs one
+//       v_permlane32_swap;
+//   O^T (128 dims x 32 queries) += V^T . P^T: P^T's fragments are the score lanes as they stand
+//       (the QK MFMA takes the keys permuted so that k-slot i of lane half h is key 16 s + 8 h + i),
+//       V^T's fragments one 16-byte ds_read of the V tile layout each.
+// Per-column causal limit (masking only where a tile crosses it), V rows past the block's last
+// position zeroed. A column's result depends only on its own key range, so chunked prefill stays
+// bit-exact.
 constexpr int kFaStages = 4;  // 64 KiB ring + page ids: two blocks per CU
 typedef __bf16 v8bf_t __attribute__((ext_vector_type(8)));
 typedef float v16f_t __attribute__((ext_vector_type(16)));
@@ -1726,239 +1233,12 @@ __device__ __forceinline__ float swap32_sum(float v) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
-#ifndef WF_FA_STUDY  // diagnostic builds only (tools/build_variant.sh): 1 DMA + barriers only, 2 compute on the
-#define WF_FA_STUDY 0  // first ring fill only, 3 no exponentials, 4 no P.V MFMAs; never libwfbitnet.so
-#endif
-__global__ __launch_bounds__(256, 2) void k_attn_prefill_fa(const uint16_t* __restrict__ q, int64_t q_rs,
-                                                            const uint16_t* __restrict__ K,
-                                                            const uint16_t* __restrict__ Vt, int64_t kv_sb,
-                                                            int64_t kv_sh, const int32_t* __restrict__ row_pos,
-                                                            const int32_t* __restrict__ row_slot, int M,
-                                                            float sl2, const int32_t* __restrict__ pt, int pps,
-                                                            int npages, int64_t kv_pgs, uint16_t* __restrict__ out,
-                                                            int64_t o_rs, int xchunk) {
-    constexpr int STUDY = WF_FA_STUDY;
-    constexpr int D = 128, P = kFaStages;
-    constexpr int kSlot = 16384;  // K 8 KiB + V 8 KiB of one 32-key tile, as in the cache
-    __shared__ __attribute__((aligned(16))) uint8_t ring[P * kSlot];
-    __shared__ int s_page[kPfMaxTiles];
-    const int nrb = M / 32;
-    // Work item = (kv head g, row group rbi), g-major, so consecutive items share a sequence's K/V.
-    // xchunk > 0 (1-D grid of 8 xchunk blocks): the blocks one XCD receives (b % 8, dealt round-robin)
-    // take one contiguous chunk of xchunk items, last first -- an XCD streams one (sequence, kv head)
-    // K/V at a time out of its own L2, heavy (late) row groups of it first. Else: grid (nrb, Hkv),
-    // late row groups first.
-    int g, rbi;
-    if (xchunk > 0) {
-        const int b = blockIdx.x, item = (b & 7) * xchunk + (xchunk - 1 - (b >> 3));
-        g = item / nrb;
-        rbi = item - g * nrb;
-    } else {
-        g = blockIdx.y;
-        rbi = nrb - 1 - (int)blockIdx.x;
-    }
-    const int hq0 = g * 4;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
-    const int rb = rbi * 32;
-    const int slot = __builtin_amdgcn_readfirstlane(row_slot[rb]);
-    const int qrow = rb + 8 * wave + (c >> 2);
-    const int lim_q = row_pos[qrow] + 1;  // keys [0, lim_q) of column c
-    int lim_b = 0;
-    for (int t = 0; t < 32; ++t) lim_b = max(lim_b, row_pos[rb + t] + 1);
-    // the C-ABI only documents row_pos < max_seq: clamp, so a bad position cannot run the page fill
-    // (s_page[kPfMaxTiles]) or the DMAs past the slot's cache (k_attn_prefill clamps the same way)
-    lim_b = __builtin_amdgcn_readfirstlane(min(lim_b, 32 * min(pps, kPfMaxTiles)));
-    const float flq = (float)min(lim_q, lim_b);  // positions < 2^24: exact
-    const int lim_w = (int)wave_max(flq), lim_min = (int)-wave_max(-flq);
-    v8bf_t qf[8];  // Q^T fragments: column c, dims 16 s + 8 h .. + 7
-    {
-        const uint16_t* qp = q + (int64_t)qrow * q_rs + (int64_t)(hq0 + (c & 3)) * D + 8 * h;
-#pragma unroll
-        for (int s2 = 0; s2 < 8; ++s2) qf[s2] = __builtin_bit_cast(v8bf_t, *reinterpret_cast<const uint4*>(qp + 16 * s2));
-    }
-    // wait for q before the ring's asm DMAs exist (hipcc cannot count those)
-#pragma unroll
-    for (int s2 = 0; s2 < 8; ++s2) asm volatile("" : "+v"(qf[s2]));
-    const int ntiles = (lim_b + 31) >> 5;
-    const uint16_t* Kg = K + (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;
-    const uint16_t* Vg = Vt + (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;
-    if (pt) {
-        for (int t = threadIdx.x; t < ntiles; t += 256) s_page[t] = min(max(pt[(int64_t)slot * pps + t], 0), npages - 1);
-        __syncthreads();
-    }
-    auto issue = [&](int t) {  // wave w DMAs pieces 4w .. 4w + 3 of tile t (K 0..7, V 8..15)
-        const int64_t blk = pt ? (int64_t)s_page[t] * kv_pgs : (int64_t)t * 4096;
-        uint8_t* st = ring + (t % P) * kSlot;
-        if (STUDY == 2 && t >= P) return;  // study: no DMA after the first ring fill
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-            const int j = wave * 4 + jj;
-            glds16_asm((j < 8 ? Kg : Vg) + blk + (j & 7) * 512, st + j * 1024);
-        }
-    };
-    float m_run = -INFINITY, l_run = 0.f;
-    v16f_t oacc[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) oacc[mt][e] = 0.f;
-    // Keys enter the QK MFMA permuted: row r of S^T is key o = r with bits 2 and 3 swapped. Lane
-    // (c, h) then holds, for j < 16, the score of key (j & 7) + 8 h + 16 (j >> 3), so the eight
-    // P^T k-slots of k-step s are keys 16 s + 8 h + 0..7: one 16-byte piece of the V tile layout
-    // (keys contiguous per dim). K fragment of row c, dims 16 s + 8 h (k_tile_off * 2):
-    // ((tau 16 + dg) 16 + row) x 16 bytes; K and V reads are bank-conflict-free.
-    const int o = (c & ~12) | ((c & 4) << 1) | ((c & 8) >> 1);
-    const int koff = ((((o >> 2) & 1) * 16 + h) * 16 + 4 * (o >> 3) + (o & 3)) * 16;
-    // S^T of one tile: all 8 K fragments in flight, then the 8 MFMAs (their results are read one
-    // iteration later: the QK of tile t + 1 runs on the matrix pipe during tile t's softmax)
-    auto qk = [&](const uint8_t* st, v16f_t& sacc) {
-        uint4 kf[8];
-#pragma unroll
-        for (int s2 = 0; s2 < 8; ++s2) kf[s2] = *reinterpret_cast<const uint4*>(st + koff + s2 * 512);
-#pragma unroll
-        for (int e = 0; e < 16; ++e) sacc[e] = 0.f;
-#pragma unroll
-        for (int s2 = 0; s2 < 8; ++s2)
-            sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf_t, kf[s2]), qf[s2], sacc, 0, 0, 0);
-    };
-    // online softmax of tile t's scores, then O^T += V^T . P^T
-    auto softmax_pv = [&](const uint8_t* st, const v16f_t& sacc, int bs) {
-        uint4 vv[4][2];  // V^T fragments (dim 32 mt + c, keys 16 s + 8 h + 0..7): issued first
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-            const int d = 32 * mt + c, n = d >> 4, l = d & 15;
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2)
-                vv[mt][s2] = *reinterpret_cast<const uint4*>(st + 8192 + ((n * 4 + 2 * s2 + h) * 16 + l) * 16);
-        }
-        float x[16], mx = -INFINITY;
-        if (bs + 32 > lim_min) {  // diagonal tile: per-column limit
-            const int lim = lim_q - bs - 8 * h;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                x[j] = (j & 7) + 16 * (j >> 3) < lim ? sacc[j] * sl2 : -INFINITY;
-                mx = fmaxf(mx, x[j]);
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                x[j] = sacc[j] * sl2;
-                mx = fmaxf(mx, x[j]);
-            }
-        }
-        mx = swap32_max(mx);
-        const float mnew = fmaxf(m_run, mx);  // finite: key 0 is valid for every column
-        const float alpha = STUDY == 3 ? 1.0f : __builtin_amdgcn_exp2f(m_run - mnew);
-        m_run = mnew;
-        float ps = 0.f;
-        // P^T as three bf16 terms hi + mid + lo (p to ~24 bits: the fp32 P of the decode step's VALU
-        // kernel). bf16-only P moved 2.5 % of the layer-1 K/V rows of an 8 x 2048 prefill off the
-        // oracle (the requantised attn_sub / ffn_sub inputs turn bf16-boundary flips of the
-        // attention output into whole code steps). At 2048 positions, layer 1 vs the oracle: hi + lo
-        // 71 positions > 1e-3 (rel-L2 4.28e-3), hi + mid + lo 41 (3.29e-3; the batch-1 decode path
-        // itself 32, 2.95e-3) for +2 % prefill time (51.0 -> 52.0 ms).
-        uint32_t pk[8], pr[8], pq[8];
-#pragma unroll
-        for (int j = 0; j < 16; j += 2) {
-            // (study 3: no exponentials -- the softmax's transcendental cost)
-            const float p0 = STUDY == 3 ? x[j] - mnew : __builtin_amdgcn_exp2f(x[j] - mnew);
-            const float p1 = STUDY == 3 ? x[j + 1] - mnew : __builtin_amdgcn_exp2f(x[j + 1] - mnew);
-            ps += p0;
-            ps += p1;
-            pk[j >> 1] = pk_bf16(p0, p1);
-            const float r0 = p0 - bf_lo(pk[j >> 1]), r1 = p1 - bf_hi(pk[j >> 1]);
-            pr[j >> 1] = pk_bf16(r0, r1);
-            pq[j >> 1] = pk_bf16(r0 - bf_lo(pr[j >> 1]), r1 - bf_hi(pr[j >> 1]));
-        }
-        l_run = l_run * alpha + ps;
-        if (__any(alpha != 1.0f)) {
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) oacc[mt][e] *= alpha;
-        }
-        const v8bf_t pb0 = __builtin_bit_cast(v8bf_t, make_uint4(pk[0], pk[1], pk[2], pk[3]));
-        const v8bf_t pb1 = __builtin_bit_cast(v8bf_t, make_uint4(pk[4], pk[5], pk[6], pk[7]));
-        const v8bf_t pc0 = __builtin_bit_cast(v8bf_t, make_uint4(pr[0], pr[1], pr[2], pr[3]));
-        const v8bf_t pc1 = __builtin_bit_cast(v8bf_t, make_uint4(pr[4], pr[5], pr[6], pr[7]));
-        const v8bf_t pd0 = __builtin_bit_cast(v8bf_t, make_uint4(pq[0], pq[1], pq[2], pq[3]));
-        const v8bf_t pd1 = __builtin_bit_cast(v8bf_t, make_uint4(pq[4], pq[5], pq[6], pq[7]));
-        const int limv = lim_b - bs - 8 * h;  // V keys past the block's last position: zero (stale)
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                uint4 a = vv[mt][s2];
-                if (limv < 32) {  // keys 16 s2 + 8 h + 0..7
-                    const int k0 = 16 * s2;
-                    a.x &= (k0 < limv ? 0xffffu : 0u) | (k0 + 1 < limv ? 0xffff0000u : 0u);
-                    a.y &= (k0 + 2 < limv ? 0xffffu : 0u) | (k0 + 3 < limv ? 0xffff0000u : 0u);
-                    a.z &= (k0 + 4 < limv ? 0xffffu : 0u) | (k0 + 5 < limv ? 0xffff0000u : 0u);
-                    a.w &= (k0 + 6 < limv ? 0xffffu : 0u) | (k0 + 7 < limv ? 0xffff0000u : 0u);
-                }
-                const v8bf_t vf = __builtin_bit_cast(v8bf_t, a);
-                if (STUDY == 4) {  // study: no P.V MFMAs (keep the operands live)
-                    uint4 pa = __builtin_bit_cast(uint4, s2 ? pb1 : pb0);
-                    reg_fence(a);
-                    reg_fence(pa);
-                    continue;
-                }
-                oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, s2 ? pb1 : pb0, oacc[mt], 0, 0, 0);
-                oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, s2 ? pc1 : pc0, oacc[mt], 0, 0, 0);
-                oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, s2 ? pd1 : pd0, oacc[mt], 0, 0, 0);
-            }
-        }
-    };
-    // ring: tiles 0 .. P - 2 issued up front, tile t + P - 1 at iteration t (into tile t - 1's slot)
-#pragma unroll
-    for (int t = 0; t < P - 1; ++t)
-        if (t < ntiles) issue(t);
-    // tiles <= t landed, tiles t + 1 .. last_issued may stay in flight (4 DMAs per tile and wave)
-    auto wait_through = [&](int t, int last_issued) {
-        const int pending = min(ntiles - 1, last_issued) - t;
-        if (STUDY == 2 || pending <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if (pending == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else if (pending == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-    };
-    v16f_t sa, sb;
-    wait_through(0, P - 2);
-    if (STUDY != 1) qk(ring, sa);
-    auto iter = [&](int t, v16f_t& cur, v16f_t& nxt) {
-        // tile t + 1 landed (one more in flight); everyone is done with tile t - 1's slot
-        if (t + 1 < ntiles) wait_through(t + 1, t + P - 2);
-        else __builtin_amdgcn_s_barrier();
-        if (t + P - 1 < ntiles) issue(t + P - 1);
-        if (STUDY == 1) return;
-        if (t + 1 < ntiles && 32 * (t + 1) < lim_w) qk(ring + ((t + 1) % P) * kSlot, nxt);
-        if (32 * t < lim_w) softmax_pv(ring + (t % P) * kSlot, cur, 32 * t);
-    };
-    int t = 0;
-    for (; t + 1 < ntiles; t += 2) {
-        iter(t, sa, sb);
-        iter(t + 1, sb, sa);
-    }
-    if (t < ntiles) iter(t, sa, sb);
-    const float inv = 1.0f / swap32_sum(l_run);
-    if (qrow < M) {
-        uint16_t* orow = out + (int64_t)qrow * o_rs + (int64_t)(hq0 + (c & 3)) * D;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-            for (int u = 0; u < 4; ++u)  // dims 32 mt + 8 u + 4 h .. + 3
-                *reinterpret_cast<uint2*>(orow + 32 * mt + 8 * u + 4 * h) =
-                    make_uint2(pk_bf16(oacc[mt][4 * u] * inv, oacc[mt][4 * u + 1] * inv),
-                               pk_bf16(oacc[mt][4 * u + 2] * inv, oacc[mt][4 * u + 3] * inv));
-    }
-}
-
 // Prefill attention with the reference's SDPA arithmetic (k_attn_sdpa's comment): the decode loop
 // the reference runs for a prompt computes each position's attention over keys [0, pos] in 512-key
-// blocks with a running max. Same block / wave / lane layout, LDS-DMA ring and XCD-chunked order as
-// k_attn_prefill_fa, but per 512-key block two passes over its tiles:
-//   pass 1 (ring stages of TWO tiles' K): S^T = K . Q^T (two 64-dim partial MFMA chains summed in f64
-//     and rounded once), the column's block maximum (causal limit per column);
+// blocks with a running max (layout above; XCD-chunked block order), per 512-key block in two passes
+// over its tiles:
+//   pass 1 (ring stages of TWO tiles' K): S^T = K . Q^T (two 64-dim MFMA chains), the column's block
+//     maximum (causal limit per column);
 //   then M_c = max(M_{c-1}, block max), r = expf(M_{c-1} - M_c) rescales the column's O^T and l;
 //   pass 2 (stages of one tile's K + V): the same S^T again, e = fexp_u20 / expf of (s - M_c) (the
 //     16-key vector part / the tail of the column's block), l += e, O^T += V^T . bf16(e)^T (one MFMA
@@ -2215,7 +1495,7 @@ int prefill_attention_check(int Hq, int Hkv, int pps) {
     return WF_OK;
 }
 
-// bf16 K/V: the flash-style 32 x 32 matrix-core kernel k_attn_prefill_fa, its blocks in XCD-chunked
+// bf16 K/V: the 32 x 32 matrix-core kernel k_attn_prefill_sdpa, its blocks in XCD-chunked
 // order when the items split evenly over the 8 XCDs (each XCD streams one (slot, kv head) K/V at a
 // time from its own L2: 333 -> 250 us per layer at 8 x 2048); FP8 K/V, or a bf16 cache longer than
 // kPfMaxTiles tiles: the row-split register kernel k_attn_prefill ("Causal attention").
@@ -2246,7 +1526,7 @@ int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const 
 int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
                               float2* ml, float* o, hipStream_t st, bool kv_tiled, const int32_t* pt, int pps,
-                              int npages, int64_t kv_pgs, int kv8, float k_scale, float v_scale, const AttnTail* tail,
+                              int npages, int64_t kv_pgs, int kv8, float k_scale, float v_scale,
                               uint16_t* merged_row, unsigned* merge_cnt, uint64_t* xmax, const int32_t* order) {
     const int grp = Hq / Hkv;
     if (grp > 8) {
@@ -2257,7 +1537,7 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
         // the reference's SDPA semantics (k_attn_sdpa): one block per (split, query head, sequence),
         // the head's records merged into the bf16 row merged_row in the launch
         if (!merged_row || !merge_cnt || !xmax || pt) {
-            set_error("decode_attention_partials: batch < 16 / untiled caches need the merged-row buffers, no page table");
+            set_error("decode_attention_partials: batch < 16 / untiled caches need the merged-row, arrival and exchange buffers, no page table");
             return WF_EINVAL;
         }
         if (S > kSdpaMaxSeq) {
@@ -2302,7 +1582,6 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
                   kAttnMfmaMaxGrp);
         return WF_EINVAL;
     }
-    (void)tail;
     const dim3 grid(Hkv, B);
     const bool g4 = Hq == 4 * Hkv;
     const float ss = kv8 ? sm_scale * k_scale : sm_scale, vs = kv8 ? v_scale : 1.0f;

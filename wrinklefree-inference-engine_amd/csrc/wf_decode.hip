@@ -37,17 +37,16 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
                               int64_t kv_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, float sm_scale,
                               float2* ml, float* o, hipStream_t st, bool kv_tiled, const int32_t* pt = nullptr,
                               int pps = 0, int npages = 0, int64_t kv_pgs = 0, int kv8 = 0, float k_scale = 1.f,
-                              float v_scale = 1.f, const AttnTail* tail = nullptr, uint16_t* merged_row = nullptr,
+                              float v_scale = 1.f, uint16_t* merged_row = nullptr,
                               unsigned* merge_cnt = nullptr, uint64_t* xmax = nullptr,
                               const int32_t* order = nullptr);
 int seq_order(const int32_t* seq_lens, int B, int S, int32_t* order, hipStream_t st);
 
 // study switches (same-box A/B builds, tools/build_var.sh; measured r04, profiles/ab_r04.txt):
 // WF_NO_XTOK restores the batch-1 embed launch (-0.5 %); WF_OLD_EPI the LDS-round O/DN epilogue
-// (+-0.1 %); WF_ATTN_TAIL has the batched attention form the O input row in its per-sequence tail
-// (batch 128 -2.2 %: attention +7.5 us, k_rownorm_attn -4.5 us per layer); WF_NO_MERGE1 has the O
-// projection merge the batch < 16 attention records itself instead of reading the bf16 row each
-// head's last attention block merges (-1.7 % batch 1: O 4.35 -> 6.01 us, attention 5.86 -> 4.55 us)
+// (+-0.1 %). Measured and removed with the round-4 attention kernels: the batched attention forming
+// the O input row in its per-sequence tail (batch 128 -2.2 %: attention +7.5 us, k_rownorm_attn
+// -4.5 us per layer).
 #ifdef WF_NO_XTOK
 constexpr bool kXTok = false;
 #else
@@ -57,16 +56,6 @@ constexpr bool kXTok = true;
 constexpr bool kPermEpi = false;
 #else
 constexpr bool kPermEpi = true;
-#endif
-#ifdef WF_ATTN_TAIL
-constexpr bool kAttnTail = true;
-#else
-constexpr bool kAttnTail = false;
-#endif
-#ifdef WF_NO_MERGE1
-constexpr bool kMerge1 = false;
-#else
-constexpr bool kMerge1 = true;
 #endif
 
 enum { MODE_QKV = 0, MODE_O = 1, MODE_GU = 2, MODE_DN = 3, MODE_LINEAR = 4 };  // LINEAR: BitNetLinear drop-in
@@ -78,9 +67,6 @@ struct GemvArgs {
     int64_t x_stride;
     const uint16_t* nw;
     float eps;
-    // MODE_O: the attention row comes from the decode-attention partials (wf_norm.h AttnRow)
-    const float2* part_ml;
-    const float* part_o;
     // or int8 codes from k_rownorm (PPT == 0)
     const int8_t* q8;          // [B, q8_stride]
     int64_t q8_stride;
@@ -202,15 +188,10 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
     // 1) the input row (issued first: vmcnt retires in order), 2) the weight stream, 3) residual
     constexpr int kNormPPT = PPT == 0 ? 1 : PPT;
     NormRow<kNormPPT, kNT> nr;
-    constexpr bool kAttnIn = (MODE == MODE_O && PPT > 0 && !kMerge1);
-    AttnRow<kAttnIn ? PPT : 1, kNT, kAttnPartSplits1> ar;  // batch < 16: the k_attn_part records
     constexpr int kMaxPiecesPerThread = 8192 / 16 / kNT;  // staged int8: K_pad <= 8192
     uint4 apre[MB][kMaxPiecesPerThread];
     const int pieces16 = F::k_pad(K) / 16;
-    if constexpr (kAttnIn) {
-        ar.issue(a.part_ml, a.part_o, b0, a.Hq, 128);
-        nr.issue_w(a.nw, K);
-    } else if constexpr (PPT > 0 && MODE == MODE_LINEAR) {
+    if constexpr (PPT > 0 && MODE == MODE_LINEAR) {
         nr.issue_x(a.x + (int64_t)b0 * a.x_stride, K);
     } else if constexpr (PPT > 0) {
         const int xrow = (MODE == MODE_QKV && a.x_tok) ? min(max(a.x_tok[b0], 0), a.vocab - 1) : b0;  // scalar load
@@ -253,10 +234,7 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
     }
     // every load above is in flight before any input-stage arithmetic (hipcc would otherwise hoist
     // that math above the weight stream to save registers)
-    if constexpr (kAttnIn) {
-        ar.fence();
-        nr.fence(false);
-    } else if constexpr (PPT > 0) {
+    if constexpr (PPT > 0) {
         nr.fence(true, MODE != MODE_LINEAR);
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -264,10 +242,7 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
     int asum[MB];
     if constexpr (PPT > 0) {
         float y[PPT][8];
-        if constexpr (kAttnIn) {
-            ar.finish(a.Hq, 128, y);
-            sf[0] = norm_core<kNormPPT, kNT, 512u * MODE>(nr, K, a.eps, y, red);
-        } else if constexpr (MODE == MODE_LINEAR) {  // quantize x itself (no norm)
+        if constexpr (MODE == MODE_LINEAR) {  // quantize x itself (no norm)
             unpack_row(nr, K, y);
             sf[0] = absmax_scale<PPT, kNT>(y, red);
         } else {
@@ -755,8 +730,7 @@ __global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm(GemvArgs a) {
 // before the norm, so the weight stream overlaps it. The last block of the tile to pass the wait
 // re-arms both words (arrivals / passes), so the words are zero at every launch boundary. Needs the
 // whole grid co-resident (host: wf_model_create checks the occupancy, else the two-launch form) and
-// gridDim.x >= 32. PRO 1: rms_norm of x (a.x, a.nw); PRO 2: the attention row merged from the
-// decode-attention records (a.part_ml / a.part_o, kAttnPartSplits per head), then rms_norm.
+// gridDim.x >= 32. PRO 1: rms_norm of x (a.x, a.nw; for O, x = the attention's bf16 rows).
 constexpr unsigned kSeamSpin = 1u << 22;  // polls before a waiting block gives up (never in a valid launch)
 // codes of the NT-thread pieces into the tile layout, write-through (the in-launch hand-off)
 template <int PPT, int NT>
@@ -787,16 +761,8 @@ __device__ __forceinline__ void dec_row_prologue(const GemvArgs& a, int r, float
     if constexpr (NT == 512) {
         NormRow<PP, 512> nr;
         float y[PP][8];
-        if constexpr (PRO == 2) {
-            AttnRow<PP, 512, kAttnPartSplits> ar;
-            ar.issue(a.part_ml, a.part_o, r, a.Hq, 128);
-            nr.issue_w(a.nw, K);
-            ar.finish(a.Hq, 128, y);
-            sf = norm_core(nr, K, a.eps, y, red);
-        } else {
-            nr.issue(a.x + (int64_t)r * a.x_stride, a.nw, K);
-            sf = norm_row(nr, K, a.eps, y, red);
-        }
+        nr.issue(a.x + (int64_t)r * a.x_stride, a.nw, K);
+        sf = norm_row(nr, K, a.eps, y, red);
         as = quant_row_tiled_wt<PP, 512>(y, sf, K / 8, q8, r, nkb);
     } else {
         static_assert(NT == 256 && PRO == 1, "4-wave blocks: rms_norm of x only");
@@ -1793,39 +1759,6 @@ __global__ __launch_bounds__(512, NP <= 14 ? 4 : 1) void k_rownorm_tile8(const u
     }
 }
 
-// Batch > 1 O-projection input: attention row from the partials -> rms_norm -> int8 codes.
-template <int PPT, bool TL = false, int NS = kAttnPartSplits>
-__global__ __launch_bounds__(kNT) void k_rownorm_attn(const float2* __restrict__ ml, const float* __restrict__ o, int Hq,
-                                                      const uint16_t* __restrict__ nw, float eps, int8_t* __restrict__ q8,
-                                                      int64_t q8s, float* __restrict__ sf, int* __restrict__ asum) {
-    __shared__ float red[2 * kNT / 64];
-    __shared__ int red_i[kNT / 64];
-    const int b = blockIdx.x, K = Hq * 128;
-    WF_STAMP_BASE(2560u);
-    WF_STAMP(0);
-    AttnRow<PPT, kNT, NS> ar;
-    ar.issue(ml, o, b, Hq, 128);
-    NormRow<PPT, kNT> nr;
-    nr.issue_w(nw, K);
-    float y[PPT][8];
-    ar.finish(Hq, 128, y);
-    const float s = norm_core(nr, K, eps, y, red);
-    WF_STAMP(1);
-    int as;
-    if constexpr (TL) as = quant_row_tiled<PPT, kNT>(y, s, K / 8, q8, b, K >> 7);
-    else as = quant_row<PPT, kNT>(y, s, K / 8, q8 + (int64_t)b * q8s, [](int p) { return 8 * p; });
-    as = wave_sum_i(as);
-    if ((threadIdx.x & 63) == 0) red_i[threadIdx.x >> 6] = as;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int t = 0;
-        for (int i = 0; i < kNT / 64; ++i) t += red_i[i];
-        asum[b] = t;
-        sf[b] = s;
-    }
-    WF_STAMP(2);
-}
-
 #ifndef WF_LM_U  // study builds only (tools/build_variant.sh): 16-byte chunks in flight per lane
 #define WF_LM_U 4
 #endif
@@ -2373,7 +2306,7 @@ void fused_norm_plan(wf_model* m) {
         const void* fn = nullptr;
         switch (op) {
             case 0: fn = dec_gemm_kernel_pro<MODE_QKV>(1, K, N, &threads); break;
-            case 1: fn = dec_gemm_kernel_pro<MODE_O>(2, K, N, &threads); break;
+            case 1: fn = dec_gemm_kernel_pro<MODE_O>(1, K, N, &threads); break;
             case 2: fn = dec_gemm_kernel_pro<MODE_GU>(1, K, N, &threads); break;
             default: fn = dec_gemm_kernel_pro<MODE_DN>(1, K, N, &threads); break;
         }
@@ -2453,13 +2386,9 @@ int gemv_input(wf_model* m, GemvArgs& a, const uint16_t* x, int64_t xs, const ui
 
 // the batched attention forms the O input row in its tail (k_attn_mfma TAIL; its 256-thread norm
 // replays the 512-thread tree for rows of up to 4096)
-bool attn_tail_on(const wf_model* m) {
-    return kAttnTail && m->d.batch >= 16 && m->kv_tiled && m->attn_cnt && m->d.n_heads * m->d.head_dim <= 4096 && !m->fuse[1];
-}
 
 // the attention merges each head's records into the bf16 row m->attn_row (k_attn_sdpa: batch < 16 and
 // untiled caches); the O input then reads that row
-bool attn_merged(const wf_model* m) { (void)m; return true; }
 // the attention also leaves per-split (m, l, o) records (k_attn_sdpa; include/wf_bitnet.h attn view)
 bool attn_records(const wf_model* m) { return m->d.batch < 16 || !m->kv_tiled; }
 
@@ -2487,51 +2416,31 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
             return launch_gemv_fmt<MODE_QKV, kLprQKV>(d.wfmt, a, st);
         case WF_OP_ATTN: {  // split partials; merged by the O projection's input stage or the tail
             if (m->kv_tiled && B >= 16 && l == 0 && (rc = seq_order(m->seq_lens, B, S, m->attn_order, st))) return rc;
-            // batch >= 16 on tile-layout caches: the attention's last block per sequence forms the O
-            // input row (AttnTail) instead of a k_rownorm_attn launch
-            AttnTail tail{d.attn_sub + (int64_t)l * H, d.eps, m->q8, m->act_sf, m->act_sum, m->attn_cnt};
-            const AttnTail* tp = attn_tail_on(m) ? &tail : nullptr;
-            uint16_t* mrow = attn_merged(m) ? m->attn_row : nullptr;
-            unsigned* mcnt = mrow ? m->attn_cnt : nullptr;
+            uint16_t* mrow = m->attn_row;
+            unsigned* mcnt = m->attn_cnt;  // k_attn_sdpa's arrival counts
             if (a.pt)  // paged pool: kv head stride 32 * D inside a page
                 return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, 0, 32 * D, B, d.n_heads,
                                                  d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D), m->part_ml,
                                                  m->part_o, st, true, a.pt, a.pps, a.npages, a.kv_pgs, d.kv_quant,
-                                                 m->kv_scale[2 * l], m->kv_scale[2 * l + 1], tp, mrow, mcnt, m->attn_xmax,
+                                                 m->kv_scale[2 * l], m->kv_scale[2 * l + 1], mrow, mcnt, m->attn_xmax,
                                                  m->attn_order);
             return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, a.kv_b_stride, (int64_t)S * D,
                                              B, d.n_heads, d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D),
                                              m->part_ml, m->part_o, st, m->kv_tiled != 0, nullptr, 0, 0, 0, d.kv_quant,
                                              d.kv_quant ? m->kv_scale[2 * l] : 1.f, d.kv_quant ? m->kv_scale[2 * l + 1] : 1.f,
-                                             tp, mrow, mcnt, m->attn_xmax, m->attn_order);
+                                             mrow, mcnt, m->attn_xmax, m->attn_order);
         }
         case WF_OP_O:  // h_b = h_a + o_proj(rms_norm(attn_sub_norm)(attn))
             a.w = d.w_o + (int64_t)l * H * wrow_bytes(d.wfmt, H); a.N = H; a.K = H; a.ws0 = wsh[3];
             a.resid = m->h_a; a.out = m->h_b; a.out_stride = H;
             if (kXTok && B == 1 && l == 0) { a.resid = d.embed; a.x_tok = m->tokens; a.vocab = d.vocab; }
-            if (attn_merged(m)) { a.x = m->attn_row; a.x_stride = H; }
+            a.x = m->attn_row;  // every attention path writes its bf16 output rows
+            a.x_stride = H;
             a.nw = d.attn_sub + (int64_t)l * H;
-            a.part_ml = m->part_ml;
-            a.part_o = m->part_o;
-            if (m->fuse[1]) return launch_gemv_fmt<MODE_O, kLprO>(d.wfmt, a, st, 2);
-            if (B > 1 && attn_merged(m)) {  // the merged bf16 rows: the plain row norm
+            if (m->fuse[1]) return launch_gemv_fmt<MODE_O, kLprO>(d.wfmt, a, st, 1);  // x = the attention rows
+            if (B > 1) {  // the attention's bf16 rows: the plain row norm
                 launch_rownorm(m, m->attn_row, H, a.nw, H, nullptr, st);
                 if ((rc = check_launch("rownorm_attn_row"))) return rc;
-            } else if (B > 1 && !attn_tail_on(m)) {
-// the records of decode_attention_partials: kAttnPartSplits1 per head below batch 16, else kAttnPartSplits
-#define WF_RA(PPTV, TL, NS)                                                                                                 \
-    hipLaunchKernelGGL((k_rownorm_attn<PPTV, TL, NS>), dim3(B), dim3(kNT), 0, st, m->part_ml, m->part_o, d.n_heads, a.nw, \
-                       d.eps, m->q8, m->q8_stride, m->act_sf, m->act_sum)
-                const bool tl = d.wfmt == WF_FMT_I2S_MFMA, few = B < 16;
-                if (norm_ppt(H) == 1) {
-                    if (tl) { if (few) WF_RA(1, true, kAttnPartSplits1); else WF_RA(1, true, kAttnPartSplits); }
-                    else { if (few) WF_RA(1, false, kAttnPartSplits1); else WF_RA(1, false, kAttnPartSplits); }
-                } else {
-                    if (tl) { if (few) WF_RA(2, true, kAttnPartSplits1); else WF_RA(2, true, kAttnPartSplits); }
-                    else { if (few) WF_RA(2, false, kAttnPartSplits1); else WF_RA(2, false, kAttnPartSplits); }
-                }
-#undef WF_RA
-                if ((rc = check_launch("rownorm_attn"))) return rc;
             }
             return launch_gemv_fmt<MODE_O, kLprO>(d.wfmt, a, st);
         case WF_OP_GATE_UP:  // act = relu(gate)^2 * up of rms_norm(post_attention_layernorm)(h_b)
@@ -2754,7 +2663,7 @@ int wf_model_attn_view(const wf_model* m, wf_attn_records* out) {
     out->part_ml = reinterpret_cast<const float*>(m->part_ml);
     out->part_o = m->part_o;
     out->records = attn_records(m) ? kAttnPartSplits1 : 0;
-    out->attn_row = attn_merged(m) ? m->attn_row : nullptr;
+    out->attn_row = m->attn_row;
     return WF_OK;
 }
 

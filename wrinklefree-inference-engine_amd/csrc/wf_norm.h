@@ -167,7 +167,7 @@ struct NormRow {
 #pragma unroll
         for (int i = 0; i < PPT; ++i) x[i] = *reinterpret_cast<const uint4*>(xrow + 8 * min((int)threadIdx.x + NT * i, npk - 1));
     }
-    // norm weight only (the row itself is computed in registers, e.g. AttnRow)
+    // norm weight only (the row itself is computed in registers)
     __device__ __forceinline__ void issue_w(const uint16_t* __restrict__ nw, int K) {
         const int npk = K >> 3;
 #pragma unroll
@@ -276,7 +276,7 @@ __device__ __forceinline__ float norm_row(const NormRow<PPT, NT>& r, int K, floa
 }
 
 // 256 threads replaying the 512-thread norm_core (the batch-1 / k_rownorm reduction tree, so the
-// codes are bit-identical): thread t holds pieces t + 256 i (NormRow<PPT2, 256> / AttnRow<PPT2, 256>).
+// codes are bit-identical): thread t holds pieces t + 256 i (NormRow<PPT2, 256>).
 template <int PPT2>
 __device__ __forceinline__ float norm_core_e512(const NormRow<PPT2, 256>& r, int K, float eps, float (&y)[PPT2][8],
                                                 float* red) {
@@ -388,11 +388,9 @@ static_assert(kAttnPartSplits <= kAttnPartSplitsMax && kAttnPartSplits1 <= kAttn
               "part_ml / part_o are sized for kAttnPartSplitsMax records per (sequence, head)");
 static_assert(kAttnPartSplits % 4 == 0 && kAttnPartSplits1 % 2 == 0, "record counts: whole 4-wave blocks / pairs");
 // Float offset of element d of split s's unnormalised o in the decode-attention partials of (b, h)
-// (bh = b * Hq + h; head_dim 128): [bh][split][half = (d >> 2) & 1][d >> 3][4]. The merging reader
-// (AttnRow) gives each thread the 8-wide piece d0 = 8 t of every split and loads it as two halves:
-// for one (split, half) the threads of a wave read consecutive 16-byte slots -- one contiguous KiB
-// per wave-instruction (the plain [bh][split][d] order left every other 16-byte slot of each line
-// to the next instruction). (m, l) records stay [bh][split].
+// (bh = b * Hq + h; head_dim 128): [bh][split][half = (d >> 2) & 1][d >> 3][4] (include/wf_bitnet.h
+// wf_attn_records; k_attn_sdpa's writers and merging block address 4-float slots of it). (m, l)
+// records stay [bh][split].
 template <int NS = kAttnPartSplits>
 __device__ __forceinline__ int64_t part_o_off(int64_t bh, int s, int d) {
     return ((bh * NS + s) * 2 + ((d >> 2) & 1)) * 64 + (d >> 3) * 4 + (d & 3);
@@ -415,101 +413,7 @@ __device__ __forceinline__ int64_t v_tile_off(int t, int d) {
     return ((((int64_t)blk * 8 + (d >> 4)) * 4 + (o >> 3)) * 16 + (d & 15)) * 8 + (o & 7);
 }
 
-// piece index of a thread's i-th piece: the NT-thread mapping p = threadIdx.x + NT * i
-template <int NT>
-struct PieceNT {
-    __device__ __forceinline__ int operator()(int i) const { return (int)threadIdx.x + NT * i; }
-};
-template <int PPT, int NT, int NS = kAttnPartSplits, class PC = PieceNT<NT>>
-struct AttnRow {
-    float4 ml[PPT][NS / 2];  // (m0, l0, m1, l1) pairs
-    float4 oa[PPT][NS], ob[PPT][NS];
-    // SC1: the records were published in this launch (the attention's tail hand-off, write-through
-    // stores + ticket): L1-bypassing 16-byte buffer loads (MI355X_MICROARCH.md Valid forms row 1)
-    template <bool SC1 = false>
-    __device__ __forceinline__ void issue(const float2* __restrict__ ml_in, const float* __restrict__ o_in, int b, int Hq,
-                                          int D) {
-        const int npk = Hq * D / 8;
-        const PC piece;
-        const __amdgpu_buffer_rsrc_t rml = make_rsrc(ml_in), ro = make_rsrc(o_in);
-#pragma unroll
-        for (int i = 0; i < PPT; ++i) {
-            const int pc = min(piece(i), npk - 1);
-            const int h = (8 * pc) / D, d0 = 8 * pc - h * D;
-            const int64_t rec = (int64_t)(b * Hq + h) * NS;
-#pragma unroll
-            for (int u = 0; u < NS / 2; ++u) {
-                if constexpr (SC1) ml[i][u] = __builtin_bit_cast(float4, ld16_sc1(rml, (int)(8 * rec + 16 * u)));
-                else ml[i][u] = reinterpret_cast<const float4*>(ml_in + rec)[u];
-            }
-#pragma unroll
-            for (int u = 0; u < NS; ++u) {
-                const int64_t ea = part_o_off<NS>(b * Hq + h, u, d0), eb = part_o_off<NS>(b * Hq + h, u, d0 + 4);
-                if constexpr (SC1) {
-                    oa[i][u] = __builtin_bit_cast(float4, ld16_sc1(ro, (int)(4 * ea)));
-                    ob[i][u] = __builtin_bit_cast(float4, ld16_sc1(ro, (int)(4 * eb)));
-                } else {
-                    oa[i][u] = *reinterpret_cast<const float4*>(o_in + ea);
-                    ob[i][u] = *reinterpret_cast<const float4*>(o_in + eb);
-                }
-            }
-        }
-    }
-    __device__ __forceinline__ void fence() {
-#pragma unroll
-        for (int i = 0; i < PPT; ++i) {
-#pragma unroll
-            for (int u = 0; u < NS / 2; ++u) reg_fence(ml[i][u]);
-#pragma unroll
-            for (int u = 0; u < NS; ++u) {
-                reg_fence(oa[i][u]);
-                reg_fence(ob[i][u]);
-            }
-        }
-    }
-    __device__ __forceinline__ void finish(int Hq, int D, float (&y)[PPT][8]) const {
-        const int npk = Hq * D / 8;
-        const PC piece;
-#pragma unroll
-        for (int i = 0; i < PPT; ++i) {
-            float mm[NS], ll[NS];
-#pragma unroll
-            for (int u = 0; u < NS / 2; ++u) {
-                mm[2 * u] = ml[i][u].x; ll[2 * u] = ml[i][u].y;
-                mm[2 * u + 1] = ml[i][u].z; ll[2 * u + 1] = ml[i][u].w;
-            }
-            float M = mm[0];
-#pragma unroll
-            for (int u = 1; u < NS; ++u) M = fmaxf(M, mm[u]);
-            float L = 0.f, O[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int u = 0; u < NS; ++u) {
-                const float w = (mm[u] == -INFINITY) ? 0.f : __expf(mm[u] - M);
-                L = fmaf(w, ll[u], L);
-                const float ov[8] = {oa[i][u].x, oa[i][u].y, oa[i][u].z, oa[i][u].w,
-                                     ob[i][u].x, ob[i][u].y, ob[i][u].z, ob[i][u].w};
-#pragma unroll
-                for (int j = 0; j < 8; ++j) O[j] = fmaf(w, ov[j], O[j]);
-            }
-            const float inv = 1.0f / L;
-            const bool valid = piece(i) < npk;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) y[i][j] = valid ? rbf(O[j] * inv) : 0.f;
-        }
-    }
-};
-
-// The batched decode attention's tail (k_attn_mfma TAIL): the last of a sequence's blocks to finish
-// merges its Hq heads' records into the O projection's input row -- attn_sub_norm rms_norm + int8
-// codes in the tile layout, scale and code sum -- in place of a k_rownorm_attn launch.
-struct AttnTail {
-    const uint16_t* nw;  // attn_sub_norm weight of the layer [Hq * 128]
-    float eps;
-    int8_t* q8;          // codes, tile layout (tile_code_pos)
-    float* sf;           // [B]
-    int* asum;           // [B]
-    unsigned* cnt;       // one arrival counter per sequence, kTailLine words apart, zero between launches
-};
+// one 128-byte line per arrival counter (memory-side atomics and polls on one line serialise)
 constexpr int kTailLine = 32;  // one 128-byte line per counter
 
 // Batch-1 GEMV prologue (k_gemv PPT > 0: NormRow + norm_core + quant_row) is VALU-issue /

@@ -513,9 +513,9 @@ class BitNetDecoder:
         return q, ml, o
 
     def attention_row(self):
-        """The merged bf16 attention output the O projection reads after WF_OP_ATTN ([B, Hq, D]), on
-        the paths whose attention merges its records in the launch (batch < 16, untiled caches:
-        include/wf_bitnet.h wf_attn_records.attn_row); None on the batched tile-layout path."""
+        """The bf16 attention output the O projection reads after WF_OP_ATTN ([B, Hq, D];
+        include/wf_bitnet.h wf_attn_records.attn_row): every attention path writes it (batch < 16 /
+        untiled caches: the head's merging block; batch >= 16 tile layout: the batched kernel)."""
         v = _lib.WFAttnView()
         call("wf_model_attn_view", self._h, C.addressof(v))
         if not v.attn_row:
