@@ -377,6 +377,11 @@ __device__ __forceinline__ uint4 kv_ld16(const uint16_t* p) {
 #ifndef WF_SDPA_WPE
 #define WF_SDPA_WPE
 #endif
+// (measured, not kept: all splits of a head on one XCD with L2 polls -- the dispatcher does deal
+// block b to XCD b % 8 (tools/ubench/xcd_map.hip), but no load without sc1 ever saw a granule another
+// CU stored, whatever the store's policy bits, and an sc1 hand-off takes 0.6 us on one XCD and across
+// two alike (tools/ubench/handoff.hip): the exchange's ~2.2 us is the siblings' QK skew (~0.9 us)
+// plus that hand-off, not the distance)
 constexpr int kSdpaMaxT = 1024;      // split length bound (max_seq <= 8192): a split spans <= 3 blocks
 constexpr int kSdpaMaxSeq = kAttnPartSplits1 * kSdpaMaxT;
 
@@ -512,10 +517,10 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
                                                int Hkv, int S, const int32_t* __restrict__ seq_lens, float sm_scale,
                                                int b0, uint64_t* __restrict__ xg, float2* __restrict__ ml_out,
                                                float* __restrict__ o_out, uint16_t* __restrict__ row_out,
-                                               unsigned* __restrict__ cnt, unsigned* __restrict__ xep) {
+                                               unsigned* __restrict__ cnt, unsigned* __restrict__ xep, int s, int hq) {
     constexpr int NS = kAttnPartSplits1, D = 128, LP = 16, NG = kAttnPartThreads / LP, CH = U * NG;
     constexpr int NWV = kAttnPartThreads / 64;
-    const int s = blockIdx.x, hq = blockIdx.y, b = b0 + (int)blockIdx.z;
+    const int b = b0 + (int)blockIdx.z;
     const int g = hq / (Hq / Hkv);
     const int gid = threadIdx.x / LP, li = threadIdx.x % LP, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int Sb = min(seq_lens[b], S);
@@ -586,9 +591,7 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
         uint64_t gv = ((uint64_t)ep << 32) | 0xff800000u;  // lanes past the granules: -inf, tagged
         int ok = 1;
         for (int it = 0;; ++it) {
-#ifndef WF_SDPA_NOPOLL
             if (lane < 3 * NS) gv = ld_sc1(xg + bh * NS * 3 + lane);
-#endif
             if (__all((unsigned)(gv >> 32) == ep)) break;
             if (it > (1 << 20)) { ok = 0; break; }  // a missing sibling ends in NaN outputs, never a hang
             __builtin_amdgcn_s_sleep(WF_SDPA_SLEEP);
@@ -720,14 +723,15 @@ __global__ __launch_bounds__(kAttnPartThreads) WF_SDPA_WPE void k_attn_sdpa(cons
                                                                 uint16_t* __restrict__ row_out, unsigned* __restrict__ cnt,
                                                                 unsigned* __restrict__ xep) {
     constexpr int NS = kAttnPartSplits1, NG = kAttnPartThreads / 16;
+    const int s = blockIdx.x, hq = blockIdx.y;
     const int Sb = min(seq_lens[b0 + (int)blockIdx.z], S);
     const int T = ((Sb + NS - 1) / NS + 15) / 16 * 16;
     if (T <= kApUShort * NG)  // block-uniform: one load round holds the split
         attn_sdpa_body<kApUShort, true>(q, q_sb, K, V, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, b0, xg, ml_out,
-                                        o_out, row_out, cnt, xep);
+                                        o_out, row_out, cnt, xep, s, hq);
     else
         attn_sdpa_body<kApULong, false>(q, q_sb, K, V, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, b0, xg, ml_out,
-                                        o_out, row_out, cnt, xep);
+                                        o_out, row_out, cnt, xep, s, hq);
 }
 
 // ---------------------------------------------------------------------------------------------
