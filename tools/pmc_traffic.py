@@ -29,8 +29,10 @@ def op_name(kernel: str):
     m = re.search(r"k_dec_gemm(?:_t)?<\d+, \d+, \d+, (\d)[,>]", kernel)
     if m:  # batched matrix-core GEMMs (last template argument = mode)
         return MODES[m.group(1)], "I2S_MFMA" if "k_dec_gemm_t" in kernel else "I2S"
-    if "k_attn_part" in kernel or "k_attn_mfma" in kernel:
+    if "k_attn_sdpa" in kernel or "k_attn_part" in kernel or "k_attn_mfma" in kernel:  # r05 / earlier rounds
         return "attn", None
+    if "k_seq_order" in kernel:
+        return "seq_order", None
     if "k_lm_head" in kernel:
         return "lm_head", None
     if "k_rownorm_attn" in kernel:

@@ -11,7 +11,10 @@ mkdir -p "$O"
 export TMPDIR=/tmp
 TAG=${TAG:-r01}
 step() { echo "== $1"; }
+PART=${PART:-all}
+on() { [ "$PART" = all ] || [ "$PART" = "$1" ]; }
 
+if on 1; then
 step pytest
 timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider -rf > "$O/pytest_gpu.log" 2>&1 || exit $?
 tail -2 "$O/pytest_gpu.log"
@@ -42,10 +45,12 @@ grep "K/V ctx" "$O/kv_quality.log"
 step bench-b1-tq
 timeout -k 10 600 python bench.py --steps 200 --warmup 10 --no-cpu-baseline --no-gemv --wfmt tq > "$O/bench_b1_tq.log" 2>&1 || exit $?
 tail -1 "$O/bench_b1_tq.log" | cut -c1-200
+fi
+if on 2; then
 for B in 1 128; do
     step "rocprof b$B"
     cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof_b$B" -o run -- \
-        python3 "$R/bench.py" --batch $B --steps 100 --warmup 10 --no-cpu-baseline --no-gemv > "$O/prof_b$B.log" 2>&1 || exit $?
+        python3 "$R/bench.py" --batch $B --steps 100 --warmup 10 --no-cpu-baseline --no-gemv --no-sub > "$O/prof_b$B.log" 2>&1 || exit $?
     cd "$R" && python3 tools/prof_summary.py "$O/prof_b$B" > "$O/kernel_stats_b$B.txt" 2>&1 || exit $?
     rm -rf "$O/prof_b$B"  # raw traces: gpurun_out/ must stay under 64 MiB
     OPS=rocprof_ops; [ $B -gt 1 ] && OPS=rocprof_ops_b$B
@@ -54,13 +59,15 @@ for B in 1 128; do
     for C in FETCH_SIZE WRITE_SIZE; do
         step "pmc $C b$B"
         cd /tmp && timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$O/pmc_${C}_b$B" -o run -- \
-            python3 "$R/bench.py" --batch $B --steps 20 --warmup 5 --no-cpu-baseline --no-op-timing --no-gemv > "$O/pmc_${C}_b$B.log" 2>&1 || exit $?
+            python3 "$R/bench.py" --batch $B --steps 20 --warmup 5 --no-cpu-baseline --no-op-timing --no-gemv --no-sub > "$O/pmc_${C}_b$B.log" 2>&1 || exit $?
         cd "$R"
     done
     STEM=pmc_traffic; [ $B -gt 1 ] && STEM=pmc_traffic_b$B
     python3 tools/pmc_traffic.py "$O/pmc_FETCH_SIZE_b$B" "$O/pmc_WRITE_SIZE_b$B" "$TAG" $STEM > /dev/null || exit $?
     cp profiles/$STEM.json "$O/" && rm -rf "$O/pmc_FETCH_SIZE_b$B" "$O/pmc_WRITE_SIZE_b$B"
 done
+fi
+if on 3; then
 step gemv
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_gemv" -o run -- python3 "$R/tools/gemv_bench.py" > "$O/prof_gemv.log" 2>&1 || exit $?
 cd "$R" && python3 tools/prof_summary.py "$O/prof_gemv" > "$O/kernel_stats_gemv.txt" 2>&1 || exit $?
@@ -87,4 +94,5 @@ cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_prefil
 cd "$R" && python3 tools/prof_summary.py "$O/prof_prefill_e2e" > "$O/kernel_stats_prefill_e2e.txt" 2>&1 || exit $?
 rm -rf "$O/prof_prefill_e2e"
 grep workload "$O/prefill_e2e.log"
+fi
 echo "== done"

@@ -1353,6 +1353,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
     };
     float m_run = -INFINITY, l_run = 0.f, bmax = -INFINITY;
     int vmin = 0;
+    const int lim_lo = (int)-wave_max((float)-lim_q);  // the wave's smallest causal limit
     v16f_t oacc[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
@@ -1387,10 +1388,15 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
                 if (32 * t >= lim_b) break;
                 float x[16];
                 qk(st + u * 8192, x);
-                const int lim = lim_q - 32 * t - 8 * h;
+                if (32 * t + 32 <= lim_lo) {  // below every column's limit (wave-uniform): no masks
 #pragma unroll
-                for (int j = 0; j < 16; ++j)
-                    if ((j & 7) + 16 * (j >> 3) < lim) bmax = fmaxf(bmax, x[j]);
+                    for (int j = 0; j < 16; ++j) bmax = fmaxf(bmax, x[j]);
+                } else {
+                    const int lim = lim_q - 32 * t - 8 * h;
+#pragma unroll
+                    for (int j = 0; j < 16; ++j)
+                        if ((j & 7) + 16 * (j >> 3) < lim) bmax = fmaxf(bmax, x[j]);
+                }
             }
         }
         {  // M_c, rescale O and l (the max of the raw dots, scaled once: rounding a product is monotone)
