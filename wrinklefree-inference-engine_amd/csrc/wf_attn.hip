@@ -1460,15 +1460,18 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
     #pragma unroll
                     for (int j = 0; j < w2; ++j) ee[j] += ee[j + w2];
                 l_run += ee[0];
-                const v8bf_t pb0 = __builtin_bit_cast(v8bf_t, make_uint4(pk[0], pk[1], pk[2], pk[3]));
-                const v8bf_t pb1 = __builtin_bit_cast(v8bf_t, make_uint4(pk[4], pk[5], pk[6], pk[7]));
+                uint4 pu0 = make_uint4(pk[0], pk[1], pk[2], pk[3]), pu1 = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+                reg_fence(pu0);  // packed once (hipcc otherwise re-packed P before every P.V MFMA)
+                reg_fence(pu1);
+                const v8bf_t pb0 = __builtin_bit_cast(v8bf_t, pu0), pb1 = __builtin_bit_cast(v8bf_t, pu1);
                 const int limv = lim_b - bs - 8 * h;  // V keys past the block's last position: zero (stale)
+                const bool vtail = lim_b - bs < 40;   // wave-uniform: some lane's V keys cross the block end
     #pragma unroll
                 for (int mt = 0; mt < 4; ++mt) {
     #pragma unroll
                     for (int s2 = 0; s2 < 2; ++s2) {
                         uint4 a = vv[mt][s2];
-                        if (limv < 32) {
+                        if (vtail) {
                             const int k0 = 16 * s2;
                             a.x &= (k0 < limv ? 0xffffu : 0u) | (k0 + 1 < limv ? 0xffff0000u : 0u);
                             a.y &= (k0 + 2 < limv ? 0xffffu : 0u) | (k0 + 3 < limv ? 0xffff0000u : 0u);
