@@ -1021,7 +1021,8 @@ __global__ __launch_bounds__(256, 3) void k_attn_sdpa_mfma(const uint16_t* __res
 __global__ __launch_bounds__(1024) void k_seq_order(const int32_t* __restrict__ seq_lens, int B, int S,
                                                     int32_t* __restrict__ order) {
     __shared__ uint32_t key[2048];
-    const int n = B <= 1024 ? 1024 : 2048;
+    int n = 2;  // the smallest power of two >= B: log2(n) (log2(n) + 1) / 2 barrier steps (28 at B = 128, not 55)
+    while (n < B) n <<= 1;
     for (int i = threadIdx.x; i < n; i += 1024) {
         const uint32_t len = i < B ? (uint32_t)min(max(seq_lens[i], 0), S) : 0u;
         // descending length = ascending (~len); pads (len 0, index >= B) sort last

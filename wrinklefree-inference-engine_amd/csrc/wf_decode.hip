@@ -786,6 +786,9 @@ __device__ __forceinline__ void dec_row_prologue(const GemvArgs& a, int r, float
     }
 }
 
+// (measured, not kept: a 1-D grid placing a column block's row blocks on one XCD so the weight
+// fragments they all decode come from one L2 -- batch 128 36.2k -> 35.5k tok/s, every GEMM 0.1-0.9 us
+// slower; the GEMMs are latency-bound, not HBM-bound)
 #ifndef WF_DG_WNT  // study: batched decode GEMM weight loads non-temporal, 1 for o / down, 2 for all
 #define WF_DG_WNT 0  // (all: gate|up 15.8 -> 17.1 us; o / down alone: no change; ab_kv_nt_r04.txt)
 #endif
