@@ -739,6 +739,10 @@ __global__ __launch_bounds__(kAttnPartThreads) WF_SDPA_WPE void k_attn_sdpa(cons
 // (k_attn_sdpa_mfma): K / V caches in their tile layouts (wf_norm.h k_tile_off / v_tile_off), every
 // fragment load one contiguous KiB per wave.
 // ---------------------------------------------------------------------------------------------
+#ifndef WF_ATTN_SPLIT2  // 0: one workgroup per (kv head, sequence) whatever the context
+#define WF_ATTN_SPLIT2 1
+#endif
+constexpr bool kAttnSplit2 = WF_ATTN_SPLIT2;
 typedef short v8s_t __attribute__((ext_vector_type(8)));
 typedef float v4f_t __attribute__((ext_vector_type(4)));
 constexpr int kAttnMfmaMaxGrp = 8;
@@ -834,7 +838,9 @@ __global__ __launch_bounds__(256, 3) void k_attn_sdpa_mfma(const uint16_t* __res
                                                           const int32_t* __restrict__ seq_lens, float sm_scale,
                                                           const int32_t* __restrict__ pt, int pps, int npages,
                                                           int64_t kv_pgs, float v_scale, uint16_t* __restrict__ row,
-                                                          const int32_t* __restrict__ order) {
+                                                          const int32_t* __restrict__ order, float2* __restrict__ rec_ml,
+                                                          float* __restrict__ rec_o, unsigned* __restrict__ cnt,
+                                                          unsigned* __restrict__ xep, uint64_t* __restrict__ xg) {
     constexpr int D = 128;
     using KF = KvFrag<KV8>;
     using FT = typename KF::T;
@@ -845,6 +851,23 @@ __global__ __launch_bounds__(256, 3) void k_attn_sdpa_mfma(const uint16_t* __res
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
     const int Sb = min(seq_lens[b], S);
     const int NB = (Sb + 511) >> 9;
+    // gridDim.z == 2: a sequence of two or more 512-key blocks takes two workgroups, block 0 and
+    // blocks 1 .. NB - 1 (5 kv heads x 128 sequences = 640 workgroups otherwise leave half the CUs 3
+    // and half 2). Workgroup 1 needs M_0, the max of block 0, before its first probabilities:
+    // workgroup 0 publishes it as epoch-tagged granules (k_attn_sdpa's exchange; all z = 0 workgroups
+    // precede z = 1 in dispatch order, so workgroup 0 never waits on workgroup 1). Both store records
+    // -- (M_0, l_0, o_0) and (R, l_1, o_1), R the product of workgroup 1's block rescale factors
+    // r_1 r_2 ... (the factor the CPU loop's running sums carry block 0 by) -- and the second to finish
+    // combines them: O = o_0 R + o_1, L = l_0 R + l_1.
+    const int sp = blockIdx.z;
+    const bool two = gridDim.z == 2 && NB >= 2;
+    if (sp == 1 && !two) return;  // whole workgroup
+    const int c0 = two ? sp : 0, c1 = two ? (sp ? NB : 1) : NB;
+    float Rp = 1.f;  // workgroup 1: product of its rescale factors
+    const int64_t gb = (int64_t)b * Hkv + g;
+    const unsigned ep = two ? ld_sc1(xep + gb * kTailLine) + 1u : 0u;  // this launch's tag
+    __shared__ float sm_m0[kAttnMfmaMaxGrp], sm_mh[kAttnMfmaMaxGrp];
+    __shared__ int sh_last;
     __shared__ float sm_mx[2][4][16];
     // the wave's scores of its 4 tiles of the block (LDS, not registers: three blocks per CU instead
     // of two); after the last block the same bytes hold the waves' output partials
@@ -889,8 +912,8 @@ __global__ __launch_bounds__(256, 3) void k_attn_sdpa_mfma(const uint16_t* __res
 #pragma unroll
     for (int n = 0; n < 8; ++n) acc[n] = v4f_t{0.f, 0.f, 0.f, 0.f};
     FT fa[8], fb[8];
-    if (NB > 0 && tbase(0, 0) < Sb) load(fa, 0, 0);
-    for (int c = 0; c < NB; ++c) {
+    if (c1 > c0 && tbase(c0, 0) < Sb) load(fa, c0, 0);
+    for (int c = c0; c < c1; ++c) {
         const int nb = min(512, Sb - 512 * c), vbnd = nb & ~15;
         float wmx = -INFINITY;
         float mblk = -INFINITY, r = 0.f;
@@ -899,18 +922,32 @@ __global__ __launch_bounds__(256, 3) void k_attn_sdpa_mfma(const uint16_t* __res
             // the next step's fragments first (one tile ahead), into the other buffer
             {
                 const int cn = s == 7 ? c + 1 : c, sn = (s + 1) & 7;
-                if (cn < NB && tbase(cn, sn) < Sb) {
+                if (cn < c1 && tbase(cn, sn) < Sb) {
                     if (s & 1) load(fa, cn, sn);
                     else load(fb, cn, sn);
                 }
             }
             if (s == 4) {  // the block's maxima: every wave's pass 1 is done
                 if (q4 == 0 && l16 < 16) sm_mx[c & 1][wave][l16] = wmx;
+                if (two && sp == 1 && wave == 0 && lane < grp) {  // M_0 of head `lane` from workgroup 0
+                    const uint64_t* gp = xg + gb * kAttnMfmaMaxGrp + lane;
+                    uint64_t gv = ld_sc1(gp);
+                    for (int it = 0; (unsigned)(gv >> 32) != ep; ++it) {
+                        if (it > (1 << 20)) { gv = 0x7fc00000u; break; }  // never in a valid launch: NaN, not a hang
+                        __builtin_amdgcn_s_sleep(1);
+                        gv = ld_sc1(gp);
+                    }
+                    sm_m0[lane] = __uint_as_float((uint32_t)gv);
+                }
                 __syncthreads();
+                if (two && sp == 1) m_run = sm_m0[l16 % grp];  // block 1 continues from block 0's max
                 mblk = fmaxf(fmaxf(sm_mx[c & 1][0][l16], sm_mx[c & 1][1][l16]), fmaxf(sm_mx[c & 1][2][l16], sm_mx[c & 1][3][l16]));
                 const float mn = fmaxf(m_run, mblk);
                 r = (c == 0) ? 0.f : expf_rn(m_run - mn);
+                Rp *= (c == 0) ? 1.f : r;
                 m_run = mn;
+                if (two && sp == 0 && wave == 0 && q4 == 0 && l16 < grp)
+                    st_sc1(xg + gb * kAttnMfmaMaxGrp + l16, ((uint64_t)ep << 32) | __float_as_uint(mn));
                 l_run *= r;
                 if (c > 0) {
                     float ar[4];  // rescale of output row (head) 4 q4 + rr
@@ -990,6 +1027,7 @@ __global__ __launch_bounds__(256, 3) void k_attn_sdpa_mfma(const uint16_t* __res
     l_run += __shfl_xor(l_run, 16, 64);
     l_run += __shfl_xor(l_run, 32, 64);
     if (q4 == 0 && l16 < grp) sm_l[wave][l16] = l_run;
+    if (wave == 0 && q4 == 0 && l16 < grp) sm_mh[l16] = sp ? Rp : m_run;  // record field 0: M_0 / R
 #pragma unroll
     for (int n = 0; n < 8; ++n)
 #pragma unroll
@@ -1005,7 +1043,50 @@ __global__ __launch_bounds__(256, 3) void k_attn_sdpa_mfma(const uint16_t* __res
             const float4 ov = *reinterpret_cast<const float4*>(&sm_u.o[w][h][d]);
             os[0] += ov.x; os[1] += ov.y; os[2] += ov.z; os[3] += ov.w;
         }
+        if (two) {  // this block's record (frame M_sp), write-through for the combining workgroup
+            const int64_t rec = (gb * 2 + sp) * grp + h;
+            st16_sc1(make_rsrc(rec_o), (int)(4 * (rec * D + d)), __builtin_bit_cast(uint4, make_float4(os[0], os[1], os[2], os[3])));
+            if (d == 0) st_sc1(reinterpret_cast<uint64_t*>(rec_ml) + rec, __builtin_bit_cast(uint64_t, make_float2(sm_mh[h], ls)));
+            continue;
+        }
         const float inv = 1.0f / ls;
+        float o4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o4[k] = KV8 ? (os[k] * v_scale) * inv : os[k] * inv;
+        *reinterpret_cast<uint2*>(row + (int64_t)b * Hq * D + (int64_t)(hq0 + h) * D + d) =
+            make_uint2(pk_bf16(o4[0], o4[1]), pk_bf16(o4[2], o4[3]));
+    }
+    if (!two) {
+        WF_STAMP(2);
+        return;
+    }
+    // the second workgroup of the sequence to get here combines the two records
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned* c = cnt + gb * kTailLine;
+        const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sh_last = old == 1u;
+        if (old == 1u) {  // both past the exchange: re-arm, advance the epoch
+            st_sc1(c, 0u);
+            st_sc1(xep + gb * kTailLine, ep);
+        }
+    }
+    __syncthreads();
+    if (!sh_last) return;
+    const __amdgpu_buffer_rsrc_t rml = make_rsrc(rec_ml), ro = make_rsrc(rec_o);
+    for (int idx = threadIdx.x; idx < grp * (D / 4); idx += 256) {
+        const int h = idx / (D / 4), d = (idx % (D / 4)) * 4;
+        const int64_t r0 = (gb * 2) * grp + h, r1 = (gb * 2 + 1) * grp + h;
+        const uint4 m0 = ld16_sc1(rml, (int)(8 * (r0 & ~1)));  // (M, l) pairs of two heads
+        const uint4 m1 = ld16_sc1(rml, (int)(8 * (r1 & ~1)));
+        const float4 o0 = __builtin_bit_cast(float4, ld16_sc1(ro, (int)(4 * (r0 * D + d))));
+        const float4 o1 = __builtin_bit_cast(float4, ld16_sc1(ro, (int)(4 * (r1 * D + d))));
+        const float L0 = __uint_as_float((r0 & 1) ? m0.w : m0.y);
+        const float rr = __uint_as_float((r1 & 1) ? m1.z : m1.x), L1 = __uint_as_float((r1 & 1) ? m1.w : m1.y);
+        const float L = L0 * rr + L1;
+        const float os[4] = {o0.x * rr + o1.x, o0.y * rr + o1.y, o0.z * rr + o1.z, o0.w * rr + o1.w};
+        const float inv = 1.0f / L;
         float o4[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) o4[k] = KV8 ? (os[k] * v_scale) * inv : os[k] * inv;
@@ -1596,14 +1677,19 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
                   kAttnMfmaMaxGrp);
         return WF_EINVAL;
     }
-    const dim3 grid(Hkv, B);
+    if (kAttnSplit2 && (!merge_cnt || !xmax)) {
+        set_error("decode_attention_partials: batched attention needs the arrival and exchange buffers");
+        return WF_EINVAL;
+    }
+    const dim3 grid(Hkv, B, kAttnSplit2 ? 2 : 1);
     const bool g4 = Hq == 4 * Hkv;
     const float ss = kv8 ? sm_scale * k_scale : sm_scale, vs = kv8 ? v_scale : 1.0f;
     auto kern = kv8 == 2 ? (g4 ? k_attn_sdpa_mfma<2, 4> : k_attn_sdpa_mfma<2, 0>)
               : kv8      ? (g4 ? k_attn_sdpa_mfma<1, 4> : k_attn_sdpa_mfma<1, 0>)
                          : (g4 ? k_attn_sdpa_mfma<0, 4> : k_attn_sdpa_mfma<0, 0>);
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, ss, pt, pps,
-                       npages, kv_pgs, vs, merged_row, order);
+                       npages, kv_pgs, vs, merged_row, order, ml, o, merge_cnt, merge_cnt + (int64_t)B * Hq * kTailLine,
+                       xmax);
     return check_launch("decode_attention_partials");
 }
 
