@@ -5,4 +5,4 @@ P="python -u -m pytest -v -s --timeout 300 --timeout-method thread"
 timeout -k 10 600 $P tests/test_gpu_configs.py -k "attention_kernels or kv_attention_cosine or batch128" > gpurun_out/tsp.log 2>&1; grep -h "passed\|failed\|attention b" gpurun_out/tsp.log | cut -c1-160
 timeout -k 10 600 $P tests/test_gpu_reference_golden.py -k "batch128" > gpurun_out/tsp2.log 2>&1; grep -h "passed\|failed\|vs reference" gpurun_out/tsp2.log | cut -c1-200
 LIBS="libwfbitnet.so libwfbitnet_nosplit.so" bash tools/ab_bench.sh --batch 128 --steps 50 --warmup 10 --no-sub
-LIBS="libwfbitnet.so libwfbitnet_nosplit.so" bash tools/ab_bench.sh --batch 128 --steps 30 --warmup 5 --no-sub --ctx-dist uniform
+

@@ -740,7 +740,7 @@ __global__ __launch_bounds__(kAttnPartThreads) WF_SDPA_WPE void k_attn_sdpa(cons
 // fragment load one contiguous KiB per wave.
 // ---------------------------------------------------------------------------------------------
 #ifndef WF_ATTN_SPLIT2  // 0: one workgroup per (kv head, sequence) whatever the context
-#define WF_ATTN_SPLIT2 1
+#define WF_ATTN_SPLIT2 0
 #endif
 constexpr bool kAttnSplit2 = WF_ATTN_SPLIT2;
 typedef short v8s_t __attribute__((ext_vector_type(8)));
@@ -929,7 +929,7 @@ __global__ __launch_bounds__(256, 3) void k_attn_sdpa_mfma(const uint16_t* __res
             }
             if (s == 4) {  // the block's maxima: every wave's pass 1 is done
                 if (q4 == 0 && l16 < 16) sm_mx[c & 1][wave][l16] = wmx;
-                if (two && sp == 1 && wave == 0 && lane < grp) {  // M_0 of head `lane` from workgroup 0
+                if (two && sp == 1 && c == c0 && wave == 0 && lane < grp) {  // M_0 of head `lane` from workgroup 0
                     const uint64_t* gp = xg + gb * kAttnMfmaMaxGrp + lane;
                     uint64_t gv = ld_sc1(gp);
                     for (int it = 0; (unsigned)(gv >> 32) != ep; ++it) {
@@ -940,7 +940,7 @@ __global__ __launch_bounds__(256, 3) void k_attn_sdpa_mfma(const uint16_t* __res
                     sm_m0[lane] = __uint_as_float((uint32_t)gv);
                 }
                 __syncthreads();
-                if (two && sp == 1) m_run = sm_m0[l16 % grp];  // block 1 continues from block 0's max
+                if (two && sp == 1 && c == c0) m_run = sm_m0[l16 % grp];  // block 1 continues from block 0's max
                 mblk = fmaxf(fmaxf(sm_mx[c & 1][0][l16], sm_mx[c & 1][1][l16]), fmaxf(sm_mx[c & 1][2][l16], sm_mx[c & 1][3][l16]));
                 const float mn = fmaxf(m_run, mblk);
                 r = (c == 0) ? 0.f : expf_rn(m_run - mn);
