@@ -740,7 +740,7 @@ __global__ __launch_bounds__(kAttnPartThreads) WF_SDPA_WPE void k_attn_sdpa(cons
 // fragment load one contiguous KiB per wave.
 // ---------------------------------------------------------------------------------------------
 #ifndef WF_ATTN_SPLIT2  // 0: one workgroup per (kv head, sequence) whatever the context
-#define WF_ATTN_SPLIT2 0
+#define WF_ATTN_SPLIT2 1
 #endif
 constexpr bool kAttnSplit2 = WF_ATTN_SPLIT2;
 typedef short v8s_t __attribute__((ext_vector_type(8)));
@@ -851,7 +851,7 @@ __global__ __launch_bounds__(256, 3) void k_attn_sdpa_mfma(const uint16_t* __res
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
     const int Sb = min(seq_lens[b], S);
     const int NB = (Sb + 511) >> 9;
-    // gridDim.z == 2: a sequence of two or more 512-key blocks takes two workgroups, block 0 and
+    // gridDim.z == 2: a sequence of two or three 512-key blocks takes two workgroups, block 0 and
     // blocks 1 .. NB - 1 (5 kv heads x 128 sequences = 640 workgroups otherwise leave half the CUs 3
     // and half 2). Workgroup 1 needs M_0, the max of block 0, before its first probabilities:
     // workgroup 0 publishes it as epoch-tagged granules (k_attn_sdpa's exchange; all z = 0 workgroups
@@ -860,7 +860,9 @@ __global__ __launch_bounds__(256, 3) void k_attn_sdpa_mfma(const uint16_t* __res
     // r_1 r_2 ... (the factor the CPU loop's running sums carry block 0 by) -- and the second to finish
     // combines them: O = o_0 R + o_1, L = l_0 R + l_1.
     const int sp = blockIdx.z;
-    const bool two = gridDim.z == 2 && NB >= 2;
+    // (two or three blocks only: at config-4 contexts a 7-block second workgroup became the tail,
+    // 136.8 -> 138.7 us; at ctx 1024, three blocks, 67.9 -> 65.9 us)
+    const bool two = gridDim.z == 2 && NB >= 2 && NB <= 3;
     if (sp == 1 && !two) return;  // whole workgroup
     const int c0 = two ? sp : 0, c1 = two ? (sp ? NB : 1) : NB;
     float Rp = 1.f;  // workgroup 1: product of its rescale factors
