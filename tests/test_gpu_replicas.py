@@ -2,7 +2,7 @@
 node tokens/sec") exercised on the GPU box: replica processes started by the node launcher
 (wfamd.replicas.launch, tools/replica_node.py) on the one GPU, each with its own weights seed, host
 core slice and gloo start barrier (no RCCL), running the mixed workload (batch-1 decode beside a
-batch-128 continuous batch at config-4 contexts, paged KV) over two full-width layers. Each replica
+batch-128 continuous batch at config-4 contexts, paged KV) over the full 30-layer model. Each replica
 records its greedy tokens of every step and a hash of its final logits; a replica's results must be
 bit-identical to a solo run of the same seed in a fresh process (independence: nothing shared,
 nothing order-dependent between replicas). Reference: scripts/launch_sglang_bitnet.sh:60-61.
@@ -24,7 +24,7 @@ NODE = str(ROOT / "tools" / "replica_node.py")
 
 
 def _argv(seed: int, steps: int = 6):
-    return [NODE, "--workload", "mixed", "--steps", str(steps), "--layers", "2", "--seed", str(seed), "--verify"]
+    return [NODE, "--workload", "mixed", "--steps", str(steps), "--layers", "30", "--seed", str(seed), "--verify"]
 
 
 def test_replicas_on_one_gpu_match_solo_runs():
