@@ -723,7 +723,7 @@ __global__ __launch_bounds__(kDgWaves * 64) void k_dec_gemm(GemvArgs a) {
 // of its column, decoded into the 4 groups g by shift 6 - 2g -- the same k for both operands.
 // PRO != 0: the row norm of the GEMM's input is fused into the launch (no k_rownorm launch and no
 // kernel boundary before the GEMM). Block (x, y) with x < rows of sequence tile y normalises and
-// quantises row 32 y + x exactly like k_rownorm / k_rownorm_attn (the 512-thread tree; 4-wave blocks
+// quantises row 32 y + x exactly like k_rownorm (the 512-thread tree; 4-wave blocks
 // replay it with two chains per lane), stores its codes, scale and code sum write-through (sc1),
 // drains, and bumps the tile's arrival word; every block of the tile waits for all of its rows
 // (one polling lane, bounded), then reads the codes with sc1 loads. The weight fragments are issued
@@ -2387,12 +2387,9 @@ int gemv_input(wf_model* m, GemvArgs& a, const uint16_t* x, int64_t xs, const ui
     return WF_OK;
 }
 
-// the batched attention forms the O input row in its tail (k_attn_mfma TAIL; its 256-thread norm
-// replays the 512-thread tree for rows of up to 4096)
-
-// the attention merges each head's records into the bf16 row m->attn_row (k_attn_sdpa: batch < 16 and
-// untiled caches); the O input then reads that row
-// the attention also leaves per-split (m, l, o) records (k_attn_sdpa; include/wf_bitnet.h attn view)
+// every decode attention path writes the bf16 row m->attn_row (k_attn_sdpa's merge ticket: batch
+// < 16 or untiled caches; k_attn_sdpa_mfma: batch >= 16 on tile-layout caches); k_attn_sdpa also
+// leaves its per-split (m, l, o) records (include/wf_bitnet.h attention view)
 bool attn_records(const wf_model* m) { return m->d.batch < 16 || !m->kv_tiled; }
 
 // One op of the decode step (WF_OP_* in include/wf_bitnet.h).

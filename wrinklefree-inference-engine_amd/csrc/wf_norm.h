@@ -318,14 +318,6 @@ __device__ __forceinline__ float norm_core_e512(const NormRow<PPT2, 256>& r, int
     return act_scale_f(mx);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Attention row of sequence b from the decode-step attention partials (wf_attn.hip k_attn_part:
-// kAttnPartSplits records per (b, head): ml = (m, l), o unnormalised). Piece p (outputs
-// 8p..8p+7, head h = 8p / D) merges the splits of its head,
-//   out = sum_s e^(m_s - M) o_s / sum_s e^(m_s - M) l_s   (M = max_s m_s; empty splits: m = -inf),
-// rounded to bf16 like the reference's attention output tensor. issue() puts every load in flight
-// (the caller then issues its weight stream); finish() merges. Zero for pieces >= Hq*D/8.
-// ---------------------------------------------------------------------------------------------
 // Quantizes the normalised pieces; piece p (< npad = padded K / 8) goes to dst + off(p). Returns
 // this thread's code sum (the caller reduces it).
 template <int PPT, int NT, class Off, unsigned wf_stamp_base = 0>
