@@ -90,12 +90,12 @@ def choose_cores(n: int) -> tuple[list[int], str]:
     return phys, f"every physical core of the {len(mask)}-CPU affinity mask"
 
 
-def build_lib(flags) -> tuple[str, str]:
-    """(library name, build kind) for this host."""
+def build_lib(flags, extra=()) -> tuple[str, str]:
+    """(library name, build kind) for this host; `extra` = study defines (tools/ab_cpu_team.sh)."""
     if "avx512_vnni" in flags and "avx512bw" in flags:
-        name = "liborc_vnni.so"
+        name = "liborc_vnni" + "".join("_" + d.lower() for d in extra) + ".so"
         try:
-            orc.build(march="native", name=name, defines=("ORC_VNNI",))
+            orc.build(march="native", name=name, defines=("ORC_VNNI",) + tuple(extra))
             return name, "avx512-vnni (vpdpbusd enc-sums" + (", vdpbf16ps LM head)" if "avx512_bf16" in flags
                                                              else ", scalar-fp32 LM head)")
         except Exception:
@@ -189,6 +189,7 @@ def main():
     ap.add_argument("--gemv-seconds", type=float, default=1.0)
     ap.add_argument("--cores", type=int, default=0,
                     help="pin to N physical cores of the affinity mask; 0 = the process's whole CPU share")
+    ap.add_argument("--define", action="append", default=[], help="study define for the VNNI build (A/B only)")
     args = ap.parse_args()
     info = host_info()  # the mask as given, before pinning
     cores, how = choose_cores(args.cores)
@@ -197,7 +198,7 @@ def main():
     os.environ.update(OMP_NUM_THREADS=str(len(cores)), OMP_PROC_BIND="close", OMP_PLACES="cores")
     info.update(cores_used=len(cores), core_choice=how, omp_proc_bind="close", omp_places="cores")
     flags = info.pop("_flags")
-    libname, kind = build_lib(flags)
+    libname, kind = build_lib(flags, args.define)
     threads = orc.num_threads(libname)
     res = {**info, "threads": threads, "build": kind, "vnni": bool(orc.lib(libname).orc_vnni_build()),
            "decode": decode_rate(libname, args.ctx, args.seconds),
