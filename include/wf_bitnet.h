@@ -239,13 +239,17 @@ int wf_model_step(wf_model* m, void* stream);
 int wf_model_graph_launch(wf_model* m, void* stream);
 /* Launch one op of the step (profiling / per-kernel timing). Ops, in step order: */
 enum {
-    WF_OP_EMBED = 0,      /* h = embed[token] + layer-0 input norm / quantize  (layer ignored) */
-    WF_OP_QKV = 1,        /* q|k|v ternary GEMV + correction + RoPE + cache write              */
-    WF_OP_ATTN = 2,       /* split-K GQA decode attention; last block: attn_sub_norm + quantize */
-    WF_OP_O = 3,          /* o_proj + residual; last block: post_attention_layernorm + quantize */
-    WF_OP_GATE_UP = 4,    /* gate|up + relu^2 * up; last block: ffn_sub_norm + quantize         */
-    WF_OP_DOWN = 5,       /* down_proj + residual; last block: next input norm or final norm    */
-    WF_OP_LM_HEAD = 6     /* tied bf16 LM head + greedy argmax + position advance (layer ignored) */
+    WF_OP_EMBED = 0,      /* h = embed[token] (layer ignored; skipped at batch 1, see below)      */
+    WF_OP_QKV = 1,        /* input_layernorm + quantize -> q|k|v ternary GEMV + correction + RoPE
+                             + K/V cache write                                                    */
+    WF_OP_ATTN = 2,       /* GQA decode attention with the reference's CPU bf16 SDPA arithmetic;
+                             writes the bf16 attention row (wf_attn_records.attn_row)             */
+    WF_OP_O = 3,          /* attn_sub_norm + quantize of that row -> o_proj + residual             */
+    WF_OP_GATE_UP = 4,    /* post_attention_layernorm + quantize -> gate|up + relu^2 * up          */
+    WF_OP_DOWN = 5,       /* ffn_sub_norm + quantize -> down_proj + residual                       */
+    WF_OP_LM_HEAD = 6     /* final norm + tied bf16 LM head + greedy argmax + position advance
+                             (layer ignored)                                                      */
+    /* (batch > 1: each GEMM op's norm + quantize runs as a row-norm launch in front of it) */
 };
 /* Batch 1: wf_model_step skips WF_OP_EMBED and layer 0's WF_OP_QKV / WF_OP_O read the token's
  * embedding row (embed[token], the residual) themselves, so wf_model_launch_op(m, 0, WF_OP_QKV or

@@ -127,3 +127,22 @@ def test_timed_window_single_rank():
     tw = timed_window(lambda: calls.append(1), 5, lambda: None)
     assert len(calls) == 5 and tw["max_s"] == tw["local_s"] >= 0 and tw["t_end"] >= tw["t_start"]
     assert timed_steps(lambda: None, 3, lambda: None) >= 0
+
+
+def test_node_line_uses_the_whole_job_clock():
+    """tools/replica_node.py's node headline is every replica's tokens over the max-over-replicas
+    window (bench.py's whole-job clock), not the sum of per-replica rates on their own clocks."""
+    import argparse
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("replica_node", ROOT / "tools" / "replica_node.py")
+    rn = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(rn)
+    args = argparse.Namespace(replicas=2, workload="mixed", same_gpu=True)
+    res = [{"tokens": 1000, "max_seconds": 2.0, "seconds": 1.0, "t_start": 10.0, "t_end": 11.0, "tokens_per_s": 1000.0,
+            "b1_tokens_per_s": 0.0, "b128_tokens_per_s": 1000.0},
+           {"tokens": 1000, "max_seconds": 2.0, "seconds": 2.0, "t_start": 10.0, "t_end": 12.5, "tokens_per_s": 500.0,
+            "b1_tokens_per_s": 0.0, "b128_tokens_per_s": 500.0}]
+    line = rn.node_line(args, res)
+    assert line["node_tokens_per_s"] == 1000.0            # 2000 tokens / 2.0 s
+    assert line["node_tokens_per_s_over_union"] == 800.0  # 2000 tokens / 2.5 s
+    assert line["per_replica_local_rates"]["sum"] == 1500.0  # diagnostic only

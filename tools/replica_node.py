@@ -133,14 +133,21 @@ def child(args):
 
 
 def node_line(args, res) -> dict:
-    """Node totals over the replicas' JSON lines: the summed per-replica rates and, because the
-    windows are barrier-aligned but not identical, the conservative rate over the union of the
-    wall-clock windows (every token of every replica / (last end - first start))."""
+    """Node totals over the replicas' JSON lines. The headline is the whole-job clock of bench.py's
+    contract: every token of every replica / the max over replicas of the timed window
+    (`max_seconds`, all-reduced by the replicas). Beside it the conservative rate over the union of
+    the wall-clock windows (last end - first start), and, as a diagnostic of the spread only, each
+    replica's rate on its own clock (summing those would over-count replicas that share a GPU and
+    finish at different times)."""
     union = max(r["t_end"] for r in res) - min(r["t_start"] for r in res)
+    tokens = sum(r["tokens"] for r in res)
+    job_s = max(r["max_seconds"] for r in res)
     return {"workload": f"{args.replicas} independent replicas ({args.workload}; BASELINE configs[4])",
-            "same_gpu": args.same_gpu, "node_tokens_per_s": aggregate(res),
+            "same_gpu": args.same_gpu, "node_tokens_per_s": round(tokens / job_s, 2),
+            "job_window_s": round(job_s, 4), "tokens": tokens,
             "union_window_s": round(union, 4),
-            "node_tokens_per_s_over_union": round(sum(r["tokens"] for r in res) / union, 2),
+            "node_tokens_per_s_over_union": round(tokens / union, 2),
+            "per_replica_local_rates": aggregate(res),
             "b1": aggregate(res, "b1_tokens_per_s") if args.workload != "b128u" else None,
             "b128": aggregate(res, "b128_tokens_per_s") if args.workload != "b1" else None,
             "replicas": res}
