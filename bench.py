@@ -50,7 +50,7 @@ def parse():
                     help="uniform: per-sequence contexts drawn from U[1, max_seq - steps) with seed 0 (SURVEY §8d "
                          "config 4), on paged KV")
     ap.add_argument("--paged", action="store_true", help="paged KV (32-token pages; batch >= 16)")
-    ap.add_argument("--no-gemv", action="store_true", help="skip the standalone GEMV benchmark")
+    ap.add_argument("--no-gemv", action="store_true", help="skip the standalone GEMV / GEMM-sweep benchmarks")
     ap.add_argument("--no-sub", action="store_true",
                     help="skip the sub-records (batch 128 at ctx 1024 and at config-4 contexts, prefill 8 x 2048) "
                          "that the default N = 1 batch-1 run appends")
@@ -152,6 +152,54 @@ def gemv_bench(rotate_bytes: float = 1.2e9, reps: int = 3):
         del w, graph
         torch.cuda.empty_cache()
     return out
+
+
+GEMM_SWEEP = (6912, 2560, (1, 4, 8, 16, 32))  # (K, N, M): scripts/benchmark_kernels.py:140,162-170 (down proj)
+
+
+def gemm_sweep(rotate_bytes: float = 1.2e9, reps: int = 3):
+    """The reference's GEMM batch sweep (scripts/benchmark_kernels.py:75-106, :162-170): sgl_kernel
+    bitnet_gemm (C-ABI wf_bitnet_gemm: Y = float(sum enc(W) A) * scale, fp32 out) on the down
+    projection 6912 -> 2560 at M in {1, 4, 8, 16, 32}, the launches of one graph replay rotating
+    through >= 1.2 GB of distinct I2_S weight buffers. Per M: µs per call, GOPS = 2 M K N / t and
+    GB/s = (W + M K + 4 M N) / t, as benchmark_kernels.py:98-106 computes them."""
+    import torch
+    from wfamd import _lib
+    lib = _lib.load()
+    K, N, Ms = GEMM_SWEEP
+    g = torch.Generator(device="cuda").manual_seed(1)
+    st = torch.cuda.current_stream()
+    wb = N * K // 4
+    nbuf = max(8, int(rotate_bytes // wb) + 1)
+    w = torch.randint(0, 255, (nbuf, N, K // 4), dtype=torch.uint8, device="cuda", generator=g)
+    w &= 0xAA
+    out = {}
+    for M in Ms:
+        a = torch.randint(-128, 128, (M, K), dtype=torch.int8, device="cuda", generator=g)
+        y = torch.empty(M, N, dtype=torch.float32, device="cuda")
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            cs = torch.cuda.current_stream().cuda_stream
+            for i in range(nbuf):
+                _lib.check(lib.wf_bitnet_gemm(w[i].data_ptr(), a.data_ptr(), 0.01, M, N, K, y.data_ptr(), cs), "gemm")
+        graph.replay()
+        times = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            graph.replay()
+            e1.record(st)
+            torch.cuda.synchronize()
+            times.append(1000.0 * e0.elapsed_time(e1) / nbuf)
+        us = sorted(times)[len(times) // 2]
+        nbytes = wb + M * K + 4 * M * N
+        out[str(M)] = {"M": M, "us": round(us, 3), "gops": round(2.0 * M * K * N / us / 1e3, 1),
+                       "gbs": round(nbytes / us / 1e3, 1), "bytes": nbytes,
+                       "hbm_frac": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4)}
+        del graph
+    del w
+    torch.cuda.empty_cache()
+    return {"layer": f"down proj {K} -> {N}", "calls_per_replay": nbuf, "by_M": out}
 
 
 INT8_DENSE_PEAK_TOPS = 5000.0  # MI355X dense int8 MFMA (MI355X_MICROARCH.md; no 2:1 sparsity)
@@ -375,6 +423,7 @@ def main():
     step_gbs = step_bytes / (ms_step / 1000.0) / 1e9
     roof = roofline(kern, B, args, step_gbs) if kern else None
     gemv = None if (args.no_gemv or B != 1) else gemv_bench()
+    gsweep = None if (args.no_gemv or B != 1) else gemm_sweep()
     sub = None
     if rank == 0 and world == 1 and B == 1 and not args.no_sub and args.ctx_dist == "fixed":
         del dec
@@ -403,7 +452,7 @@ def main():
                           if args.ctx_dist == "uniform" else {})},
             "step_hbm_gbs": round(step_gbs, 1),
             "gemv_hbm_gbs": kern.get("gate_up", {}).get("gbs") if kern else None,
-            "gemv": gemv,
+            "gemv": gemv, "gemm_sweep": gsweep,
             "roofline": roof, "cpu_baseline": cpu, "kernels": kern, "sub_records": sub,
         }
         print(json.dumps(line))

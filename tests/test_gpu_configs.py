@@ -31,6 +31,9 @@ ATTN_S = [1, 31, 32, 33, 1024, 4096]
 # batch-1 attention body switch (wf_attn.hip: one 160-key chunk per split up to 1280 keys, the
 # double-buffered 128-key chunks above): a full one-chunk split, both sides of the switch, two chunks
 ATTN_S_B1 = ATTN_S + [1152, 1280, 1281, 2048]
+# batched rows: the 512-key block edges too (k_attn_sdpa_mfma splits a sequence of two or three
+# blocks over two workgroups and combines their records: one, two and three blocks, both sides)
+ATTN_S_BATCH = ATTN_S + [512, 513, 1025, 1536, 1537]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -297,7 +300,7 @@ def test_step_attention_kernels_vs_oracle(orc, variant):
     cfg = make_cfg(1, 1024, smax)
     w = make_weights(cfg, seed=3, trained_like=True)
     rng = np.random.default_rng(5)
-    S = np.array([ATTN_S[b] if b < len(ATTN_S) else int(rng.integers(1, 4097)) for b in range(B)])
+    S = np.array([ATTN_S_BATCH[b] if b < len(ATTN_S_BATCH) else int(rng.integers(1, 4097)) for b in range(B)])
     if B == 1:
         cases = [np.array([s]) for s in ATTN_S_B1]
     else:
