@@ -257,15 +257,10 @@ enum {
 int wf_model_launch_op(wf_model* m, int layer, int op, void* stream);
 /* Read-only view of the step's attention hand-off, for kernel-level checks (tests/, profiling):
  * after WF_OP_QKV and WF_OP_ATTN of a layer, q holds that layer's query rows after RoPE
- * ([batch, n_heads * head_dim] bf16) and the partial records of the split-K attention: per
- * (sequence b, query head h, record s < records), part_ml[2 ((b n_heads + h) records + s) + {0, 1}] =
- * (running max m, sum l) and the unnormalised output o[d] at part_o[((b n_heads + h) records + s) *
- * 128 + ((d >> 2) & 1) * 64 + (d >> 3) * 4 + (d & 3)] (head_dim 128); the attention output is
- * sum_s e^(m_s - M) o_s / sum_s e^(m_s - M) l_s, M = max_s m_s (records with l = 0 are empty).
- * Batch < 16 and untiled caches: records in one frame (m = 0; the reference's SDPA semantics), which
- * each head's last attention block sums into attn_row. Batch >= 16 on tile-layout caches: no records
- * (records = 0). attn_row is the bf16 attention output [batch, n_heads * head_dim] the O projection
- * reads, on every path. Device pointers owned by the model; valid until wf_model_destroy. */
+ * ([batch, n_heads * head_dim] bf16) and attn_row the bf16 attention output [batch, n_heads *
+ * head_dim] the O projection reads, on every path. records = 0: no path exposes split partials
+ * (part_ml / part_o are the model's scratch). Device pointers owned by the model; valid until
+ * wf_model_destroy. */
 typedef struct {
     const uint16_t* q;
     const float* part_ml;
@@ -274,6 +269,18 @@ typedef struct {
     const uint16_t* attn_row;
 } wf_attn_records;
 int wf_model_attn_view(const wf_model* m, wf_attn_records* out);
+/* The decode attention exchanges split maxima / records between the workgroups of one launch
+ * (batch < 16 or untiled caches; batched split-2 sequences) and bounds every poll: if a sibling
+ * workgroup never becomes resident (the device shared with other work that holds every CU), the
+ * poll gives up after ~0.2-0.5 s, that launch's attention rows are NaN and the kernel raises a
+ * host-visible error word. wf_model_step / wf_model_graph_launch / wf_model_launch_op report (and
+ * clear) it at their next call with WF_EHIP; wf_model_check reports it without launching (call it
+ * after synchronising the stream to check the steps launched so far). */
+int wf_model_check(wf_model* m);
+/* Test hook: with on != 0, the model's batch < 16 / untiled decode attention polls for a tag no
+ * workgroup publishes, so its next EAGER launches (wf_model_step, wf_model_launch_op; a captured
+ * graph keeps the flag of its capture) take the timeout path above. */
+int wf_model_debug_stall_attention(wf_model* m, int on);
 /* Read-only view of the last wf_model_prefill call's last layer, for kernel-level checks (tests/):
  * q = its query rows after RoPE and attn = its causal attention output rows, both [rows][n_heads *
  * head_dim] bf16 in the call's row order. Device pointers owned by the model; valid until the next

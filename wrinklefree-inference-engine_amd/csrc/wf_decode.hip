@@ -39,7 +39,7 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
                               int pps = 0, int npages = 0, int64_t kv_pgs = 0, int kv8 = 0, float k_scale = 1.f,
                               float v_scale = 1.f, uint16_t* merged_row = nullptr,
                               unsigned* merge_cnt = nullptr, uint64_t* xmax = nullptr,
-                              const int32_t* order = nullptr);
+                              const int32_t* order = nullptr, const SdpaBufs* sb = nullptr);
 int seq_order(const int32_t* seq_lens, int B, int S, int32_t* order, hipStream_t st);
 
 // study switches (same-box A/B builds, tools/build_var.sh; measured r04, profiles/ab_r04.txt):
@@ -2096,7 +2096,9 @@ struct wf_model {
     unsigned* seam = nullptr;  // fused row-norm hand-off words (k_dec_gemm_t PRO), zero between launches
     unsigned* attn_cnt = nullptr;  // batched attention tail: one arrival counter per sequence (kTailLine apart)
     uint16_t* attn_row = nullptr;  // batch < 16 / untiled caches: the merged bf16 attention rows [B][H] (kMerge1)
-    uint64_t* attn_xmax = nullptr;  // k_attn_sdpa's exchange: {max, epoch} granules [B][Hq][splits][3]
+    uint64_t* attn_xmax = nullptr;  // k_attn_sdpa_mfma's split-2 exchange: {max, epoch} granules [B][Hkv][8]
+    wf::SdpaBufs sdpa;              // k_attn_sdpa's exchange / record granules and launch counts (batch < 16, untiled)
+    unsigned* err_host = nullptr;   // host-mapped error word the attention raises on a poll timeout (wf_model_check)
     int32_t* attn_order = nullptr;  // batched attention: sequences by decreasing context (k_seq_order)
     int fuse[4] = {0, 0, 0, 0};  // per GEMM op (QKV, O, GU, DN): row norm fused into the GEMM launch
     uint2* am_part = nullptr;
@@ -2390,7 +2392,18 @@ int gemv_input(wf_model* m, GemvArgs& a, const uint16_t* x, int64_t xs, const ui
 // every decode attention path writes the bf16 row m->attn_row (k_attn_sdpa's merge ticket: batch
 // < 16 or untiled caches; k_attn_sdpa_mfma: batch >= 16 on tile-layout caches); k_attn_sdpa also
 // leaves its per-split (m, l, o) records (include/wf_bitnet.h attention view)
-bool attn_records(const wf_model* m) { return m->d.batch < 16 || !m->kv_tiled; }
+bool attn_sdpa_path(const wf_model* m) { return m->d.batch < 16 || !m->kv_tiled; }
+
+// the host-visible error word the decode attention raises when a poll of its in-launch exchange
+// times out (a sibling block never became resident): reported, and cleared, by the next call
+int take_device_error(wf_model* m) {
+    if (!m->err_host) return WF_OK;
+    const unsigned e = __atomic_exchange_n(m->err_host, 0u, __ATOMIC_ACQ_REL);
+    if (!e) return WF_OK;
+    set_error("decode attention: an in-launch exchange timed out (code %u: %s); that step's attention rows are NaN", e,
+              e == WF_ATTN_ERR_SDPA ? "k_attn_sdpa split maxima / records" : "k_attn_sdpa_mfma split-2 block max");
+    return WF_EHIP;
+}
 
 // One op of the decode step (WF_OP_* in include/wf_bitnet.h).
 int run_op(wf_model* m, int l, int op, hipStream_t st) {
@@ -2423,12 +2436,12 @@ int run_op(wf_model* m, int l, int op, hipStream_t st) {
                                                  d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D), m->part_ml,
                                                  m->part_o, st, true, a.pt, a.pps, a.npages, a.kv_pgs, d.kv_quant,
                                                  m->kv_scale[2 * l], m->kv_scale[2 * l + 1], mrow, mcnt, m->attn_xmax,
-                                                 m->attn_order);
+                                                 m->attn_order, &m->sdpa);
             return decode_attention_partials(m->qbuf, (int64_t)d.n_heads * D, a.kc, a.vc, a.kv_b_stride, (int64_t)S * D,
                                              B, d.n_heads, d.n_kv_heads, S, m->seq_lens, 1.0f / sqrtf((float)D),
                                              m->part_ml, m->part_o, st, m->kv_tiled != 0, nullptr, 0, 0, 0, d.kv_quant,
                                              d.kv_quant ? m->kv_scale[2 * l] : 1.f, d.kv_quant ? m->kv_scale[2 * l + 1] : 1.f,
-                                             mrow, mcnt, m->attn_xmax, m->attn_order);
+                                             mrow, mcnt, m->attn_xmax, m->attn_order, &m->sdpa);
         }
         case WF_OP_O:  // h_b = h_a + o_proj(rms_norm(attn_sub_norm)(attn))
             a.w = d.w_o + (int64_t)l * H * wrow_bytes(d.wfmt, H); a.N = H; a.K = H; a.ws0 = wsh[3];
@@ -2511,7 +2524,11 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     const wf_model_desc& d = *dp;
     WF_REQUIRE(d.head_dim == 128, "model_create: head_dim must be 128 (got %d)", d.head_dim);
     WF_REQUIRE(d.hidden == d.n_heads * d.head_dim, "model_create: hidden != n_heads * head_dim");
-    WF_REQUIRE(d.n_kv_heads > 0 && d.n_heads % d.n_kv_heads == 0 && d.n_heads / d.n_kv_heads <= 8, "model_create: bad GQA");
+    WF_REQUIRE(d.n_kv_heads > 0 && d.n_heads % d.n_kv_heads == 0, "model_create: bad GQA");
+    {
+        const int grp = d.n_heads / d.n_kv_heads;
+        WF_REQUIRE(grp == 1 || grp == 2 || grp == 4 || grp == 8, "model_create: GQA group %d not in {1, 2, 4, 8}", grp);
+    }
     WF_REQUIRE(d.hidden % 128 == 0 && d.inter % 128 == 0, "model_create: hidden/inter must be multiples of 128");
     WF_REQUIRE(k_pad(d.wfmt, d.hidden) <= 8192 && k_pad(d.wfmt, d.inter) <= 8192,
                "model_create: hidden/inter (padded to the weight format) > 8192 not supported");
@@ -2602,7 +2619,27 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     // (the second half: k_attn_sdpa's exchange counters)
     WF_ALLOC(m->attn_cnt, 2 * sizeof(unsigned) * (size_t)B * d.n_heads * kTailLine);
     WF_ALLOC(m->attn_row, 2 * (size_t)B * d.hidden);
-    WF_ALLOC(m->attn_xmax, sizeof(uint64_t) * 3 * (size_t)B * d.n_heads * kAttnPartSplits1);
+    WF_ALLOC(m->attn_xmax, sizeof(uint64_t) * 8 * (size_t)B * d.n_kv_heads);
+    if (attn_sdpa_path(m)) {  // k_attn_sdpa: splits, granule buffers, per-block launch counts
+        const int ns = sdpa_splits(B, d.n_kv_heads);
+        if (d.max_seq > ns * kSdpaMaxT) {
+            set_error("model_create: max_seq %d > %d: the batch-%d decode attention takes %d splits of <= %d keys", d.max_seq,
+                      ns * kSdpaMaxT, B, ns, kSdpaMaxT);
+            wf_model_destroy(m);
+            return WF_EINVAL;
+        }
+        const size_t blocks = (size_t)B * d.n_kv_heads * ns;
+        m->sdpa.ns = ns;
+        WF_ALLOC(m->sdpa.xg, sizeof(uint64_t) * kSdpaXG * blocks);
+        WF_ALLOC(m->sdpa.rec, sizeof(uint64_t) * kSdpaRec * blocks);
+        WF_ALLOC(m->sdpa.epoch, sizeof(unsigned) * blocks);
+        if ((e = hipMemset(m->sdpa.xg, 0, sizeof(uint64_t) * kSdpaXG * blocks)) != hipSuccess) return fail(e);
+        if ((e = hipMemset(m->sdpa.rec, 0, sizeof(uint64_t) * kSdpaRec * blocks)) != hipSuccess) return fail(e);
+        if ((e = hipMemset(m->sdpa.epoch, 0, sizeof(unsigned) * blocks)) != hipSuccess) return fail(e);
+    }
+    if ((e = hipHostMalloc((void**)&m->err_host, 64, hipHostMallocMapped)) != hipSuccess) return fail(e);
+    *m->err_host = 0u;
+    if ((e = hipHostGetDevicePointer((void**)&m->sdpa.err, m->err_host, 0)) != hipSuccess) return fail(e);
     WF_ALLOC(m->attn_order, sizeof(int32_t) * (size_t)B);
     {  // identity order until the first step sorts the batch
         std::vector<int32_t> id(B);
@@ -2616,8 +2653,7 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     if ((e = hipMemset(m->seam, 0, sizeof(unsigned) * 2 * kSeamTiles * kSeamLine)) != hipSuccess) return fail(e);
     if ((e = hipMemset(m->attn_cnt, 0, 2 * sizeof(unsigned) * (size_t)B * d.n_heads * kTailLine)) != hipSuccess) return fail(e);
     // granule tags start at 0; the first launch's epoch is 1
-    if ((e = hipMemset(m->attn_xmax, 0, sizeof(uint64_t) * 3 * (size_t)B * d.n_heads * kAttnPartSplits1)) != hipSuccess)
-        return fail(e);
+    if ((e = hipMemset(m->attn_xmax, 0, sizeof(uint64_t) * 8 * (size_t)B * d.n_kv_heads)) != hipSuccess) return fail(e);
     fused_norm_plan(m);
     if ((e = hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking)) != hipSuccess) return fail(e);
     *out = m;
@@ -2629,7 +2665,8 @@ int wf_model_destroy(wf_model* m) {
     if (m->exec) (void)hipGraphExecDestroy(m->exec);
     if (m->graph) (void)hipGraphDestroy(m->graph);
     if (m->cap) (void)hipStreamDestroy(m->cap);
-    void* ptrs[] = {m->attn_cnt, m->attn_row, m->attn_xmax, m->attn_order, m->seq_lens, m->h_a, m->h_b, m->qbuf, m->part_ml, m->part_o, m->hn, m->act, m->q8, m->dec_ws,
+    if (m->err_host) (void)hipHostFree(m->err_host);
+    void* ptrs[] = {m->sdpa.xg, m->sdpa.rec, m->sdpa.epoch, m->attn_cnt, m->attn_row, m->attn_xmax, m->attn_order, m->seq_lens, m->h_a, m->h_b, m->qbuf, m->part_ml, m->part_o, m->hn, m->act, m->q8, m->dec_ws,
                     m->act_sf, m->act_sum, m->tickets, m->seam, m->am_part, m->embed_t, m->pf_h_a, m->pf_h_b, m->pf_q,
                     m->pf_attn, m->pf_act, m->pf_q8, m->pf_sf, m->pf_asum, m->pf_seq};
     for (void* p : ptrs)
@@ -2642,13 +2679,27 @@ int wf_model_destroy(wf_model* m) {
 
 int wf_model_step(wf_model* m, void* stream) {
     WF_REQUIRE(m, "model_step: null model");
+    if (int rc = take_device_error(m)) return rc;
     return model_step(m, as_stream(stream));
 }
 
 int wf_model_launch_op(wf_model* m, int layer, int op, void* stream) {
     WF_REQUIRE(m, "model_launch_op: null model");
     WF_REQUIRE(layer >= 0 && layer < m->d.layers, "model_launch_op: layer %d out of range", layer);
+    if (int rc = take_device_error(m)) return rc;
     return run_op(m, layer, op, as_stream(stream));
+}
+
+int wf_model_check(wf_model* m) {
+    WF_REQUIRE(m, "model_check: null model");
+    return take_device_error(m);
+}
+
+int wf_model_debug_stall_attention(wf_model* m, int on) {
+    WF_REQUIRE(m, "model_debug_stall_attention: null model");
+    WF_REQUIRE(attn_sdpa_path(m), "model_debug_stall_attention: the model's decode attention has no in-launch exchange");
+    m->sdpa.stall = on ? 1 : 0;
+    return WF_OK;
 }
 
 int wf_model_fused_norm(const wf_model* m, int* flags4) {
@@ -2662,7 +2713,7 @@ int wf_model_attn_view(const wf_model* m, wf_attn_records* out) {
     out->q = m->qbuf;
     out->part_ml = reinterpret_cast<const float*>(m->part_ml);
     out->part_o = m->part_o;
-    out->records = attn_records(m) ? kAttnPartSplits1 : 0;
+    out->records = 0;  // round 6: k_attn_sdpa keeps its split records as tagged granules
     out->attn_row = m->attn_row;
     return WF_OK;
 }
@@ -2956,6 +3007,7 @@ int wf_bitnet_mlp(int fmt, const uint8_t* w_gate_up, const uint8_t* w_down, floa
 
 int wf_model_graph_launch(wf_model* m, void* stream) {
     WF_REQUIRE(m, "model_graph_launch: null model");
+    if (int rc = take_device_error(m)) return rc;
     if (!m->exec) {
         WF_HIP(hipStreamBeginCapture(m->cap, hipStreamCaptureModeThreadLocal));
         int rc = model_step(m, m->cap);

@@ -66,6 +66,8 @@ SIGNATURES = {
     "wf_model_graph_launch": (i32, [vp, vp]),
     "wf_model_launch_op": (i32, [vp, i32, i32, vp]),
     "wf_model_attn_view": (i32, [vp, vp]),
+    "wf_model_check": (i32, [vp]),
+    "wf_model_debug_stall_attention": (i32, [vp, i32]),
     "wf_model_fused_norm": (i32, [vp, vp]),
     "wf_model_prefill_reserve": (i32, [vp, i32]),
     "wf_model_prefill": (i32, [vp, vp, vp, vp, i32, vp]),

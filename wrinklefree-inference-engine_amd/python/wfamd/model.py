@@ -489,6 +489,16 @@ class BitNetDecoder:
         st = torch.cuda.current_stream().cuda_stream
         call("wf_model_graph_launch" if graph else "wf_model_step", self._h, st)
 
+    def check(self) -> None:
+        """Raise RuntimeError if a decode attention launched so far gave up on its in-launch exchange
+        (include/wf_bitnet.h wf_model_check; synchronise the stream first to cover every step)."""
+        call("wf_model_check", self._h)
+
+    def debug_stall_attention(self, on: bool) -> None:
+        """Test hook (wf_model_debug_stall_attention): the next eager attention launches poll for a tag
+        no workgroup publishes and take the bounded-spin timeout path."""
+        call("wf_model_debug_stall_attention", self._h, 1 if on else 0)
+
     def attention_records(self):
         """The last WF_OP_QKV / WF_OP_ATTN hand-off (include/wf_bitnet.h wf_model_attn_view) as torch
         tensors on the device: q [B, Hq, D] bf16, ml [B, Hq, R, 2] (m, l), o [B, Hq, R, D] float
