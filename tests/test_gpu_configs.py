@@ -479,15 +479,20 @@ def test_fp8_kv_attention_cosine(orc, ctx):
 # ------------------------------------------------------------------------------------------------
 # (d) prefill 8 x 2048 (BASELINE configs[2])
 # ------------------------------------------------------------------------------------------------
-def test_prefill_attention_vs_oracle_sdpa(orc):
+@pytest.mark.parametrize("kv", ["bf16", "fp8", "int8"])
+def test_prefill_attention_vs_oracle_sdpa(orc, kv):
     """k_attn_prefill_sdpa's causal attention rows (include/wf_bitnet.h wf_model_prefill_view, one
     full-width layer, 2 sequences x 2048 prompt rows, trained-like weights) against the reference's
     SDPA (orc_attention_sdpa_cpu_bf16) on the same q rows and cached K/V over keys [0, pos]: at most
-    0.1 % of the sampled bf16 elements differ (fp32 summation-order ties), as the decode kernels."""
+    0.1 % of the sampled bf16 elements differ (fp32 summation-order ties), as the decode kernels.
+    One-byte K/V (fp8 = e4m3, int8 = the reference's default KVCacheDtype.INT8, power-of-two scales so
+    the dequantised codes are exact bf16): the oracle on the decoded codes, like the batched decode
+    test -- the prompt and its decode steps follow the same SDPA."""
     from wfamd.model import BitNetDecoder, pack_prefill_rows
     cfg = make_cfg(1, 1024, 2080)
     w = make_weights(cfg, seed=6, trained_like=True)
-    dec = BitNetDecoder(cfg, w, batch=16)
+    scale = {"bf16": None, "fp8": [(0.5, 0.25)], "int8": [(1 / 16, 1 / 32)]}[kv]
+    dec = BitNetDecoder(cfg, w, batch=16, kv_dtype=kv, kv_scale=scale)
     del w
     rng = np.random.default_rng(12)
     n = 2048
@@ -497,19 +502,19 @@ def test_prefill_attention_vs_oracle_sdpa(orc):
     _, slot, pos = pack_prefill_rows(seqs)
     q, at = dec.prefill_view(len(slot))
     qb, ab = bits(q), bits(at)
-    kv = {b: [bits(t) for t in logical_kv(dec, 0, b, n)] for b in range(2)}
+    kvb = {b: [kv_bits(dec, t, 0, j) for j, t in enumerate(logical_kv(dec, 0, b, n))] for b in range(2)}
     picks = sorted(set(list(range(0, len(slot), 13)) + list(range(n - 40, n)) + [n, n + 511, n + 512, n + 513]))
     mism = elems = 0
     worst = []
     for r in picks:
         b, p = slot[r], pos[r]
-        exp = orc.attention_sdpa_cpu_bf16(qb[r], kv[b][0], kv[b][1], p + 1)
+        exp = orc.attention_sdpa_cpu_bf16(qb[r], kvb[b][0], kvb[b][1], p + 1)
         m = int((exp != ab[r]).sum())
         mism += m
         elems += exp.size
         if m:
             worst.append((b, p, m))
-    print(f"prefill attention: {mism} of {elems} sampled bf16 elements off the oracle; rows {worst[:20]}")
+    print(f"prefill attention ({kv} K/V): {mism} of {elems} sampled bf16 elements off the oracle; rows {worst[:20]}")
     assert mism <= max(2, elems // 1000), (mism, elems, worst[:20])
     # the batched decode attention (k_attn_sdpa_mfma) on the same caches: 16 slots, slot s < 2 at
     # positions of its prompt (its K/V row is rewritten bit-identically), the others at position 0
@@ -527,7 +532,7 @@ def test_prefill_attention_vs_oracle_sdpa(orc):
         for s_ in range(2):
             r = s_ * n + p0
             assert np.array_equal(qdb[s_], qb[r]), (s_, p0)  # the decode step's q row is the prefill's
-            exp = orc.attention_sdpa_cpu_bf16(qdb[s_], kv[s_][0], kv[s_][1], p0 + 1)
+            exp = orc.attention_sdpa_cpu_bf16(qdb[s_], kvb[s_][0], kvb[s_][1], p0 + 1)
             dm += int((exp != row[s_]).sum())
             dme += exp.size
     print(f"batched decode attention on the same caches: {dm} of {dme} bf16 elements off the oracle")

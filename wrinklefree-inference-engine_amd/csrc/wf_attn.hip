@@ -516,14 +516,17 @@ __device__ __forceinline__ void sdpa_pv(const float (&sv)[G], uint4 vr, int t, i
     else sdpa_pv_blk<G>(sv, vx, vec, bm[2], br[2], l, o);
 }
 
-template <int G, bool ONE>
-__device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, int64_t q_sb, const uint16_t* __restrict__ K,
-                                               const uint16_t* __restrict__ V, int64_t kv_sb, int64_t kv_sh, int Hkv, int S,
-                                               int b, int Sb, float sm_scale, int NS, const uint64_t* qkpre,
-                                               uint64_t* __restrict__ xg, uint64_t* __restrict__ rec, unsigned ep,
-                                               unsigned want, uint16_t* __restrict__ row_out, unsigned* __restrict__ err) {
-    constexpr int D = 128, NWV = 4, UC = 4, CH = UC * 16;  // UC keys per lane group per 64-key chunk
+template <int G, int NT, bool ONE>
+__device__ __forceinline__ unsigned attn_sdpa_body(const uint16_t* __restrict__ q, int64_t q_sb, const uint16_t* __restrict__ K,
+                                                   const uint16_t* __restrict__ V, int64_t kv_sb, int64_t kv_sh, int Hkv, int S,
+                                                   int b, int Sb, float sm_scale, int NS, unsigned* __restrict__ ew,
+                                                   int stall, uint64_t* __restrict__ xg, uint64_t* __restrict__ rec,
+                                                   uint16_t* __restrict__ row_out, unsigned* __restrict__ err) {
+    constexpr int D = 128, NWV = NT / 64, NG = NT / 16;  // waves, 16-lane key groups
+    constexpr int CH = 64, UC = CH / NG;                 // 64-key chunks: UC keys per lane group
     constexpr bool QD = G <= 4;
+    constexpr int MP = (G * 64 + kSdpaNSMax + 63) / 64;  // merge: record pair granules per lane of the polling wave
+    constexpr int ML = (kSdpaNSMax * G + 63) / 64;       // merge: l granules per lane
     const int s = blockIdx.x, g = blockIdx.y;
     const int tid = threadIdx.x, gid = tid >> 4, li = tid & 15, wv = tid >> 6, lane = tid & 63;
     const int64_t bg = (int64_t)b * Hkv + g;
@@ -531,7 +534,6 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
     const int nact = (Sb + T - 1) / T;
     const int t0 = s * T, t1 = min(t0 + T, Sb);
     const int cb0 = t0 >> 9, cb1 = (t1 - 1) >> 9;
-    (void)qkpre;
     __shared__ float red[NWV][G][3];
     __shared__ float blk_m[G][3], blk_r[G][3], fin_r[G];
     __shared__ __attribute__((aligned(16))) float sm_o[NWV][G][D];
@@ -539,18 +541,21 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
     __shared__ float sc_lds[ONE ? 1 : G][ONE ? 1 : kSdpaMaxT];
     __shared__ __attribute__((aligned(16))) float mv[2 * (8 * 64 + kSdpaNSMax)];
     __shared__ float mL[kSdpaNSMax * G];
+    __shared__ int sh_bad;
 
-    // ---- loads: K (and V) of the split's keys, q of the group's heads ----
+    // ---- loads: this block's launch count (the tag; every lane, no branch, so no wait until it is
+    // used), K (and V) of the split's keys, q of the group's heads ----
+    const unsigned ep0 = ld_sc1(ew);
     const int64_t kvb = b * kv_sb + g * kv_sh + li * 8;
     const int tl = max(t1 - 1, 0);
     uint4 kA[UC], vA[UC], kB[ONE ? 1 : UC], vB[ONE ? 1 : UC];
 #pragma unroll
     for (int u = 0; u < UC; ++u)
-        if (u * 16 < T) kA[u] = *reinterpret_cast<const uint4*>(K + kvb + (int64_t)min(t0 + gid + 16 * u, tl) * D);
+        if (u * NG < T) kA[u] = *reinterpret_cast<const uint4*>(K + kvb + (int64_t)min(t0 + gid + NG * u, tl) * D);
     if constexpr (ONE) {
 #pragma unroll
         for (int u = 0; u < UC; ++u)
-            if (u * 16 < T) vA[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)min(t0 + gid + 16 * u, tl) * D);
+            if (u * NG < T) vA[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)min(t0 + gid + NG * u, tl) * D);
     }
     double qd[QD ? G : 1][8];
     uint4 qr[QD ? 1 : G];
@@ -574,8 +579,8 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
     if constexpr (ONE) {
 #pragma unroll
         for (int u = 0; u < UC; ++u)
-            if (u * 16 < T) {
-                const int t = t0 + gid + 16 * u;
+            if (u * NG < T) {
+                const int t = t0 + gid + NG * u;
                 sdpa_score<G, QD>(qd, qr, kA[u], sm_scale, sc[u]);
                 sdpa_max<G>(sc[u], t, t1, cb0, mx);
             }
@@ -584,11 +589,11 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
             if (c0 + CH < t1) {
 #pragma unroll
                 for (int u = 0; u < UC; ++u)
-                    kB[u] = *reinterpret_cast<const uint4*>(K + kvb + (int64_t)min(c0 + CH + gid + 16 * u, tl) * D);
+                    kB[u] = *reinterpret_cast<const uint4*>(K + kvb + (int64_t)min(c0 + CH + gid + NG * u, tl) * D);
             }
 #pragma unroll
             for (int u = 0; u < UC; ++u) {
-                const int t = c0 + gid + 16 * u;
+                const int t = c0 + gid + NG * u;
                 float sv[G];
                 sdpa_score<G, QD>(qd, qr, kA[u], sm_scale, sv);
                 sdpa_max<G>(sv, t, t1, cb0, mx);
@@ -600,12 +605,12 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
             if (c0 + 2 * CH < t1) {
 #pragma unroll
                 for (int u = 0; u < UC; ++u)
-                    kA[u] = *reinterpret_cast<const uint4*>(K + kvb + (int64_t)min(c0 + 2 * CH + gid + 16 * u, tl) * D);
+                    kA[u] = *reinterpret_cast<const uint4*>(K + kvb + (int64_t)min(c0 + 2 * CH + gid + NG * u, tl) * D);
             }
             if (c0 + CH < t1) {
 #pragma unroll
                 for (int u = 0; u < UC; ++u) {
-                    const int t = c0 + CH + gid + 16 * u;
+                    const int t = c0 + CH + gid + NG * u;
                     float sv[G];
                     sdpa_score<G, QD>(qd, qr, kB[u], sm_scale, sv);
                     sdpa_max<G>(sv, t, t1, cb0, mx);
@@ -618,11 +623,11 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
         }
         // V chunks 0 and 1 in flight across the exchange
 #pragma unroll
-        for (int u = 0; u < UC; ++u) vA[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)min(t0 + gid + 16 * u, tl) * D);
+        for (int u = 0; u < UC; ++u) vA[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)min(t0 + gid + NG * u, tl) * D);
         if (t0 + CH < t1) {
 #pragma unroll
             for (int u = 0; u < UC; ++u)
-                vB[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)min(t0 + CH + gid + 16 * u, tl) * D);
+                vB[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)min(t0 + CH + gid + NG * u, tl) * D);
         }
     }
 #pragma unroll
@@ -632,29 +637,33 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
             const float m4 = pl_max4(mx[h][jj]);
             if (lane == 0) red[wv][h][jj] = m4;
         }
+    // every wave has its launch count in hand before the barrier (readfirstlane waits for the load),
+    // so the word can be re-stored once this block is done with it (the caller, at the end)
+    const unsigned ep = (unsigned)__builtin_amdgcn_readfirstlane((int)ep0) + 1u;
     __syncthreads();
     WF_STAMP(1);
+    const unsigned want = stall ? ep + 1u : ep;  // test hook (wf_model_debug_stall_attention): a tag nobody stores
     // ---- the exchange: publish this split's G x 3 block maxima, fold every split's ----
     if (tid < 3 * G) {
         const int h = tid / 3, jj = tid - 3 * h;
-        const float m = fmaxf(fmaxf(red[0][h][jj], red[1][h][jj]), fmaxf(red[2][h][jj], red[3][h][jj]));
+        float m = red[0][h][jj];
+#pragma unroll
+        for (int w = 1; w < NWV; ++w) m = fmaxf(m, red[w][h][jj]);
         st_sc1(xg + (bg * NS + s) * kSdpaXG + tid, ((uint64_t)ep << 32) | __float_as_uint(m));
     }
-    for (int h = wv; h < G; h += NWV) {  // wave w: head w (and w + 4)
+    for (int h = wv; h < G; h += NWV) {  // wave w: head w (and w + 4 at 4 waves)
         const int n = 3 * nact;          // granules of head h: (split, block entry)
         uint64_t gv[3] = {0, 0, 0};
         bool bad = false;
-        for (int it = 0;; ++it) {
-            bool good = true;
+        for (int it = 0;; ++it) {  // every load of a pass issued before any is checked (clamped indices:
+            bool good = true;      // a load under a lane condition is waited for on the spot)
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
-                const int e = lane + 64 * i;
-                if (e < n) {
-                    const int sp = e / 3;
-                    gv[i] = ld_sc1(xg + (bg * NS + sp) * kSdpaXG + h * 3 + (e - 3 * sp));
-                    good = good && (unsigned)(gv[i] >> 32) == want;
-                }
+                const int e = min(lane + 64 * i, n - 1), sp = e / 3;
+                gv[i] = ld_sc1(xg + (bg * NS + sp) * kSdpaXG + h * 3 + (e - 3 * sp));
             }
+#pragma unroll
+            for (int i = 0; i < 3; ++i) good = good && (unsigned)(gv[i] >> 32) == want;
             if (__all(good)) break;
             if (it >= WF_SDPA_SPIN) {
                 bad = true;
@@ -717,15 +726,15 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
     if constexpr (ONE) {
 #pragma unroll
         for (int u = 0; u < UC; ++u)
-            if (u * 16 < T) {
-                const int t = t0 + gid + 16 * u;
+            if (u * NG < T) {
+                const int t = t0 + gid + NG * u;
                 if (t < t1) sdpa_pv<G>(sc[u], vA[u], t, cb0, Sb, bm, br, l, o);
             }
     } else {
         for (int c0 = t0; c0 < t1; c0 += 2 * CH) {
 #pragma unroll
             for (int u = 0; u < UC; ++u) {
-                const int t = c0 + gid + 16 * u;
+                const int t = c0 + gid + NG * u;
                 if (t < t1) {
                     float sv[G];
 #pragma unroll
@@ -736,12 +745,12 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
             if (c0 + 2 * CH < t1) {
 #pragma unroll
                 for (int u = 0; u < UC; ++u)
-                    vA[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)min(c0 + 2 * CH + gid + 16 * u, tl) * D);
+                    vA[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)min(c0 + 2 * CH + gid + NG * u, tl) * D);
             }
             if (c0 + CH < t1) {
 #pragma unroll
                 for (int u = 0; u < UC; ++u) {
-                    const int t = c0 + CH + gid + 16 * u;
+                    const int t = c0 + CH + gid + NG * u;
                     if (t < t1) {
                         float sv[G];
 #pragma unroll
@@ -752,12 +761,14 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
                 if (c0 + 3 * CH < t1) {
 #pragma unroll
                     for (int u = 0; u < UC; ++u)
-                        vB[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)min(c0 + 3 * CH + gid + 16 * u, tl) * D);
+                        vB[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)min(c0 + 3 * CH + gid + NG * u, tl) * D);
                 }
             }
         }
     }
-    // ---- the block's record per head: lane groups summed (permlane swaps), then the 4 waves ----
+    WF_STAMP(6);
+    // ---- the block's record per head: the wave's 4 lane groups summed (permlane swaps), then the
+    // waves in order ----
 #pragma unroll
     for (int h = 0; h < G; ++h) {
         l[h] = pl32_sum(pl16_sum(l[h]));
@@ -776,7 +787,7 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
     WF_STAMP(3);
     uint16_t* orow = row_out + (int64_t)b * (G * Hkv) * D + (int64_t)g * G * D;  // the group's G x 128 outputs
     if (nact == 1) {  // the whole context in this split: the row directly
-        for (int p = tid; p < G * 64; p += 256) {
+        for (int p = tid; p < G * 64; p += NT) {
             const int h = p >> 6, d = 2 * (p & 63);
             const float fr = fin_r[h];
             float O0 = 0.f, O1 = 0.f, L = 0.f;
@@ -786,12 +797,13 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
             const float inv = 1.0f / L;
             *reinterpret_cast<uint32_t*>(orow + 2 * p) = pk_bf16(O0 * inv, O1 * inv);
         }
-        return;
+        WF_STAMP(4);
+        return ep;
     }
     // ---- phase 3: publish the record, merge this block's slice of the group's outputs ----
     const __amdgpu_buffer_rsrc_t rr = make_rsrc(rec);
     const int64_t rbase = (bg * NS + s) * kSdpaRec;
-    for (int p = tid; p < G * 64; p += 256) {
+    for (int p = tid; p < G * 64; p += NT) {
         const int h = p >> 6, d = 2 * (p & 63);
         const float fr = fin_r[h];
         float O0 = 0.f, O1 = 0.f;
@@ -807,24 +819,34 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
     }
     const int P = G * 64, CHP = (P + nact - 1) / nact;  // output pairs of the group / per merging block
     const int p0 = s * CHP, np = min(P, p0 + CHP) - p0;
-    if (np <= 0) return;
-    const int pi = tid % np, slot = tid / np, nslot = 256 / np;
-    {
+    if (np <= 0) {
+        WF_STAMP(4);
+        return ep;
+    }
+    // wave 0 polls this block's slice of every split's record -- np pair granules of each split
+    // (<= MP per lane) and the splits' G l granules (<= ML per lane) -- every load of a pass issued
+    // before any is checked; one polling wave keeps the sc1 traffic at a few KB per pass
+    if (wv == 0) {
+        const int npg = np * nact, nl = nact * G;
         bool bad = false;
+        uint4 v[MP];
+        uint64_t x[ML];
         for (int it = 0;; ++it) {
-            bool good = true;
-            if (slot < nslot)
-                for (int sp = slot; sp < nact; sp += nslot) {
-                    const uint4 v = ld16_sc1(rr, (int)(8 * ((bg * NS + sp) * kSdpaRec + 2 * (p0 + pi))));
-                    good = good && v.y == want && v.w == want;
-                    *reinterpret_cast<float2*>(&mv[2 * (sp * np + pi)]) = make_float2(__uint_as_float(v.x), __uint_as_float(v.z));
-                }
-            for (int e = tid; e < nact * G; e += 256) {
-                const int sp = e / G;
-                const uint64_t x = ld_sc1(rec + (bg * NS + sp) * kSdpaRec + G * D + (e - G * sp));
-                good = good && (unsigned)(x >> 32) == want;
-                mL[e] = __uint_as_float((uint32_t)x);
+#pragma unroll
+            for (int k = 0; k < MP; ++k) {
+                const int e = min(lane + 64 * k, npg - 1), sp = e / np;
+                v[k] = ld16_sc1(rr, (int)(8 * ((bg * NS + sp) * kSdpaRec + 2 * (p0 + e - np * sp))));
             }
+#pragma unroll
+            for (int k = 0; k < ML; ++k) {
+                const int e = min(lane + 64 * k, nl - 1), sp = e / G;
+                x[k] = ld_sc1(rec + (bg * NS + sp) * kSdpaRec + G * D + (e - G * sp));
+            }
+            bool good = true;
+#pragma unroll
+            for (int k = 0; k < MP; ++k) good = good && v[k].y == want && v[k].w == want;
+#pragma unroll
+            for (int k = 0; k < ML; ++k) good = good && (unsigned)(x[k] >> 32) == want;
             if (__all(good)) break;
             if (it >= WF_SDPA_SPIN) {
                 bad = true;
@@ -833,52 +855,63 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        __syncthreads();
-        if (tid < np) {
-            const int p = p0 + tid, h = p >> 6;
-            float O0 = 0.f, O1 = 0.f, L = 0.f;
-            for (int sp = 0; sp < nact; ++sp) {  // split order
-                const float2 v = *reinterpret_cast<const float2*>(&mv[2 * (sp * np + tid)]);
-                O0 += v.x;
-                O1 += v.y;
-                L += mL[sp * G + h];
-            }
-            const float inv = bad ? __uint_as_float(0x7fc00000u) : 1.0f / L;
-            *reinterpret_cast<uint32_t*>(orow + 2 * p) = pk_bf16(O0 * inv, O1 * inv);
+#pragma unroll
+        for (int k = 0; k < MP; ++k)  // pair granule e = (split e / np, pair e % np) -> mv[e]
+            if (lane + 64 * k < npg)
+                *reinterpret_cast<float2*>(&mv[2 * (lane + 64 * k)]) = make_float2(__uint_as_float(v[k].x), __uint_as_float(v[k].z));
+#pragma unroll
+        for (int k = 0; k < ML; ++k)
+            if (lane + 64 * k < nl) mL[lane + 64 * k] = __uint_as_float((uint32_t)x[k]);
+        if (lane == 0) sh_bad = bad;
+    }
+    __syncthreads();
+    WF_STAMP(5);
+    if (tid < np) {
+        const int p = p0 + tid, h = p >> 6;
+        float O0 = 0.f, O1 = 0.f, L = 0.f;
+        for (int sp = 0; sp < nact; ++sp) {  // split order
+            const float2 v = *reinterpret_cast<const float2*>(&mv[2 * (sp * np + tid)]);
+            O0 += v.x;
+            O1 += v.y;
+            L += mL[sp * G + h];
         }
+        const float inv = sh_bad ? __uint_as_float(0x7fc00000u) : 1.0f / L;
+        *reinterpret_cast<uint32_t*>(orow + 2 * p) = pk_bf16(O0 * inv, O1 * inv);
     }
     WF_STAMP(4);
+    return ep;
 }
 
+#ifndef WF_SDPA_THREADS  // study builds: threads per k_attn_sdpa block (256 or 512)
+#define WF_SDPA_THREADS 512
+#endif
+constexpr int kSdpaThreads = WF_SDPA_THREADS;
 template <int G>
-__global__ __launch_bounds__(256) void k_attn_sdpa(const uint16_t* __restrict__ q, int64_t q_sb, const uint16_t* __restrict__ K,
-                                                   const uint16_t* __restrict__ V, int64_t kv_sb, int64_t kv_sh, int S,
-                                                   const int32_t* __restrict__ seq_lens, float sm_scale, int b0, int NS,
-                                                   uint64_t* __restrict__ xg, uint64_t* __restrict__ rec,
-                                                   unsigned* __restrict__ epw, uint16_t* __restrict__ row_out,
-                                                   unsigned* __restrict__ err, int stall) {
+__global__ __launch_bounds__(kSdpaThreads) void k_attn_sdpa(const uint16_t* __restrict__ q, int64_t q_sb,
+                                                            const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+                                                            int64_t kv_sb, int64_t kv_sh, int S,
+                                                            const int32_t* __restrict__ seq_lens, float sm_scale, int b0,
+                                                            int NS, uint64_t* __restrict__ xg, uint64_t* __restrict__ rec,
+                                                            unsigned* __restrict__ epw, uint16_t* __restrict__ row_out,
+                                                            unsigned* __restrict__ err, int stall) {
     const int s = blockIdx.x, g = blockIdx.y, b = b0 + (int)blockIdx.z, Hkv = gridDim.y;
-    // this block's launch count: its tag (the first lane reads and re-stores its own word; every
-    // block of the grid does, so the words of a group stay equal)
-    __shared__ unsigned sh_ep;
-    if (threadIdx.x == 0) {
-        unsigned* w = epw + ((int64_t)b * Hkv + g) * NS + s;
-        const unsigned e = ld_sc1(w) + 1u;
-        st_sc1(w, e);
-        sh_ep = e;
-    }
+    // this block's launch count is its tag: every block of the grid reads and re-stores its own word
+    // (first lane), so the words of a group stay equal; read inside the body behind the K / V loads
+    unsigned* ew = epw + ((int64_t)b * Hkv + g) * NS + s;
     const int Sb = min(seq_lens[b], S);
     const int T = sdpa_T(max(Sb, 1), NS);
-    __syncthreads();
-    const unsigned ep = sh_ep;
-    if (Sb <= 0 || s * T >= Sb) return;  // no keys in this split (block-uniform)
-    const unsigned want = stall ? ep + 1u : ep;  // test hook (wf_model_debug_stall_attention): a tag nobody stores
+    if (Sb <= 0 || s * T >= Sb) {  // no keys in this split (block-uniform)
+        if (threadIdx.x == 0) st_sc1(ew, ld_sc1(ew) + 1u);
+        return;
+    }
+    unsigned ep;
     if (T <= kSdpaOneT)
-        attn_sdpa_body<G, true>(q, q_sb, K, V, kv_sb, kv_sh, Hkv, S, b, Sb, sm_scale, NS, nullptr, xg, rec, ep, want,
-                                row_out, err);
+        ep = attn_sdpa_body<G, kSdpaThreads, true>(q, q_sb, K, V, kv_sb, kv_sh, Hkv, S, b, Sb, sm_scale, NS, ew, stall, xg,
+                                                   rec, row_out, err);
     else
-        attn_sdpa_body<G, false>(q, q_sb, K, V, kv_sb, kv_sh, Hkv, S, b, Sb, sm_scale, NS, nullptr, xg, rec, ep, want,
-                                 row_out, err);
+        ep = attn_sdpa_body<G, kSdpaThreads, false>(q, q_sb, K, V, kv_sb, kv_sh, Hkv, S, b, Sb, sm_scale, NS, ew, stall, xg,
+                                                    rec, row_out, err);
+    if (threadIdx.x == 0) st_sc1(ew, ep);  // every wave read the word before the body's first barrier
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1288,164 +1321,11 @@ int seq_order(const int32_t* seq_lens, int B, int S, int32_t* order, hipStream_t
 // ---------------------------------------------------------------------------------------------
 // Prefill (causal) attention on the tile-layout K/V caches, after the prefill QKV GEMM has written
 // the prompt's K/V rows: query row m (a prompt token of KV slot row_slot[m] at position
-// row_pos[m]) attends to keys [0, row_pos[m]] of its slot. Block = (4 waves, kv head g); a wave
-// takes RPW = 4 CG consecutive rows as CG column groups: MFMA column c = 4 tk + h of group u is
-// token 4u + tk with query head h of the group (the decode kernel's head columns, all 16 used),
-// and every K/V fragment it loads feeds all CG groups. The host packs every aligned group of
-// kPrefillRowGroup rows from one slot (padding with repeats of a sequence's last token). Per 32-key tile:
-// the decode kernel's QK / online softmax / P.V with a per-column causal limit, P as bf16 hi + lo
-// for the P.V MFMAs (the decode kernel's ~16 mantissa bits) and the
-// accumulator rescale skipped while no column's running max moves; V rows past the wave's last
-// position are zeroed (stale pages). Each wave streams its whole key
-// range and writes the normalised output rows bf16(o / l) (no split partials).
+// row_pos[m]) attends to keys [0, row_pos[m]] of its slot, with the reference's SDPA arithmetic
+// (k_attn_prefill_sdpa below; every K/V element type, round 6 -- the round-1..5 row-split
+// exact-softmax kernel k_attn_prefill that one-byte caches took is gone).
 // ---------------------------------------------------------------------------------------------
-template <int CG, int OCC, int KV8 = 0>
-__global__ __launch_bounds__(256, OCC) void k_attn_prefill(const uint16_t* __restrict__ q, int64_t q_rs,
-                                                         const uint16_t* __restrict__ K, const uint16_t* __restrict__ Vt,
-                                                         int64_t kv_sb, int64_t kv_sh, int Hq, int Hkv,
-                                                         const int32_t* __restrict__ row_pos,
-                                                         const int32_t* __restrict__ row_slot, int M, float sm_scale,
-                                                         const int32_t* __restrict__ pt, int pps, int npages,
-                                                         int64_t kv_pgs, uint16_t* __restrict__ out, int64_t o_rs,
-                                                         float v_scale) {
-    constexpr int D = 128, RPW = 4 * CG;
-    using KF = KvFrag<KV8>;
-    using FT = typename KF::T;  // rows per wave: CG column groups of 4 tokens x 4 heads
-    const int g = blockIdx.y, hq0 = g * 4;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
-    const int r0 = (blockIdx.x * 4 + wave) * RPW;  // this wave's rows
-    if (r0 >= M) return;                            // whole wave
-    const int slot = row_slot[r0];
-    int lim_c[CG], lim_w = 0;  // column l16 of group u = (token 4u + (l16 >> 2), head l16 & 3)
-#pragma unroll
-    for (int u = 0; u < CG; ++u) lim_c[u] = row_pos[min(r0 + 4 * u + (l16 >> 2), M - 1)] + 1;
-#pragma unroll
-    for (int t = 0; t < RPW; ++t) lim_w = max(lim_w, row_pos[min(r0 + t, M - 1)] + 1);
-    const int64_t kvo = (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;  // element offset
-    const int32_t* ptb = pt ? pt + (int64_t)slot * pps : nullptr;
-
-    v8s_t qf[CG][4];
-#pragma unroll
-    for (int u = 0; u < CG; ++u) {
-        const int row = min(r0 + 4 * u + (l16 >> 2), M - 1);
-        const uint16_t* qp = q + (int64_t)row * q_rs + (int64_t)(hq0 + (l16 & 3)) * D + 8 * q4;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) qf[u][c] = __builtin_bit_cast(v8s_t, *reinterpret_cast<const uint4*>(qp + 32 * c));
-    }
-    auto load = [&](FT (&kr)[2][4], FT (&vr)[8], int bs) {
-        const int64_t blk = ptb ? (int64_t)min(max(ptb[__builtin_amdgcn_readfirstlane(bs) >> 5], 0), npages - 1) * kv_pgs
-                                : (int64_t)(bs >> 5) * 4096;
-#pragma unroll
-        for (int tau = 0; tau < 2; ++tau)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) kr[tau][c] = KF::ld(K, kvo + blk + (tau * 4 + c) * 512);
-#pragma unroll
-        for (int n = 0; n < 8; ++n) vr[n] = KF::ld(Vt, kvo + blk + n * 512);
-    };
-    float m_run[CG], l_run[CG];
-    v4f_t acc[CG][8];
-#pragma unroll
-    for (int u = 0; u < CG; ++u) {
-        m_run[u] = -INFINITY;
-        l_run[u] = 0.f;
-#pragma unroll
-        for (int n = 0; n < 8; ++n) acc[u][n] = v4f_t{0.f, 0.f, 0.f, 0.f};
-    }
-    FT kA[2][4], vA[8];
-    load(kA, vA, 0);
-    for (int bs = 0; bs < lim_w; bs += 32) {
-        v8s_t ph[CG], pl[CG];
-        float ar[CG][4];
-        bool resc[CG];
-#pragma unroll
-        for (int u = 0; u < CG; ++u) {
-            v4f_t sc[2];
-#pragma unroll
-            for (int tau = 0; tau < 2; ++tau) {
-                sc[tau] = v4f_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    sc[tau] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8s_t, KF::bf(kA[tau][c])),
-                                                                      qf[u][c], sc[tau], 0, 0, 0);
-            }
-            const int lim = lim_c[u] - bs - 8 * q4;  // valid keys of column l16 among this lane's 8
-            float x[8], mx = -INFINITY;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                x[e] = e < lim ? sc[e >> 2][e & 3] * sm_scale : -INFINITY;
-                mx = fmaxf(mx, x[e]);
-            }
-            mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-            // key 0 is valid for every column, so m_run is finite after the first tile; a later tile
-            // with no valid key for a column leaves it unchanged (alpha = 1, p = 0)
-            const float mnew = fmaxf(m_run[u], mx);
-            const float alpha = __expf(m_run[u] - mnew);
-            m_run[u] = mnew;
-            float p[8], ps = 0.f;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                p[e] = __expf(x[e] - mnew);
-                ps += p[e];
-            }
-            l_run[u] = l_run[u] * alpha + ps;
-            uint32_t hi[4], lo[4];  // P as bf16 hi + lo (~16 mantissa bits), as the decode kernels
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                hi[j] = pk_bf16(p[2 * j], p[2 * j + 1]);
-                lo[j] = pk_bf16(p[2 * j] - bf_lo(hi[j]), p[2 * j + 1] - bf_hi(hi[j]));
-            }
-            ph[u] = __builtin_bit_cast(v8s_t, make_uint4(hi[0], hi[1], hi[2], hi[3]));
-            pl[u] = __builtin_bit_cast(v8s_t, make_uint4(lo[0], lo[1], lo[2], lo[3]));
-            resc[u] = __any(alpha != 1.0f);  // the running max moved for some column: rescale acc
-#pragma unroll
-            for (int r = 0; r < 4; ++r) ar[u][r] = __shfl(alpha, 4 * q4 + r, 64);
-        }
-        const int limv = lim_w - bs - 8 * q4;  // V rows past every column's limit: zero (stale)
-        v8s_t vf[8];
-#pragma unroll
-        for (int n = 0; n < 8; ++n) vf[n] = __builtin_bit_cast(v8s_t, KF::bf(KF::mask(vA[n], limv)));
-        if (bs + 32 < lim_w) load(kA, vA, bs + 32);  // next tile in flight during the P.V MFMAs
-#pragma unroll
-        for (int u = 0; u < CG; ++u)
-#pragma unroll
-            for (int n = 0; n < 8; ++n) {
-                if (resc[u]) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) acc[u][n][r] *= ar[u][r];
-                }
-                acc[u][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph[u], vf[n], acc[u][n], 0, 0, 0);
-                acc[u][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl[u], vf[n], acc[u][n], 0, 0, 0);
-            }
-    }
-    if constexpr (KV8 != 0) {
-#pragma unroll
-        for (int u = 0; u < CG; ++u)
-#pragma unroll
-            for (int n = 0; n < 8; ++n)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) acc[u][n][r] *= v_scale;
-    }
-    // acc[u] rows 4 q4 + r = column (token 4u + q4, head r); its l sits in lane 4 q4 + r
-#pragma unroll
-    for (int u = 0; u < CG; ++u) {
-        float lr = l_run[u];
-        lr += __shfl_xor(lr, 16, 64);
-        lr += __shfl_xor(lr, 32, 64);
-        const int row = r0 + 4 * u + q4;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float inv = 1.0f / __shfl(lr, 4 * q4 + r, 64);
-            if (row < M) {
-#pragma unroll
-                for (int n = 0; n < 8; ++n)
-                    out[(int64_t)row * o_rs + (int64_t)(hq0 + r) * D + 16 * n + l16] = f2bf(rbf(acc[u][n][r] * inv));
-            }
-        }
-    }
-}
-
-constexpr int kPfMaxTiles = 256;  // 32-key tiles per sequence (max_seq <= 8192)
+constexpr int kPfMaxTiles = 1024;  // 32-key tiles per sequence (max_seq <= 32768; page ids in LDS)
 
 // Prefill attention on 32 x 32 bf16 matrix cores (k_attn_prefill_sdpa, the default for bf16 K/V):
 // block = one row group of kPrefillRowGroup = 32 consecutive rows of one slot x kv head g; wave w
@@ -1483,7 +1363,14 @@ __device__ __forceinline__ float swap32_sum(float v) {
 //   pass 2 (stages of one tile's K + V): the same S^T again, e = fexp_u20 / expf of (s - M_c) (the
 //     16-key vector part / the tail of the column's block), l += e, O^T += V^T . bf16(e)^T (one MFMA
 //     term per k-step: P is bf16, 24 instead of 32 MFMAs per tile).
-// Every stage is 16 KiB and four 1-KiB DMAs per wave, so the ring's vmcnt accounting is unchanged.
+// Every stage is 16 KiB and four 1-KiB DMAs per wave (bf16 K/V). One-byte K/V (KV8 = 1 e4m3, 2 int8;
+// kv_cache tile layouts with one byte per element): the same stages at half the bytes (two 1-KiB
+// DMAs per wave), every K / V^T fragment 8 codes widened to bf16 in registers exactly as the decode
+// kernels do (KvFrag<KV8>); the K scale is folded into `scale`, the V scale multiplies the output
+// (k_attn_sdpa_mfma's arithmetic), so a prompt and its decode steps share the SDPA semantics.
+// F64: q.k as eight zero-C 16-product MFMA partials summed in f64 in both passes (study: 109 vs 307
+// of 911360 outputs off the oracle, +30 % kernel time; round 5).
+template <int KV8, bool F64>
 __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __restrict__ q, int64_t q_rs,
                                                               const uint16_t* __restrict__ K,
                                                               const uint16_t* __restrict__ Vt, int64_t kv_sb,
@@ -1491,9 +1378,13 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
                                                               const int32_t* __restrict__ row_slot, int M,
                                                               float scale, const int32_t* __restrict__ pt, int pps,
                                                               int npages, int64_t kv_pgs, uint16_t* __restrict__ out,
-                                                              int64_t o_rs, int xchunk) {
+                                                              int64_t o_rs, int xchunk, float v_scale) {
     constexpr int D = 128, P = kFaStages;
     constexpr int kSlot = 16384;
+    constexpr int EB = KV8 ? 1 : 2;            // bytes per K / V element
+    constexpr int NDMA = 4 / EB;               // 1-KiB DMAs per wave per stage
+    constexpr int TB = 4096 * EB;              // bytes of one 32-key K or V tile
+    using KF = KvFrag<KV8>;
     __shared__ __attribute__((aligned(16))) uint8_t ring[P * kSlot];
     __shared__ int s_page[kPfMaxTiles];
     const int nrb = M / 32;
@@ -1525,8 +1416,9 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
     for (int s2 = 0; s2 < 8; ++s2) asm volatile("" : "+v"(qf[s2]));
     const int ntiles = (lim_b + 31) >> 5;
     const int NB = (ntiles + 15) >> 4;
-    const uint16_t* Kg = K + (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;
-    const uint16_t* Vg = Vt + (pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh + lane * 8;
+    // (element offsets; one-byte caches index bytes, as the decode kernels)
+    const uint8_t* Kg = reinterpret_cast<const uint8_t*>(K) + ((pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh) * EB + lane * 16;
+    const uint8_t* Vg = reinterpret_cast<const uint8_t*>(Vt) + ((pt ? 0 : (int64_t)slot * kv_sb) + g * kv_sh) * EB + lane * 16;
     if (pt) {
         for (int t = threadIdx.x; t < ntiles; t += 256) s_page[t] = min(max(pt[(int64_t)slot * pps + t], 0), npages - 1);
         __syncthreads();
@@ -1551,18 +1443,19 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
     auto issue = [=](int i) __attribute__((always_inline)) {
         int cb, pass, ta, tb;
         stage_of(i, cb, pass, ta, tb);
-        const int64_t ba = pt ? (int64_t)s_page[ta] * kv_pgs : (int64_t)ta * 4096;
-        const int64_t bb = pt ? (int64_t)s_page[tb] * kv_pgs : (int64_t)tb * 4096;
+        const int64_t ba = (pt ? (int64_t)s_page[ta] * kv_pgs : (int64_t)ta * 4096) * EB;
+        const int64_t bb = (pt ? (int64_t)s_page[tb] * kv_pgs : (int64_t)tb * 4096) * EB;
         uint8_t* st = ring + (i % P) * kSlot;
-        const uint16_t* second = pass == 1 ? Kg + bb : Vg + bb;
+        const uint8_t* second = pass == 1 ? Kg + bb : Vg + bb;
+        constexpr int HALF = 4 * NDMA;  // KiB of the stage's first tile
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-            const int j = wave * 4 + jj;
-            glds16_asm(j < 8 ? Kg + ba + j * 512 : second + (j - 8) * 512, st + j * 1024);
+        for (int jj = 0; jj < NDMA; ++jj) {
+            const int j = wave * NDMA + jj;
+            glds16_asm(j < HALF ? Kg + ba + j * 1024 : second + (j - HALF) * 1024, st + j * 1024);
         }
     };
     const int o = (c & ~12) | ((c & 4) << 1) | ((c & 8) >> 1);
-    const int koff = ((((o >> 2) & 1) * 16 + h) * 16 + 4 * (o >> 3) + (o & 3)) * 16;
+    const int koff = ((((o >> 2) & 1) * 16 + h) * 16 + 4 * (o >> 3) + (o & 3)) * 8 * EB;
     // S^T of one tile, raw dots (unscaled): two 64-dim MFMA accumulator chains and one fp32 add.
     // Measured against the oracle on the same caches (tests/test_gpu_configs.py
     // test_prefill_attention_vs_oracle_sdpa; 2 x 2048 rows, 911360 sampled outputs): these chains
@@ -1573,19 +1466,36 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
     // each 8-product group to its largest product and truncate (tools/ubench/mfma_round.hip), and
     // every fp32 partial sum rounds; the block max M_c enters every probability (l is summed from
     // the unrounded e, P.V from the rounded P), so pass 1 needs the precision as much as pass 2.
+    auto kfrag = [=](const uint8_t* p) __attribute__((always_inline)) {  // 8 keys' or dims' bf16 values
+        if constexpr (KV8) return KF::bf(*reinterpret_cast<const uint2*>(p));
+        else return *reinterpret_cast<const uint4*>(p);
+    };
     auto qk = [=](const uint8_t* st, float (&x)[16]) __attribute__((always_inline)) {
         uint4 kf[8];
 #pragma unroll
-        for (int s2 = 0; s2 < 8; ++s2) kf[s2] = *reinterpret_cast<const uint4*>(st + koff + s2 * 512);
-        v16f_t a0 = {}, a1 = {};
+        for (int s2 = 0; s2 < 8; ++s2) kf[s2] = kfrag(st + koff + s2 * 256 * EB);
+        if constexpr (F64) {
+            double dd[16];
 #pragma unroll
-        for (int s2 = 0; s2 < 8; s2 += 2) {
-            a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf_t, kf[s2]), qf[s2], a0, 0, 0, 0);
-            a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf_t, kf[s2 + 1]), qf[s2 + 1], a1, 0, 0, 0);
+            for (int s2 = 0; s2 < 8; ++s2) {
+                const v16f_t pr = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf_t, kf[s2]), qf[s2],
+                                                                          v16f_t{}, 0, 0, 0);
+#pragma unroll
+                for (int e = 0; e < 16; ++e) dd[e] = s2 ? dd[e] + (double)pr[e] : (double)pr[e];
+            }
+#pragma unroll
+            for (int e = 0; e < 16; ++e) x[e] = (float)dd[e];
+        } else {
+            v16f_t a0 = {}, a1 = {};
+#pragma unroll
+            for (int s2 = 0; s2 < 8; s2 += 2) {
+                a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf_t, kf[s2]), qf[s2], a0, 0, 0, 0);
+                a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf_t, kf[s2 + 1]), qf[s2 + 1], a1, 0, 0, 0);
+            }
+            const v16f_t t = a0 + a1;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) x[e] = t[e];
         }
-        const v16f_t t = a0 + a1;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) x[e] = t[e];
     };
     float m_run = -INFINITY, l_run = 0.f, bmax = -INFINITY;
     int vmin = 0;
@@ -1601,7 +1511,11 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
     auto wait_through = [=](int i, int last_issued) __attribute__((always_inline)) {
         const int pending = min(nstages - 1, last_issued) - i;
         if (pending <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if (pending == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if (NDMA == 2) {
+            if (pending == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            else if (pending == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else if (pending == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else if (pending == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -1653,13 +1567,19 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
             const uint8_t* st = ring + (i % P) * kSlot;
             const int bs = 32 * (16 * cb + jj);
             if (bs >= lim_b) continue;  // wave-uniform (the block's tiles past the group's last row)
-                uint4 vv[4][2];  // V^T fragments (dim 32 mt + c, keys 16 s + 8 h + 0..7): issued first
+                // V^T fragments (dim 32 mt + c, keys 16 s + 8 h + 0..7): issued first (one-byte caches:
+                // the raw codes, masked and widened at their MFMA)
+                uint4 vv[4][2];
+                uint2 vc[KV8 ? 4 : 1][KV8 ? 2 : 1];
     #pragma unroll
                 for (int mt = 0; mt < 4; ++mt) {
                     const int d = 32 * mt + c, n = d >> 4, l = d & 15;
     #pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2)
-                        vv[mt][s2] = *reinterpret_cast<const uint4*>(st + 8192 + ((n * 4 + 2 * s2 + h) * 16 + l) * 16);
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        const uint8_t* vp = st + TB + ((n * 4 + 2 * s2 + h) * 16 + l) * 8 * EB;
+                        if constexpr (KV8) vc[mt][s2] = *reinterpret_cast<const uint2*>(vp);
+                        else vv[mt][s2] = *reinterpret_cast<const uint4*>(vp);
+                    }
                 }
                 float x[16];
                 qk(st, x);
@@ -1706,13 +1626,18 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
                 for (int mt = 0; mt < 4; ++mt) {
     #pragma unroll
                     for (int s2 = 0; s2 < 2; ++s2) {
-                        uint4 a = vv[mt][s2];
-                        if (vtail) {
-                            const int k0 = 16 * s2;
-                            a.x &= (k0 < limv ? 0xffffu : 0u) | (k0 + 1 < limv ? 0xffff0000u : 0u);
-                            a.y &= (k0 + 2 < limv ? 0xffffu : 0u) | (k0 + 3 < limv ? 0xffff0000u : 0u);
-                            a.z &= (k0 + 4 < limv ? 0xffffu : 0u) | (k0 + 5 < limv ? 0xffff0000u : 0u);
-                            a.w &= (k0 + 6 < limv ? 0xffffu : 0u) | (k0 + 7 < limv ? 0xffff0000u : 0u);
+                        uint4 a;
+                        if constexpr (KV8) {
+                            a = KF::bf(vtail ? KF::mask(vc[mt][s2], limv - 16 * s2) : vc[mt][s2]);
+                        } else {
+                            a = vv[mt][s2];
+                            if (vtail) {
+                                const int k0 = 16 * s2;
+                                a.x &= (k0 < limv ? 0xffffu : 0u) | (k0 + 1 < limv ? 0xffff0000u : 0u);
+                                a.y &= (k0 + 2 < limv ? 0xffffu : 0u) | (k0 + 3 < limv ? 0xffff0000u : 0u);
+                                a.z &= (k0 + 4 < limv ? 0xffffu : 0u) | (k0 + 5 < limv ? 0xffff0000u : 0u);
+                                a.w &= (k0 + 6 < limv ? 0xffffu : 0u) | (k0 + 7 < limv ? 0xffff0000u : 0u);
+                            }
                         }
                         oacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf_t, a), s2 ? pb1 : pb0,
                                                                            oacc[mt], 0, 0, 0);
@@ -1722,6 +1647,12 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
         }
     }
     const float inv = 1.0f / swap32_sum(l_run);
+    if constexpr (KV8 != 0) {  // the V scale on the unnormalised sums, then 1 / l (k_attn_sdpa_mfma's order)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) oacc[mt][e] *= v_scale;
+    }
     if (qrow < M) {
         uint16_t* orow = out + (int64_t)qrow * o_rs + (int64_t)(hq0 + (c & 3)) * D;
 #pragma unroll
@@ -1741,34 +1672,36 @@ int prefill_attention_check(int Hq, int Hkv, int pps) {
         set_error("prefill_attention: GQA group %d != 4 not supported", Hq / Hkv);
         return WF_EINVAL;
     }
+    if (pps > kPfMaxTiles) {
+        set_error("prefill_attention: max_seq %d > %d keys", 32 * pps, 32 * kPfMaxTiles);
+        return WF_EINVAL;
+    }
     return WF_OK;
 }
 
-// bf16 K/V: the 32 x 32 matrix-core kernel k_attn_prefill_sdpa, its blocks in XCD-chunked
-// order when the items split evenly over the 8 XCDs (each XCD streams one (slot, kv head) K/V at a
-// time from its own L2: 333 -> 250 us per layer at 8 x 2048); FP8 K/V, or a bf16 cache longer than
-// kPfMaxTiles tiles: the row-split register kernel k_attn_prefill ("Causal attention").
+// k_attn_prefill_sdpa for every K/V element type (bf16, e4m3, int8), its blocks in XCD-chunked order
+// when the items split evenly over the 8 XCDs (each XCD streams one (slot, kv head) K/V at a time
+// from its own L2: 333 -> 250 us per layer at 8 x 2048). Rows come in aligned groups of 32 of one slot
+// (wf_model_prefill checks M % kPrefillRowGroup == 0).
+#ifndef WF_PF_QK_F64  // study: q.k partials in f64 in both passes (+30 % kernel time, round 5)
+#define WF_PF_QK_F64 0
+#endif
 int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                       int64_t kv_sh, int Hq, int Hkv, const int32_t* row_pos, const int32_t* row_slot, int M,
                       float sm_scale, const int32_t* pt, int pps, int npages, int64_t kv_pgs, uint16_t* out,
                       int64_t o_rs, hipStream_t st, int kv8, float k_scale, float v_scale) {
     if (int rc = prefill_attention_check(Hq, Hkv, pps)) return rc;
-    if (!kv8 && pps <= kPfMaxTiles && M % 32 == 0) {
-        const int items = (M / 32) * Hkv, xchunk = items % 8 == 0 ? items / 8 : 0;
-        const dim3 grid = xchunk ? dim3(items) : dim3(M / 32, Hkv);
-        hipLaunchKernelGGL(k_attn_prefill_sdpa, grid, dim3(256), 0, st, q, q_rs, k, v, kv_sb, kv_sh, row_pos, row_slot, M,
-                           sm_scale, pt, pps, npages, kv_pgs, out, o_rs, xchunk);
-    } else if (kv8 == 2)
-        hipLaunchKernelGGL((k_attn_prefill<1, 2, 2>), dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v, kv_sb,
-                           kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale * k_scale, pt, pps, npages, kv_pgs, out, o_rs,
-                           v_scale);
-    else if (kv8)
-        hipLaunchKernelGGL((k_attn_prefill<1, 2, 1>), dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v, kv_sb,
-                           kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale * k_scale, pt, pps, npages, kv_pgs, out, o_rs,
-                           v_scale);
-    else
-        hipLaunchKernelGGL((k_attn_prefill<1, 2>), dim3((M + 15) / 16, Hkv), dim3(256), 0, st, q, q_rs, k, v, kv_sb,
-                           kv_sh, Hq, Hkv, row_pos, row_slot, M, sm_scale, pt, pps, npages, kv_pgs, out, o_rs, 1.0f);
+    if (M % 32 != 0) {
+        set_error("prefill_attention: rows %d not a multiple of 32", M);
+        return WF_EINVAL;
+    }
+    constexpr bool F = WF_PF_QK_F64;
+    const int items = (M / 32) * Hkv, xchunk = items % 8 == 0 ? items / 8 : 0;
+    const dim3 grid = xchunk ? dim3(items) : dim3(M / 32, Hkv);
+    auto kern = kv8 == 2 ? k_attn_prefill_sdpa<2, F> : kv8 == 1 ? k_attn_prefill_sdpa<1, F> : k_attn_prefill_sdpa<0, F>;
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, q, q_rs, k, v, kv_sb, kv_sh, row_pos, row_slot, M,
+                       kv8 ? sm_scale * k_scale : sm_scale, pt, pps, npages, kv_pgs, out, o_rs, xchunk,
+                       kv8 ? v_scale : 1.0f);
     return check_launch("prefill_attention");
 }
 
@@ -1808,7 +1741,7 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
         if (!caps[gi]) {
             int dev = 0, ncu = 0, per = 0;
             if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 256, 0) != hipSuccess) {
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kSdpaThreads, 0) != hipSuccess) {
                 set_error("decode_attention_partials: occupancy query failed");
                 return WF_EHIP;
             }
@@ -1821,7 +1754,7 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
         }
         const int chunk = std::max(1, caps[gi] / per_seq);
         for (int b0 = 0; b0 < B; b0 += chunk) {
-            hipLaunchKernelGGL(kern, dim3(NS, Hkv, std::min(chunk, B - b0)), dim3(256), 0, st, q, q_sb, k, v, kv_sb, kv_sh,
+            hipLaunchKernelGGL(kern, dim3(NS, Hkv, std::min(chunk, B - b0)), dim3(kSdpaThreads), 0, st, q, q_sb, k, v, kv_sb, kv_sh,
                                S, seq_lens, sm_scale, b0, NS, sb->xg, sb->rec, sb->epoch, merged_row, sb->err, sb->stall);
             if (int rc = check_launch("decode_attention_partials")) return rc;
         }

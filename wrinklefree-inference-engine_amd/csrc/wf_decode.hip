@@ -2721,7 +2721,7 @@ int wf_model_attn_view(const wf_model* m, wf_attn_records* out) {
 // ---------------------------------------------------------------------------------------------
 // Prefill: the prompt tokens of any KV slots as GEMM rows (BASELINE configs[2]). Per layer:
 // row norm + quantize (tile order) -> fused prefill GEMM (k_pgemm_fused) for QKV (+ RoPE, K/V
-// rows written into each token's slot / position), causal attention (k_attn_prefill), row norm ->
+// rows written into each token's slot / position), causal attention (k_attn_prefill_sdpa), row norm ->
 // O (+ residual), row norm -> gate|up (ReLU^2 * up), row norm -> down (+ residual). The float
 // sequence per token is the decode step's (same epilogues, same row norm); attention sums over the
 // whole prefix in one pass instead of the decode step's 8 merged splits.
