@@ -257,10 +257,14 @@ enum {
 int wf_model_launch_op(wf_model* m, int layer, int op, void* stream);
 /* Read-only view of the step's attention hand-off, for kernel-level checks (tests/, profiling):
  * after WF_OP_QKV and WF_OP_ATTN of a layer, q holds that layer's query rows after RoPE
- * ([batch, n_heads * head_dim] bf16) and attn_row the bf16 attention output [batch, n_heads *
- * head_dim] the O projection reads, on every path. records = 0: no path exposes split partials
- * (part_ml / part_o are the model's scratch). Device pointers owned by the model; valid until
- * wf_model_destroy. */
+ * ([batch, n_heads * head_dim] bf16) and the partial records of the split attention: per
+ * (sequence b, query head h, record s < records), part_ml[2 ((b n_heads + h) records + s) + {0, 1}] =
+ * (running max m, sum l) and the unnormalised output o[d] at part_o[((b n_heads + h) records + s) *
+ * 128 + ((d >> 2) & 1) * 64 + (d >> 3) * 4 + (d & 3)] (head_dim 128). Batch < 16 and untiled caches:
+ * records in one frame (m = 0; the reference's SDPA semantics), which each head's last attention
+ * block sums into attn_row. Batch >= 16 on tile-layout caches: no records (records = 0). attn_row is
+ * the bf16 attention output [batch, n_heads * head_dim] the O projection reads, on every path. Device
+ * pointers owned by the model; valid until wf_model_destroy. */
 typedef struct {
     const uint16_t* q;
     const float* part_ml;

@@ -316,8 +316,22 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
 }
 
 // ---------------------------------------------------------------------------------------------
-// Decode-step attention shared constants and the K/V load form.
+// Decode-step attention shared constants: k_attn_sdpa's block size and keys per lane group per chunk,
+// and the K/V load form.
 // ---------------------------------------------------------------------------------------------
+#ifndef WF_AP_THREADS  // study builds only (tools/build_variant.sh): threads per block
+#define WF_AP_THREADS 256
+#endif
+constexpr int kAttnPartThreads = WF_AP_THREADS;
+// keys per lane group per chunk (chunk = 16 U keys at 256 threads): a split that one 160-key chunk
+// covers (contexts <= 1280 at 8 splits) takes U = 10 -- one load round; longer splits the
+// double-buffered 128-key chunks (same-box, batch 1: U 10 vs 8 at ctx 1024 attention 5.59 -> 4.85 us,
+// 1080 -> 1104 tok/s; at ctx 4000 U 10 alone lost 10.3 -> 11.3 us). -DWF_AP_U=n: one U everywhere.
+#ifdef WF_AP_U
+constexpr int kApUShort = WF_AP_U, kApULong = WF_AP_U;
+#else
+constexpr int kApUShort = 10, kApULong = 8;
+#endif
 #ifndef WF_KV_NT  // decode-attention K/V loads with the non-temporal hint (each byte is read once per step)
 #define WF_KV_NT 1
 #endif
@@ -325,6 +339,9 @@ __device__ __forceinline__ uint4 kv_ld16(const uint16_t* p) {
     if constexpr (WF_KV_NT) return ldg_nt(reinterpret_cast<const uint8_t*>(p));
     else return *reinterpret_cast<const uint4*>(p);
 }
+#ifndef WF_KV_NT_B1  // study: 1 = the hint in the batch < 16 attention too (5.8 -> 6.4 us there: not kept)
+#define WF_KV_NT_B1 0
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // The reference's attention AS IT RUNS (scripts/direct_inference_full.py:241: torch 2.10's CPU
@@ -334,39 +351,44 @@ __device__ __forceinline__ uint4 kv_ld16(const uint16_t* p) {
 // tail, P = bf16(e) into P.V, the UNROUNDED e into the row sum, blocks combined by
 // r_c = expf(M_{c-1} - M_c), out = bf16(dst * (1 / sum)).
 //
-// Decode step, batch < 16 and untiled caches (k_attn_sdpa, round 6): block = (split s, kv head g,
-// sequence b) with ALL the G query heads of the group, so every K / V byte is loaded by one CU once
-// (round 5 gave each query head its own block: 4x the per-CU load volume, 160 of 256 CUs busy). NS
-// splits per (sequence, kv head) (sdpa_splits: ~240 blocks at batch 1), T = round_up(ceil(S / NS), 16)
-// keys each, read by 16-lane groups (8 dims per lane, a wave reads 4 contiguous 256-byte rows), the
-// nact = ceil(S / T) splits that hold keys taking part. Three phases:
-//   1. q.k of the split's keys for the G heads (products exact, summed in f64 and rounded once:
-//      torch's oneDNN GEMM is that close to exact, tests/golden/sdpa_probe.py), the split's
-//      per-(head, 512-key block) maxima published as epoch-tagged 8-byte granules (<= 3 blocks per
-//      split); wave w polls head w's granules of every split of the group (MI355X_MICROARCH.md
-//      handoff-1to1: data-tagged granules, no counter round trip) and folds them into M_c, r_c and
-//      the suffix products R;
-//   2. P and e of the split's keys, scaled by the product of the r's after the key's block, l and o
-//      per head: one record (l, o[128]) per head in the frame of the sequence's last block;
-//   3. the records published as granules (every value with the launch's tag), and the group's G x 128
-//      outputs divided among the nact blocks: each polls its slice of every split's record, sums the
-//      records in split order and writes out = bf16(O * (1 / L)) into the bf16 attention row the O
-//      projection reads. A split that holds the whole context (nact = 1) writes the row directly.
-// No ticket, no counter: a block's only waits are its two polls, each ending one hand-off after the
-// last sibling published. Tags: every block keeps its own launch count (epoch word, read and
-// re-stored by its first lane), so all blocks of a launch agree on the tag without communicating;
-// granules of earlier launches carry smaller tags. Residency: every active split of a group polls
-// its siblings; the host launches at most half the resident block count (occupancy API) per launch
-// (whole sequences) and the polls are bounded: on a timeout the kernel raises the model's
-// host-visible error word (wf_model_check / the next wf_model_step report it) and writes NaN.
+// Decode step, batch < 16 and untiled caches: block (split s, query head, sequence), kAttnPartSplits1
+// splits of T = round_up(ceil(S / NS), 16) keys read by 16-lane groups (8 dims per lane, a wave
+// reads 4 contiguous 256-byte key rows), in two phases around an in-launch exchange of the 512-key
+// block maxima:
+//   1. q.k of the split's keys (products exact in fp32, summed in f64 and rounded once -- torch's
+//      oneDNN GEMM is that close to exact, tests/golden/sdpa_probe.py), the split's per-block maxima
+//      published as epoch-tagged granules; wave 0 polls the head's granules (all NS splits);
+//   2. wave 0 folds the NS x 3 published maxima into M_c, r_c and the suffix products R, every
+//      lane forms P and e of its keys, scales by the product of the r's after the key's block
+//      (1.0 exactly inside the split's last block), and accumulates l = sum e and o = sum P v.
+// Every record (m = 0, l, o) is then in the frame of the head's last block; the head's last block
+// (merge ticket) sums the NS records and writes out = bf16(O * (1 / L)) into the bf16 attention row,
+// resets the ticket and stores this launch's tag as the head's epoch word (the next launch's tag is
+// that + 1). Merging in the O projection's input stage instead (round 5, same box): attention 10.4
+// -> 9.0 us, O 4.4 -> 6.0 us per layer (every O block reads all 83 KB of records), 1019 -> 1011
+// tok/s. Pipelined polls (four in flight, 256 clocks apart) did not shorten the exchange (2.2 ->
+// 2.6 us).
+// Residency: every split of a head must be resident while its siblings poll: the host launches
+// at most kSdpaMaxBlocks blocks per launch (B = 1: 160), below the chip's resident count.
 // ---------------------------------------------------------------------------------------------
-constexpr int kSdpaOneT = 64;  // splits of <= 64 keys: one load round (4 keys per lane group)
-#ifndef WF_SDPA_SPIN  // poll bound (iterations of an sc1 load round trip + s_sleep): ~0.2-0.5 s
-#define WF_SDPA_SPIN (1 << 18)
+#ifndef WF_SDPA_SLEEP
+#define WF_SDPA_SLEEP 1
 #endif
-__host__ __device__ __forceinline__ int sdpa_T(int Sb, int NS) { return ((Sb + NS - 1) / NS + 15) / 16 * 16; }
-
-// a poll bound was hit: raise the model's host-visible error word (WF_ATTN_ERR_*)
+#ifndef WF_SDPA_WPE
+#define WF_SDPA_WPE
+#endif
+// (measured, not kept: all splits of a head on one XCD with L2 polls -- the dispatcher does deal
+// block b to XCD b % 8 (tools/ubench/xcd_map.hip), but no load without sc1 ever saw a granule another
+// CU stored, whatever the store's policy bits, and an sc1 hand-off takes 0.6 us on one XCD and across
+// two alike (tools/ubench/handoff.hip): the exchange's ~2.2 us is the siblings' QK skew (~0.9 us)
+// plus that hand-off, not the distance)
+constexpr int kSdpaMaxT = 1024;      // split length bound (max_seq <= 8192): a split spans <= 3 blocks
+constexpr int kSdpaMaxSeq = kAttnPartSplits1 * kSdpaMaxT;
+#ifndef WF_SDPA_SPIN  // poll bound (iterations of an sc1 load round trip + s_sleep): ~0.3-1 s, never in a valid launch
+#define WF_SDPA_SPIN (1 << 20)
+#endif
+// a poll bound was hit (a sibling workgroup never became resident): raise the model's host-visible
+// error word (WF_ATTN_ERR_*; wf_model_check and the next wf_model_step report it)
 __device__ __forceinline__ void attn_fail(unsigned* err, unsigned code) {
     if (err) __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -420,275 +442,183 @@ __device__ __forceinline__ double group16_sum_d(double v) {
     v += dpp_d<DPP_MIRROR>(v);
     return v;
 }
-// lane l and l ^ 16 / l ^ 32 combined (v_permlane16/32_swap: rows 2i, 2i+1 / halves exchanged); both
-// lanes of a pair get the same bits
-__device__ __forceinline__ float pl16_sum(float v) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ float pl32_sum(float v) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ float pl_max4(float v) {  // max over the wave's four 16-lane groups
-    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-    r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
 
-// q.k of one key for the G heads (k: this lane's 8 dims as bf16): the 128 products are exact in
-// f64, summed per lane in dim order and across the 16 lanes by the DPP tree, rounded to fp32 once,
-// then scaled (the round-5 kernel's arithmetic bit for bit). G <= 4 keeps q in f64 (one fma per
-// product); G = 8 multiplies in fp32 (exact for bf16 x bf16) and adds in f64.
-template <int G, bool QD>
-__device__ __forceinline__ void sdpa_score(const double (&qd)[QD ? G : 1][8], const uint4 (&qr)[QD ? 1 : G], uint4 kr,
-                                           float sm_scale, float (&sv)[G]) {
-    const uint32_t w[4] = {kr.x, kr.y, kr.z, kr.w};
-    if constexpr (QD) {
-        double kd[8];
+// k_attn_sdpa's per-chunk steps as plain functions: lambdas capturing the kernel's locals by reference
+// left their closure objects (pointers to the locals) in scratch
+template <int U>
+__device__ __forceinline__ void sdpa_load(uint4 (&r)[U], const uint16_t* __restrict__ base, int64_t kvb, int c0, int gid,
+                                          int t1) {
+    constexpr int NG = kAttnPartThreads / 16;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { kd[2 * i] = (double)bf_lo(w[i]); kd[2 * i + 1] = (double)bf_hi(w[i]); }
+    for (int u = 0; u < U; ++u) {
+        const int t = min(c0 + gid + NG * u, max(t1 - 1, 0));
+        r[u] = *reinterpret_cast<const uint4*>(base + kvb + (int64_t)t * 128);
+    }
+}
+// q.k of the chunk's keys (products exact in fp32, summed in f64, rounded once), the split's per-block
+// maxima; the scores into sc (one-chunk splits) or the LDS score buffer
+template <int U, bool ONE>
+__device__ __forceinline__ void sdpa_scores(const uint4 (&kr)[U], const uint32_t (&qw)[4], int c0, int gid, int li, int t0,
+                                            int t1, int cb0, float sm_scale, float (&mx)[3], float (&sc)[ONE ? U : 1],
+                                            float* sc_lds) {
+    constexpr int NG = kAttnPartThreads / 16;
 #pragma unroll
-        for (int h = 0; h < G; ++h) {
-            double a = qd[h][0] * kd[0];
+    for (int u = 0; u < U; ++u) {
+        const uint32_t w[4] = {kr[u].x, kr[u].y, kr[u].z, kr[u].w};
+        double dd = 0.0;
 #pragma unroll
-            for (int j = 1; j < 8; ++j) a = fma(qd[h][j], kd[j], a);
-            sv[h] = (float)group16_sum_d(a) * sm_scale;
+        for (int i = 0; i < 4; ++i) {
+            dd += (double)(bf_lo(qw[i]) * bf_lo(w[i]));  // bf16 x bf16: exact in fp32
+            dd += (double)(bf_hi(qw[i]) * bf_hi(w[i]));
         }
-    } else {
+        const float sv = (float)group16_sum_d(dd) * sm_scale;
+        const int t = c0 + gid + NG * u;
+        const bool valid = t < t1;
+        const bool in0 = t < 512 * (cb0 + 1), in1 = t < 512 * (cb0 + 2);
+        mx[0] = (valid && in0) ? fmaxf(mx[0], sv) : mx[0];
+        mx[1] = (valid && !in0 && in1) ? fmaxf(mx[1], sv) : mx[1];
+        mx[2] = (valid && !in1) ? fmaxf(mx[2], sv) : mx[2];
+        if constexpr (ONE) sc[u] = sv;
+        else if (valid && li == 0) sc_lds[t - t0] = sv;
+    }
+}
+// probabilities of the chunk's keys and their P.V: e = fexp_u20 / expf of (s - M_c) (vector part /
+// tail of the key's 512-key block), l += e R, o += bf16(e) R v, R = the product of the block
+// rescale factors between the key's block and the split's last one (1.0 in the last block)
+// (the six block values by value: a struct passed by reference became a private array that the
+// per-key selects indexed, in scratch -- or, under an occupancy attribute, in LDS, which stretched
+// the launch's block dispatch over ~9 us)
+template <int U, bool ONE>
+__device__ __forceinline__ void sdpa_pv(const uint4 (&vr)[U], const float (&sc)[ONE ? U : 1], const float* sc_lds, int c0,
+                                        int gid, int t0, int t1, int cb0, int Sb, float bm0, float bm1, float bm2,
+                                        float br0, float br1, float br2, float& l, float (&o)[8]) {
+    constexpr int NG = kAttnPartThreads / 16;
 #pragma unroll
-        for (int h = 0; h < G; ++h) {
-            const uint32_t qw[4] = {qr[h].x, qr[h].y, qr[h].z, qr[h].w};
-            double a = 0.0;
+    for (int u = 0; u < U; ++u) {
+        const int t = c0 + gid + NG * u;
+        if (t < t1) {
+            float sv;
+            if constexpr (ONE) sv = sc[u];
+            else sv = sc_lds[t - t0];
+            const bool in0 = t < 512 * (cb0 + 1), in1 = t < 512 * (cb0 + 2);
+            const float Mc = in0 ? bm0 : (in1 ? bm1 : bm2);
+            const float Rc = in0 ? br0 : (in1 ? br1 : br2);
+            const int blk0 = t & ~511;
+            const int vbnd = min(512, Sb - blk0) & ~15;  // the 16-wide vector part of the block
+            const float x = sv - Mc;
+            const float e = ((t - blk0) < vbnd) ? fexp_u20(x) : expf_rn(x);
+            const float p = rbf(e) * Rc;
+            l = fmaf(e, Rc, l);
+            const uint32_t w[4] = {vr[u].x, vr[u].y, vr[u].z, vr[u].w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                a += (double)(bf_lo(qw[i]) * bf_lo(w[i]));
-                a += (double)(bf_hi(qw[i]) * bf_hi(w[i]));
+                o[2 * i] = fmaf(p, bf_lo(w[i]), o[2 * i]);
+                o[2 * i + 1] = fmaf(p, bf_hi(w[i]), o[2 * i + 1]);
             }
-            sv[h] = (float)group16_sum_d(a) * sm_scale;
         }
     }
 }
-// the maxima of the split's 512-key blocks (cb0 .. cb0 + 2) per head, for key t
-template <int G>
-__device__ __forceinline__ void sdpa_max(const float (&sv)[G], int t, int t1, int cb0, float (&mx)[G][3]) {
-    const bool valid = t < t1;
-    const int jj = (t >> 9) - cb0;
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-        mx[h][0] = (valid && jj == 0) ? fmaxf(mx[h][0], sv[h]) : mx[h][0];
-        mx[h][1] = (valid && jj == 1) ? fmaxf(mx[h][1], sv[h]) : mx[h][1];
-        mx[h][2] = (valid && jj == 2) ? fmaxf(mx[h][2], sv[h]) : mx[h][2];
-    }
-}
-// probabilities of key t and its P.V for the G heads (Mc / Rc: the maximum and suffix rescale
-// product of the key's 512-key block, uniform): e = fexp_u20 / expf of (s - M_c) (vector part / tail
-// of the block), l += e R, o += bf16(e) R v
-template <int G>
-__device__ __forceinline__ void sdpa_pv_blk(const float (&sv)[G], const float (&vx)[8], bool vec, const float (&Mc)[G],
-                                            const float (&Rc)[G], float (&l)[G], float (&o)[G][8]) {
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-        const float x = sv[h] - Mc[h];
-        const float e = vec ? fexp_u20(x) : expf_rn(x);
-        const float p = rbf(e) * Rc[h];
-        l[h] = fmaf(e, Rc[h], l[h]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[h][j] = fmaf(p, vx[j], o[h][j]);
-    }
-}
-// the key's block among the split's <= 3 (bm / br [block][head]) picked by a branch per block, so
-// every block's values are read with constant indices (a select chain on a runtime block index
-// became a private array in scratch)
-template <int G>
-__device__ __forceinline__ void sdpa_pv(const float (&sv)[G], uint4 vr, int t, int cb0, int Sb, const float (&bm)[3][G],
-                                        const float (&br)[3][G], float (&l)[G], float (&o)[G][8]) {
-    const int jj = (t >> 9) - cb0;
-    const int blk0 = t & ~511;
-    const bool vec = (t - blk0) < (min(512, Sb - blk0) & ~15);  // the 16-wide vector part of the block
-    const uint32_t w[4] = {vr.x, vr.y, vr.z, vr.w};
-    float vx[8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { vx[2 * i] = bf_lo(w[i]); vx[2 * i + 1] = bf_hi(w[i]); }
-    if (jj == 0) sdpa_pv_blk<G>(sv, vx, vec, bm[0], br[0], l, o);
-    else if (jj == 1) sdpa_pv_blk<G>(sv, vx, vec, bm[1], br[1], l, o);
-    else sdpa_pv_blk<G>(sv, vx, vec, bm[2], br[2], l, o);
-}
 
-template <int G, int NT, bool ONE>
-__device__ __forceinline__ unsigned attn_sdpa_body(const uint16_t* __restrict__ q, int64_t q_sb, const uint16_t* __restrict__ K,
-                                                   const uint16_t* __restrict__ V, int64_t kv_sb, int64_t kv_sh, int Hkv, int S,
-                                                   int b, int Sb, float sm_scale, int NS, unsigned* __restrict__ ew,
-                                                   int stall, uint64_t* __restrict__ xg, uint64_t* __restrict__ rec,
-                                                   uint16_t* __restrict__ row_out, unsigned* __restrict__ err) {
-    constexpr int D = 128, NWV = NT / 64, NG = NT / 16;  // waves, 16-lane key groups
-    constexpr int CH = 64, UC = CH / NG;                 // 64-key chunks: UC keys per lane group
-    constexpr bool QD = G <= 4;
-    constexpr int MP = (G * 64 + kSdpaNSMax + 63) / 64;  // merge: record pair granules per lane of the polling wave
-    constexpr int ML = (kSdpaNSMax * G + 63) / 64;       // merge: l granules per lane
-    const int s = blockIdx.x, g = blockIdx.y;
-    const int tid = threadIdx.x, gid = tid >> 4, li = tid & 15, wv = tid >> 6, lane = tid & 63;
-    const int64_t bg = (int64_t)b * Hkv + g;
-    const int T = sdpa_T(Sb, NS);
-    const int nact = (Sb + T - 1) / T;
+template <int U, bool ONE>
+__device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, int64_t q_sb, const uint16_t* __restrict__ K,
+                                               const uint16_t* __restrict__ V, int64_t kv_sb, int64_t kv_sh, int Hq,
+                                               int Hkv, int S, const int32_t* __restrict__ seq_lens, float sm_scale,
+                                               int b0, uint64_t* __restrict__ xg, float2* __restrict__ ml_out,
+                                               float* __restrict__ o_out, uint16_t* __restrict__ row_out,
+                                               unsigned* __restrict__ cnt, unsigned* __restrict__ xep, int s, int hq,
+                                               unsigned* __restrict__ err, int stall) {
+    constexpr int NS = kAttnPartSplits1, D = 128, LP = 16, NG = kAttnPartThreads / LP, CH = U * NG;
+    constexpr int NWV = kAttnPartThreads / 64;
+    const int b = b0 + (int)blockIdx.z;
+    const int g = hq / (Hq / Hkv);
+    const int gid = threadIdx.x / LP, li = threadIdx.x % LP, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int Sb = min(seq_lens[b], S);
+    const int T = ((Sb + NS - 1) / NS + 15) / 16 * 16;
     const int t0 = s * T, t1 = min(t0 + T, Sb);
-    const int cb0 = t0 >> 9, cb1 = (t1 - 1) >> 9;
-    __shared__ float red[NWV][G][3];
-    __shared__ float blk_m[G][3], blk_r[G][3], fin_r[G];
-    __shared__ __attribute__((aligned(16))) float sm_o[NWV][G][D];
-    __shared__ float sm_l[NWV][G];
-    __shared__ float sc_lds[ONE ? 1 : G][ONE ? 1 : kSdpaMaxT];
-    __shared__ __attribute__((aligned(16))) float mv[2 * (8 * 64 + kSdpaNSMax)];
-    __shared__ float mL[kSdpaNSMax * G];
-    __shared__ int sh_bad;
-
-    // ---- loads: this block's launch count (the tag; every lane, no branch, so no wait until it is
-    // used), K (and V) of the split's keys, q of the group's heads ----
-    const unsigned ep0 = ld_sc1(ew);
-    const int64_t kvb = b * kv_sb + g * kv_sh + li * 8;
-    const int tl = max(t1 - 1, 0);
-    uint4 kA[UC], vA[UC], kB[ONE ? 1 : UC], vB[ONE ? 1 : UC];
-#pragma unroll
-    for (int u = 0; u < UC; ++u)
-        if (u * NG < T) kA[u] = *reinterpret_cast<const uint4*>(K + kvb + (int64_t)min(t0 + gid + NG * u, tl) * D);
-    if constexpr (ONE) {
-#pragma unroll
-        for (int u = 0; u < UC; ++u)
-            if (u * NG < T) vA[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)min(t0 + gid + NG * u, tl) * D);
-    }
-    double qd[QD ? G : 1][8];
-    uint4 qr[QD ? 1 : G];
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-        const uint4 v = *reinterpret_cast<const uint4*>(q + b * q_sb + (int64_t)(g * G + h) * D + li * 8);
-        if constexpr (QD) {
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) { qd[h][2 * i] = (double)bf_lo(w[i]); qd[h][2 * i + 1] = (double)bf_hi(w[i]); }
-        } else {
-            qr[h] = v;
-        }
-    }
+    const int cb0 = t0 >> 9;
+    const int64_t bh = (int64_t)b * Hq + hq;
     WF_STAMP(0);
-    // ---- phase 1: scores and the split's block maxima ----
-    float mx[G][3];
-#pragma unroll
-    for (int h = 0; h < G; ++h) mx[h][0] = mx[h][1] = mx[h][2] = -INFINITY;
-    float sc[ONE ? UC : 1][G];
-    if constexpr (ONE) {
-#pragma unroll
-        for (int u = 0; u < UC; ++u)
-            if (u * NG < T) {
-                const int t = t0 + gid + NG * u;
-                sdpa_score<G, QD>(qd, qr, kA[u], sm_scale, sc[u]);
-                sdpa_max<G>(sc[u], t, t1, cb0, mx);
+    __shared__ float sc_lds[ONE ? 1 : kSdpaMaxT];
+    __shared__ float red[NWV][3];
+    __shared__ float blk_m[3], blk_r[3], fin_r;
+    __shared__ float sm_l[NWV];
+    __shared__ __attribute__((aligned(16))) float sm_o[NWV][D];
+    __shared__ int sh_last;
+
+    const int64_t kvb = b * kv_sb + g * kv_sh + li * 8;
+    const uint4 qv = *reinterpret_cast<const uint4*>(q + b * q_sb + (int64_t)hq * D + li * 8);
+    const uint32_t qw[4] = {qv.x, qv.y, qv.z, qv.w};
+    float mx[3] = {-INFINITY, -INFINITY, -INFINITY};  // per 512-key block of the split (<= 3)
+    float sc[ONE ? U : 1];
+    uint4 vA[U], vB[ONE ? 1 : U];
+    if (t0 < t1) {
+        uint4 kA[U];
+        sdpa_load<U>(kA, K, kvb, t0, gid, t1);
+        if constexpr (ONE) {
+            sdpa_load<U>(vA, V, kvb, t0, gid, t1);
+            sdpa_scores<U, ONE>(kA, qw, t0, gid, li, t0, t1, cb0, sm_scale, mx, sc, sc_lds);
+        } else {
+            uint4 kB[U];
+            for (int c0 = t0; c0 < t1; c0 += 2 * CH) {
+                if (c0 + CH < t1) sdpa_load<U>(kB, K, kvb, c0 + CH, gid, t1);
+                sdpa_scores<U, ONE>(kA, qw, c0, gid, li, t0, t1, cb0, sm_scale, mx, sc, sc_lds);
+                if (c0 + 2 * CH < t1) sdpa_load<U>(kA, K, kvb, c0 + 2 * CH, gid, t1);
+                if (c0 + CH < t1) sdpa_scores<U, ONE>(kB, qw, c0 + CH, gid, li, t0, t1, cb0, sm_scale, mx, sc, sc_lds);
             }
-    } else {
-        for (int c0 = t0; c0 < t1; c0 += 2 * CH) {  // two 64-key chunks per turn, the next one in flight
-            if (c0 + CH < t1) {
-#pragma unroll
-                for (int u = 0; u < UC; ++u)
-                    kB[u] = *reinterpret_cast<const uint4*>(K + kvb + (int64_t)min(c0 + CH + gid + NG * u, tl) * D);
-            }
-#pragma unroll
-            for (int u = 0; u < UC; ++u) {
-                const int t = c0 + gid + NG * u;
-                float sv[G];
-                sdpa_score<G, QD>(qd, qr, kA[u], sm_scale, sv);
-                sdpa_max<G>(sv, t, t1, cb0, mx);
-                if (li == 0 && t < t1) {
-#pragma unroll
-                    for (int h = 0; h < G; ++h) sc_lds[h][t - t0] = sv[h];
-                }
-            }
-            if (c0 + 2 * CH < t1) {
-#pragma unroll
-                for (int u = 0; u < UC; ++u)
-                    kA[u] = *reinterpret_cast<const uint4*>(K + kvb + (int64_t)min(c0 + 2 * CH + gid + NG * u, tl) * D);
-            }
-            if (c0 + CH < t1) {
-#pragma unroll
-                for (int u = 0; u < UC; ++u) {
-                    const int t = c0 + CH + gid + NG * u;
-                    float sv[G];
-                    sdpa_score<G, QD>(qd, qr, kB[u], sm_scale, sv);
-                    sdpa_max<G>(sv, t, t1, cb0, mx);
-                    if (li == 0 && t < t1) {
-#pragma unroll
-                        for (int h = 0; h < G; ++h) sc_lds[h][t - t0] = sv[h];
-                    }
-                }
-            }
-        }
-        // V chunks 0 and 1 in flight across the exchange
-#pragma unroll
-        for (int u = 0; u < UC; ++u) vA[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)min(t0 + gid + NG * u, tl) * D);
-        if (t0 + CH < t1) {
-#pragma unroll
-            for (int u = 0; u < UC; ++u)
-                vB[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)min(t0 + CH + gid + NG * u, tl) * D);
+            sdpa_load<U>(vA, V, kvb, t0, gid, t1);  // V chunks 0 and 1 in flight across the exchange
+            if (t0 + CH < t1) sdpa_load<U>(vB, V, kvb, t0 + CH, gid, t1);
         }
     }
+    WF_STAMP(1);
+    // ---- the exchange: per-block maxima of every split of this head ----
+    // Each split publishes one 8-byte granule {max, epoch} per 512-key block it covers (a split spans
+    // <= 3 blocks at T <= 1024) with an sc1 store; wave 0 polls the head's 3 NS granules with sc1
+    // loads until every tag is this launch's epoch (MI355X_MICROARCH.md handoff-1to1: data-tagged
+    // granules, no counter round trip). The epoch is the head's launch count, advanced by the
+    // head's merging block after every split has passed its poll.
 #pragma unroll
-    for (int h = 0; h < G; ++h)
+    for (int jj = 0; jj < 3; ++jj) {
+        const float w = wave_max(mx[jj]);
+        if (lane == 0) red[wv][jj] = w;
+    }
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(wv) == 0) {  // wave 0 (a scalar branch: no exec-masked loop)
+        const unsigned ep = ld_sc1(xep + bh * kTailLine) + 1u;  // this launch's tag
+        const unsigned want = stall ? ep + 1u : ep;  // test hook (wf_model_debug_stall_attention): a tag nobody stores
+        float bmx[3];  // the block's maxima (constant LDS indices: uniform scalars)
 #pragma unroll
         for (int jj = 0; jj < 3; ++jj) {
-            const float m4 = pl_max4(mx[h][jj]);
-            if (lane == 0) red[wv][h][jj] = m4;
+            bmx[jj] = red[0][jj];
+#pragma unroll
+            for (int w = 1; w < NWV; ++w) bmx[jj] = fmaxf(bmx[jj], red[w][jj]);
         }
-    // every wave has its launch count in hand before the barrier (readfirstlane waits for the load),
-    // so the word can be re-stored once this block is done with it (the caller, at the end)
-    const unsigned ep = (unsigned)__builtin_amdgcn_readfirstlane((int)ep0) + 1u;
-    __syncthreads();
-    WF_STAMP(1);
-    const unsigned want = stall ? ep + 1u : ep;  // test hook (wf_model_debug_stall_attention): a tag nobody stores
-    // ---- the exchange: publish this split's G x 3 block maxima, fold every split's ----
-    if (tid < 3 * G) {
-        const int h = tid / 3, jj = tid - 3 * h;
-        float m = red[0][h][jj];
-#pragma unroll
-        for (int w = 1; w < NWV; ++w) m = fmaxf(m, red[w][h][jj]);
-        st_sc1(xg + (bg * NS + s) * kSdpaXG + tid, ((uint64_t)ep << 32) | __float_as_uint(m));
-    }
-    for (int h = wv; h < G; h += NWV) {  // wave w: head w (and w + 4 at 4 waves)
-        const int n = 3 * nact;          // granules of head h: (split, block entry)
-        uint64_t gv[3] = {0, 0, 0};
-        bool bad = false;
-        for (int it = 0;; ++it) {  // every load of a pass issued before any is checked (clamped indices:
-            bool good = true;      // a load under a lane condition is waited for on the spot)
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                const int e = min(lane + 64 * i, n - 1), sp = e / 3;
-                gv[i] = ld_sc1(xg + (bg * NS + sp) * kSdpaXG + h * 3 + (e - 3 * sp));
-            }
-#pragma unroll
-            for (int i = 0; i < 3; ++i) good = good && (unsigned)(gv[i] >> 32) == want;
-            if (__all(good)) break;
-            if (it >= WF_SDPA_SPIN) {
-                bad = true;
+        if (lane < 3) {
+            const float m = lane == 0 ? bmx[0] : (lane == 1 ? bmx[1] : bmx[2]);
+            st_sc1(xg + (bh * NS + s) * 3 + lane, ((uint64_t)ep << 32) | __float_as_uint(m));
+        }
+        // lanes 0 .. 3 NS - 1: split lane / 3, block cb0(split) + lane % 3
+        const int sp = lane / 3, ent = lane - 3 * sp;
+        uint64_t gv = ((uint64_t)ep << 32) | 0xff800000u;  // lanes past the granules: -inf, tagged
+        int ok = 1;
+        for (int it = 0;; ++it) {
+            if (lane < 3 * NS) gv = ld_sc1(xg + bh * NS * 3 + lane);
+            if (__all((unsigned)(gv >> 32) == want)) break;
+            if (it > WF_SDPA_SPIN) {  // a missing sibling ends in NaN outputs and the error word, never a hang
+                ok = 0;
                 if (lane == 0) attn_fail(err, WF_ATTN_ERR_SDPA);
                 break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(WF_SDPA_SLEEP);
         }
-        float val[3];
-        int blk[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int e = lane + 64 * i, sp = e / 3;
-            blk[i] = e < n ? ((sp * T) >> 9) + (e - 3 * sp) : -1;
-            val[i] = __uint_as_float((uint32_t)gv[i]);
-        }
+        const float val = __uint_as_float((uint32_t)gv);
+        const int blk = lane < 3 * NS ? ((sp * T) >> 9) + ent : -1;
         const int NB = (Sb + 511) >> 9;
+        const int cb1 = max(t1 - 1, t0) >> 9;
         // prefix maxima, rescale factors and, for this split, the products of the factors after each
         // of its blocks up to its last one (blk_r) and after its last block (fin_r): uniform loop
         float M = -INFINITY, rr[3] = {1.f, 1.f, 1.f}, fin = 1.f;
         for (int c = 0; c < NB; ++c) {
-            float loc = -INFINITY;
-#pragma unroll
-            for (int i = 0; i < 3; ++i) loc = blk[i] == c ? fmaxf(loc, val[i]) : loc;
-            const float bmc = wave_max(loc);
+            const float bmc = wave_max((blk == c) ? val : -INFINITY);
             const float Mn = fmaxf(M, bmc);
             const float r = (c == 0) ? 1.f : expf_rn(M - Mn);
             M = Mn;
@@ -696,222 +626,127 @@ __device__ __forceinline__ unsigned attn_sdpa_body(const uint16_t* __restrict__ 
 #pragma unroll
             for (int jj = 0; jj < 3; ++jj)
                 if (c > cb0 + jj && c <= cb1) rr[jj] *= r;
-            if (lane == 0 && c >= cb0 && c < cb0 + 3) blk_m[h][c - cb0] = bad ? __uint_as_float(0x7fc00000u) : M;
+            if (lane == 0 && c >= cb0 && c < cb0 + 3) blk_m[c - cb0] = ok ? M : __uint_as_float(0x7fc00000u);
         }
         if (lane == 0) {
 #pragma unroll
-            for (int jj = 0; jj < 3; ++jj) blk_r[h][jj] = rr[jj];
-            fin_r[h] = fin;
+            for (int jj = 0; jj < 3; ++jj) blk_r[jj] = rr[jj];
+            fin_r = fin;
         }
     }
     __syncthreads();
     WF_STAMP(2);
-    // ---- phase 2: probabilities and P.V ----
-    // block-uniform values read once into scalar registers
-    float bm[3][G], br[3][G];
-#pragma unroll
-    for (int h = 0; h < G; ++h)
-#pragma unroll
-        for (int jj = 0; jj < 3; ++jj) {
-            bm[jj][h] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(blk_m[h][jj])));
-            br[jj][h] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(blk_r[h][jj])));
-        }
-    float l[G], o[G][8];
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-        l[h] = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[h][j] = 0.f;
-    }
-    if constexpr (ONE) {
-#pragma unroll
-        for (int u = 0; u < UC; ++u)
-            if (u * NG < T) {
-                const int t = t0 + gid + NG * u;
-                if (t < t1) sdpa_pv<G>(sc[u], vA[u], t, cb0, Sb, bm, br, l, o);
-            }
-    } else {
-        for (int c0 = t0; c0 < t1; c0 += 2 * CH) {
-#pragma unroll
-            for (int u = 0; u < UC; ++u) {
-                const int t = c0 + gid + NG * u;
-                if (t < t1) {
-                    float sv[G];
-#pragma unroll
-                    for (int h = 0; h < G; ++h) sv[h] = sc_lds[h][t - t0];
-                    sdpa_pv<G>(sv, vA[u], t, cb0, Sb, bm, br, l, o);
-                }
-            }
-            if (c0 + 2 * CH < t1) {
-#pragma unroll
-                for (int u = 0; u < UC; ++u)
-                    vA[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)min(c0 + 2 * CH + gid + NG * u, tl) * D);
-            }
-            if (c0 + CH < t1) {
-#pragma unroll
-                for (int u = 0; u < UC; ++u) {
-                    const int t = c0 + CH + gid + NG * u;
-                    if (t < t1) {
-                        float sv[G];
-#pragma unroll
-                        for (int h = 0; h < G; ++h) sv[h] = sc_lds[h][t - t0];
-                        sdpa_pv<G>(sv, vB[u], t, cb0, Sb, bm, br, l, o);
-                    }
-                }
-                if (c0 + 3 * CH < t1) {
-#pragma unroll
-                    for (int u = 0; u < UC; ++u)
-                        vB[u] = *reinterpret_cast<const uint4*>(V + kvb + (int64_t)min(c0 + 3 * CH + gid + NG * u, tl) * D);
+    // ---- probabilities and P.V ----
+    // block-uniform values read once into scalar registers (hipcc otherwise sank the LDS loads into
+    // the per-key selects and built a table of LDS addresses in scratch)
+    auto sload = [](const float& v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+    const float bm0 = sload(blk_m[0]), bm1 = sload(blk_m[1]), bm2 = sload(blk_m[2]);
+    const float br0 = sload(blk_r[0]), br1 = sload(blk_r[1]), br2 = sload(blk_r[2]);
+    float l = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (t0 < t1) {
+        if constexpr (ONE) {
+            sdpa_pv<U, ONE>(vA, sc, sc_lds, t0, gid, t0, t1, cb0, Sb, bm0, bm1, bm2, br0, br1, br2, l, o);
+        } else {
+            for (int c0 = t0; c0 < t1; c0 += 2 * CH) {
+                sdpa_pv<U, ONE>(vA, sc, sc_lds, c0, gid, t0, t1, cb0, Sb, bm0, bm1, bm2, br0, br1, br2, l, o);
+                if (c0 + 2 * CH < t1) sdpa_load<U>(vA, V, kvb, c0 + 2 * CH, gid, t1);
+                if (c0 + CH < t1) {
+                    sdpa_pv<U, ONE>(vB, sc, sc_lds, c0 + CH, gid, t0, t1, cb0, Sb, bm0, bm1, bm2, br0, br1, br2, l, o);
+                    if (c0 + 3 * CH < t1) sdpa_load<U>(vB, V, kvb, c0 + 3 * CH, gid, t1);
                 }
             }
         }
     }
-    WF_STAMP(6);
-    // ---- the block's record per head: the wave's 4 lane groups summed (permlane swaps), then the
-    // waves in order ----
+    // ---- sum the lane groups (every record is in one frame: plain sums) ----
+    auto sum16 = [](float v) __attribute__((always_inline)) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    };
+    auto sum32 = [](float v) __attribute__((always_inline)) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    };
+    l = sum32(sum16(l));
 #pragma unroll
-    for (int h = 0; h < G; ++h) {
-        l[h] = pl32_sum(pl16_sum(l[h]));
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[h][j] = pl32_sum(pl16_sum(o[h][j]));
-    }
-    if (lane < 16) {
-#pragma unroll
-        for (int h = 0; h < G; ++h) {
-            if (li == 0) sm_l[wv][h] = l[h];
-            *reinterpret_cast<float4*>(&sm_o[wv][h][li * 8]) = make_float4(o[h][0], o[h][1], o[h][2], o[h][3]);
-            *reinterpret_cast<float4*>(&sm_o[wv][h][li * 8 + 4]) = make_float4(o[h][4], o[h][5], o[h][6], o[h][7]);
-        }
+    for (int j = 0; j < 8; ++j) o[j] = sum32(sum16(o[j]));
+    if (lane < LP) {
+        if (li == 0) sm_l[wv] = l;
+        *reinterpret_cast<float4*>(&sm_o[wv][li * 8]) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(&sm_o[wv][li * 8 + 4]) = make_float4(o[4], o[5], o[6], o[7]);
     }
     __syncthreads();
+    const float fr = sload(fin_r);
+    if (threadIdx.x < D / 4) {
+        const int d = 4 * threadIdx.x;
+        float ls = 0.f, os[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) {
+            ls += sm_l[w];
+            const float4 ov = *reinterpret_cast<const float4*>(&sm_o[w][d]);
+            os[0] += ov.x; os[1] += ov.y; os[2] += ov.z; os[3] += ov.w;
+        }
+        const int64_t rec = bh * NS + s;
+        st16_sc1(make_rsrc(o_out), (int)(4 * part_o_off<NS>(bh, s, d)),
+                 __builtin_bit_cast(uint4, make_float4(os[0] * fr, os[1] * fr, os[2] * fr, os[3] * fr)));
+        if (d == 0) st_sc1(reinterpret_cast<uint64_t*>(ml_out) + rec, __builtin_bit_cast(uint64_t, make_float2(0.f, ls * fr)));
+    }
     WF_STAMP(3);
-    uint16_t* orow = row_out + (int64_t)b * (G * Hkv) * D + (int64_t)g * G * D;  // the group's G x 128 outputs
-    if (nact == 1) {  // the whole context in this split: the row directly
-        for (int p = tid; p < G * 64; p += NT) {
-            const int h = p >> 6, d = 2 * (p & 63);
-            const float fr = fin_r[h];
-            float O0 = 0.f, O1 = 0.f, L = 0.f;
-#pragma unroll
-            for (int w = 0; w < NWV; ++w) { O0 += sm_o[w][h][d]; O1 += sm_o[w][h][d + 1]; L += sm_l[w][h]; }
-            O0 *= fr; O1 *= fr; L *= fr;
-            const float inv = 1.0f / L;
-            *reinterpret_cast<uint32_t*>(orow + 2 * p) = pk_bf16(O0 * inv, O1 * inv);
+    // ---- the head's last block sums the NS records into the bf16 attention row ----
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned* c = cnt + bh * kTailLine;
+        const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sh_last = (old == (unsigned)NS - 1u);
+        if (old == (unsigned)NS - 1u) {  // every split is past its poll: re-arm, advance the epoch
+            st_sc1(c, 0u);
+            st_sc1(xep + bh * kTailLine, ld_sc1(xep + bh * kTailLine) + 1u);
         }
-        WF_STAMP(4);
-        return ep;
-    }
-    // ---- phase 3: publish the record, merge this block's slice of the group's outputs ----
-    const __amdgpu_buffer_rsrc_t rr = make_rsrc(rec);
-    const int64_t rbase = (bg * NS + s) * kSdpaRec;
-    for (int p = tid; p < G * 64; p += NT) {
-        const int h = p >> 6, d = 2 * (p & 63);
-        const float fr = fin_r[h];
-        float O0 = 0.f, O1 = 0.f;
-#pragma unroll
-        for (int w = 0; w < NWV; ++w) { O0 += sm_o[w][h][d]; O1 += sm_o[w][h][d + 1]; }
-        st16_sc1(rr, (int)(8 * (rbase + 2 * p)), make_uint4(__float_as_uint(O0 * fr), ep, __float_as_uint(O1 * fr), ep));
-    }
-    if (tid < G) {
-        float L = 0.f;
-#pragma unroll
-        for (int w = 0; w < NWV; ++w) L += sm_l[w][tid];
-        st_sc1(rec + rbase + G * D + tid, ((uint64_t)ep << 32) | __float_as_uint(L * fin_r[tid]));
-    }
-    const int P = G * 64, CHP = (P + nact - 1) / nact;  // output pairs of the group / per merging block
-    const int p0 = s * CHP, np = min(P, p0 + CHP) - p0;
-    if (np <= 0) {
-        WF_STAMP(4);
-        return ep;
-    }
-    // wave 0 polls this block's slice of every split's record -- np pair granules of each split
-    // (<= MP per lane) and the splits' G l granules (<= ML per lane) -- every load of a pass issued
-    // before any is checked; one polling wave keeps the sc1 traffic at a few KB per pass
-    if (wv == 0) {
-        const int npg = np * nact, nl = nact * G;
-        bool bad = false;
-        uint4 v[MP];
-        uint64_t x[ML];
-        for (int it = 0;; ++it) {
-#pragma unroll
-            for (int k = 0; k < MP; ++k) {
-                const int e = min(lane + 64 * k, npg - 1), sp = e / np;
-                v[k] = ld16_sc1(rr, (int)(8 * ((bg * NS + sp) * kSdpaRec + 2 * (p0 + e - np * sp))));
-            }
-#pragma unroll
-            for (int k = 0; k < ML; ++k) {
-                const int e = min(lane + 64 * k, nl - 1), sp = e / G;
-                x[k] = ld_sc1(rec + (bg * NS + sp) * kSdpaRec + G * D + (e - G * sp));
-            }
-            bool good = true;
-#pragma unroll
-            for (int k = 0; k < MP; ++k) good = good && v[k].y == want && v[k].w == want;
-#pragma unroll
-            for (int k = 0; k < ML; ++k) good = good && (unsigned)(x[k] >> 32) == want;
-            if (__all(good)) break;
-            if (it >= WF_SDPA_SPIN) {
-                bad = true;
-                if (lane == 0) attn_fail(err, WF_ATTN_ERR_SDPA);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-#pragma unroll
-        for (int k = 0; k < MP; ++k)  // pair granule e = (split e / np, pair e % np) -> mv[e]
-            if (lane + 64 * k < npg)
-                *reinterpret_cast<float2*>(&mv[2 * (lane + 64 * k)]) = make_float2(__uint_as_float(v[k].x), __uint_as_float(v[k].z));
-#pragma unroll
-        for (int k = 0; k < ML; ++k)
-            if (lane + 64 * k < nl) mL[lane + 64 * k] = __uint_as_float((uint32_t)x[k]);
-        if (lane == 0) sh_bad = bad;
     }
     __syncthreads();
-    WF_STAMP(5);
-    if (tid < np) {
-        const int p = p0 + tid, h = p >> 6;
-        float O0 = 0.f, O1 = 0.f, L = 0.f;
-        for (int sp = 0; sp < nact; ++sp) {  // split order
-            const float2 v = *reinterpret_cast<const float2*>(&mv[2 * (sp * np + tid)]);
-            O0 += v.x;
-            O1 += v.y;
-            L += mL[sp * G + h];
-        }
-        const float inv = sh_bad ? __uint_as_float(0x7fc00000u) : 1.0f / L;
-        *reinterpret_cast<uint32_t*>(orow + 2 * p) = pk_bf16(O0 * inv, O1 * inv);
+    if (!sh_last || threadIdx.x >= D / 4) return;
+    const int d = 4 * threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rml = make_rsrc(ml_out), ro = make_rsrc(o_out);
+    float ll[NS];
+    float4 ov[NS];
+#pragma unroll
+    for (int u = 0; u < NS / 2; ++u) {
+        const float4 v = __builtin_bit_cast(float4, ld16_sc1(rml, (int)(8 * (bh * NS) + 16 * u)));
+        ll[2 * u] = v.y; ll[2 * u + 1] = v.w;
     }
-    WF_STAMP(4);
-    return ep;
+#pragma unroll
+    for (int u = 0; u < NS; ++u) ov[u] = __builtin_bit_cast(float4, ld16_sc1(ro, (int)(4 * part_o_off<NS>(bh, u, d))));
+    float L = 0.f, O[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+        L += ll[u];
+        O[0] += ov[u].x; O[1] += ov[u].y; O[2] += ov[u].z; O[3] += ov[u].w;
+    }
+    const float inv = 1.0f / L;
+    *reinterpret_cast<uint2*>(row_out + bh * D + d) =
+        make_uint2(pk_bf16(O[0] * inv, O[1] * inv), pk_bf16(O[2] * inv, O[3] * inv));
 }
 
-#ifndef WF_SDPA_THREADS  // study builds: threads per k_attn_sdpa block (256 or 512)
-#define WF_SDPA_THREADS 512
-#endif
-constexpr int kSdpaThreads = WF_SDPA_THREADS;
-template <int G>
-__global__ __launch_bounds__(kSdpaThreads) void k_attn_sdpa(const uint16_t* __restrict__ q, int64_t q_sb,
-                                                            const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
-                                                            int64_t kv_sb, int64_t kv_sh, int S,
-                                                            const int32_t* __restrict__ seq_lens, float sm_scale, int b0,
-                                                            int NS, uint64_t* __restrict__ xg, uint64_t* __restrict__ rec,
-                                                            unsigned* __restrict__ epw, uint16_t* __restrict__ row_out,
-                                                            unsigned* __restrict__ err, int stall) {
-    const int s = blockIdx.x, g = blockIdx.y, b = b0 + (int)blockIdx.z, Hkv = gridDim.y;
-    // this block's launch count is its tag: every block of the grid reads and re-stores its own word
-    // (first lane), so the words of a group stay equal; read inside the body behind the K / V loads
-    unsigned* ew = epw + ((int64_t)b * Hkv + g) * NS + s;
-    const int Sb = min(seq_lens[b], S);
-    const int T = sdpa_T(max(Sb, 1), NS);
-    if (Sb <= 0 || s * T >= Sb) {  // no keys in this split (block-uniform)
-        if (threadIdx.x == 0) st_sc1(ew, ld_sc1(ew) + 1u);
-        return;
-    }
-    unsigned ep;
-    if (T <= kSdpaOneT)
-        ep = attn_sdpa_body<G, kSdpaThreads, true>(q, q_sb, K, V, kv_sb, kv_sh, Hkv, S, b, Sb, sm_scale, NS, ew, stall, xg,
-                                                   rec, row_out, err);
+__global__ __launch_bounds__(kAttnPartThreads) WF_SDPA_WPE void k_attn_sdpa(const uint16_t* __restrict__ q, int64_t q_sb,
+                                                                const uint16_t* __restrict__ K,
+                                                                const uint16_t* __restrict__ V, int64_t kv_sb,
+                                                                int64_t kv_sh, int Hq, int Hkv, int S,
+                                                                const int32_t* __restrict__ seq_lens, float sm_scale,
+                                                                int b0, uint64_t* __restrict__ xg,
+                                                                float2* __restrict__ ml_out, float* __restrict__ o_out,
+                                                                uint16_t* __restrict__ row_out, unsigned* __restrict__ cnt,
+                                                                unsigned* __restrict__ xep, unsigned* __restrict__ err,
+                                                                int stall) {
+    constexpr int NS = kAttnPartSplits1, NG = kAttnPartThreads / 16;
+    const int s = blockIdx.x, hq = blockIdx.y;
+    const int Sb = min(seq_lens[b0 + (int)blockIdx.z], S);
+    const int T = ((Sb + NS - 1) / NS + 15) / 16 * 16;
+    if (T <= kApUShort * NG)  // block-uniform: one load round holds the split
+        attn_sdpa_body<kApUShort, true>(q, q_sb, K, V, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, b0, xg, ml_out,
+                                        o_out, row_out, cnt, xep, s, hq, err, stall);
     else
-        ep = attn_sdpa_body<G, kSdpaThreads, false>(q, q_sb, K, V, kv_sb, kv_sh, Hkv, S, b, Sb, sm_scale, NS, ew, stall, xg,
-                                                    rec, row_out, err);
-    if (threadIdx.x == 0) st_sc1(ew, ep);  // every wave read the word before the body's first barrier
+        attn_sdpa_body<kApULong, false>(q, q_sb, K, V, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, b0, xg, ml_out,
+                                        o_out, row_out, cnt, xep, s, hq, err, stall);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1382,7 +1217,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
     constexpr int D = 128, P = kFaStages;
     constexpr int kSlot = 16384;
     constexpr int EB = KV8 ? 1 : 2;            // bytes per K / V element
-    constexpr int NDMA = 4 / EB;               // 1-KiB DMAs per wave per stage
+    constexpr int NDMA = 2 * EB;               // 1-KiB DMAs per wave per stage (16 KiB bf16, 8 KiB one-byte)
     constexpr int TB = 4096 * EB;              // bytes of one 32-key K or V tile
     using KF = KvFrag<KV8>;
     __shared__ __attribute__((aligned(16))) uint8_t ring[P * kSlot];
@@ -1447,7 +1282,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
         const int64_t bb = (pt ? (int64_t)s_page[tb] * kv_pgs : (int64_t)tb * 4096) * EB;
         uint8_t* st = ring + (i % P) * kSlot;
         const uint8_t* second = pass == 1 ? Kg + bb : Vg + bb;
-        constexpr int HALF = 4 * NDMA;  // KiB of the stage's first tile
+        constexpr int HALF = 2 * NDMA;  // KiB of the stage's first tile (4 waves x NDMA KiB per stage)
 #pragma unroll
         for (int jj = 0; jj < NDMA; ++jj) {
             const int j = wave * NDMA + jj;
@@ -1537,7 +1372,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __
                 if (u && tb == ta) break;  // wave-uniform
                 if (32 * t >= lim_b) break;
                 float x[16];
-                qk(st + u * 8192, x);
+                qk(st + u * TB, x);
                 if (32 * t + 32 <= lim_lo) {  // below every column's limit (wave-uniform): no masks
 #pragma unroll
                     for (int j = 0; j < 16; ++j) bmax = fmaxf(bmax, x[j]);
@@ -1717,45 +1552,39 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
         return WF_EINVAL;
     }
     if (B < 16 || !kv_tiled) {
-        // the reference's SDPA semantics (k_attn_sdpa): one block per (split, kv head, sequence) with
-        // the group's query heads, the group's rows merged into merged_row in the launch
-        if (!merged_row || !sb || !sb->xg || !sb->rec || !sb->epoch || pt) {
-            set_error("decode_attention_partials: batch < 16 / untiled caches need the merged-row and exchange buffers, no page table");
+        // the reference's SDPA semantics (k_attn_sdpa): one block per (split, query head, sequence),
+        // the head's records merged into the bf16 row merged_row in the launch
+        if (!merged_row || !merge_cnt || !xmax || pt) {
+            set_error("decode_attention_partials: batch < 16 / untiled caches need the merged-row, arrival and exchange buffers, no page table");
             return WF_EINVAL;
         }
-        if (grp != 1 && grp != 2 && grp != 4 && grp != 8) {
-            set_error("decode_attention_partials: GQA group %d not in {1, 2, 4, 8}", grp);
+        if (S > kSdpaMaxSeq) {
+            set_error("decode_attention_partials: max_seq %d > %d at batch < 16 / untiled caches", S, kSdpaMaxSeq);
             return WF_EINVAL;
         }
-        const int NS = sb->ns;
-        if (NS < 1 || NS > kSdpaNSMax || S > NS * kSdpaMaxT) {
-            set_error("decode_attention_partials: max_seq %d > %d (%d splits x %d keys) at batch < 16 / untiled caches", S,
-                      NS * kSdpaMaxT, NS, kSdpaMaxT);
-            return WF_EINVAL;
-        }
-        auto kern = grp == 1 ? k_attn_sdpa<1> : grp == 2 ? k_attn_sdpa<2> : grp == 4 ? k_attn_sdpa<4> : k_attn_sdpa<8>;
-        // every active split of a group polls its siblings: a launch holds only blocks the chip keeps
-        // resident at once (half the occupancy API's count), whole sequences per launch
-        static int caps[4] = {0, 0, 0, 0};
-        const int gi = grp == 1 ? 0 : grp == 2 ? 1 : grp == 4 ? 2 : 3;
-        if (!caps[gi]) {
+        // every split of a head polls its siblings: a launch holds only blocks the chip keeps resident
+        // at once (half the occupancy API's count), whole sequences per launch
+        static int cap = 0;
+        if (!cap) {
             int dev = 0, ncu = 0, per = 0;
             if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kSdpaThreads, 0) != hipSuccess) {
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_attn_sdpa, kAttnPartThreads, 0) != hipSuccess) {
                 set_error("decode_attention_partials: occupancy query failed");
                 return WF_EHIP;
             }
-            caps[gi] = std::max(1, per * ncu / 2);
+            cap = std::max(1, per * ncu / 2);
         }
-        const int per_seq = NS * Hkv;
-        if (per_seq > caps[gi]) {
-            set_error("decode_attention_partials: %d blocks per sequence exceed the resident bound %d", per_seq, caps[gi]);
+        const int per_seq = kAttnPartSplits1 * Hq;
+        if (per_seq > cap) {
+            set_error("decode_attention_partials: %d blocks per sequence exceed the resident bound %d", per_seq, cap);
             return WF_EINVAL;
         }
-        const int chunk = std::max(1, caps[gi] / per_seq);
+        const int chunk = std::max(1, cap / per_seq);
+        unsigned* xep = merge_cnt + (int64_t)B * Hq * kTailLine;  // per-head launch epochs
         for (int b0 = 0; b0 < B; b0 += chunk) {
-            hipLaunchKernelGGL(kern, dim3(NS, Hkv, std::min(chunk, B - b0)), dim3(kSdpaThreads), 0, st, q, q_sb, k, v, kv_sb, kv_sh,
-                               S, seq_lens, sm_scale, b0, NS, sb->xg, sb->rec, sb->epoch, merged_row, sb->err, sb->stall);
+            hipLaunchKernelGGL(k_attn_sdpa, dim3(kAttnPartSplits1, Hq, std::min(chunk, B - b0)), dim3(kAttnPartThreads), 0, st,
+                               q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, b0, xmax, ml, o, merged_row,
+                               merge_cnt, xep, sb ? sb->err : nullptr, sb ? sb->stall : 0);
             if (int rc = check_launch("decode_attention_partials")) return rc;
         }
         return WF_OK;

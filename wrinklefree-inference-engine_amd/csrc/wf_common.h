@@ -26,26 +26,12 @@ inline int check_launch(const char* what) {
     return WF_OK;
 }
 
-// Batch < 16 / untiled-cache decode attention (k_attn_sdpa, wf_attn.hip): splits per (sequence, kv
-// head) and the model-owned buffers of its in-launch exchange (sizes in 8-byte granules).
-constexpr int kSdpaNSMax = 48;         // splits per (sequence, kv head)
-constexpr int kSdpaMaxT = 1024;        // keys per split: a split spans <= 3 512-key blocks
-constexpr int kSdpaXG = 32;            // exchange granules per split: G heads x 3 blocks (G <= 8), padded
-constexpr int kSdpaRec = 8 * 128 + 8;  // record granules per split: G x 128 o, then G l (G <= 8), padded
-// ~240 blocks per launch at batch 1 (one per CU), at least 8 splits per (sequence, kv head)
-inline int sdpa_splits(int B, int Hkv) {
-    const int n = 240 / (B * Hkv > 0 ? B * Hkv : 1);
-    return n < 8 ? 8 : (n > kSdpaNSMax ? kSdpaNSMax : n);
-}
-// codes of the model's host-visible error word (wf_model_check)
+// Decode attention's in-launch exchanges (k_attn_sdpa, k_attn_sdpa_mfma's split-2 sequences): codes of
+// the model's host-visible error word (wf_model_check) and the model-owned hook the launches take.
 enum { WF_ATTN_ERR_SDPA = 1, WF_ATTN_ERR_SPLIT2 = 2 };
 struct SdpaBufs {
-    uint64_t* xg = nullptr;     // exchange granules [B][Hkv][ns][kSdpaXG]
-    uint64_t* rec = nullptr;    // record granules [B][Hkv][ns][kSdpaRec]
-    unsigned* epoch = nullptr;  // per-block launch counts [B][Hkv][ns]
-    unsigned* err = nullptr;    // host-mapped error word (device address)
-    int ns = 0;
-    int stall = 0;              // test hook: polls expect a tag no block stores (the timeout path)
+    unsigned* err = nullptr;  // host-mapped error word (device address)
+    int stall = 0;            // test hook: k_attn_sdpa polls for a tag no block stores (the timeout path)
 };
 
 }  // namespace wf

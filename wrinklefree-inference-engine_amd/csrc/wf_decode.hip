@@ -2096,8 +2096,8 @@ struct wf_model {
     unsigned* seam = nullptr;  // fused row-norm hand-off words (k_dec_gemm_t PRO), zero between launches
     unsigned* attn_cnt = nullptr;  // batched attention tail: one arrival counter per sequence (kTailLine apart)
     uint16_t* attn_row = nullptr;  // batch < 16 / untiled caches: the merged bf16 attention rows [B][H] (kMerge1)
-    uint64_t* attn_xmax = nullptr;  // k_attn_sdpa_mfma's split-2 exchange: {max, epoch} granules [B][Hkv][8]
-    wf::SdpaBufs sdpa;              // k_attn_sdpa's exchange / record granules and launch counts (batch < 16, untiled)
+    uint64_t* attn_xmax = nullptr;  // exchange granules: k_attn_sdpa {max, epoch} [B][Hq][splits][3]; k_attn_sdpa_mfma [B][Hkv][8]
+    wf::SdpaBufs sdpa;              // the attention's error word and test hook
     unsigned* err_host = nullptr;   // host-mapped error word the attention raises on a poll timeout (wf_model_check)
     int32_t* attn_order = nullptr;  // batched attention: sequences by decreasing context (k_seq_order)
     int fuse[4] = {0, 0, 0, 0};  // per GEMM op (QKV, O, GU, DN): row norm fused into the GEMM launch
@@ -2525,10 +2525,7 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     WF_REQUIRE(d.head_dim == 128, "model_create: head_dim must be 128 (got %d)", d.head_dim);
     WF_REQUIRE(d.hidden == d.n_heads * d.head_dim, "model_create: hidden != n_heads * head_dim");
     WF_REQUIRE(d.n_kv_heads > 0 && d.n_heads % d.n_kv_heads == 0, "model_create: bad GQA");
-    {
-        const int grp = d.n_heads / d.n_kv_heads;
-        WF_REQUIRE(grp == 1 || grp == 2 || grp == 4 || grp == 8, "model_create: GQA group %d not in {1, 2, 4, 8}", grp);
-    }
+    WF_REQUIRE(d.n_heads / d.n_kv_heads <= 8, "model_create: GQA group %d > 8", d.n_heads / d.n_kv_heads);
     WF_REQUIRE(d.hidden % 128 == 0 && d.inter % 128 == 0, "model_create: hidden/inter must be multiples of 128");
     WF_REQUIRE(k_pad(d.wfmt, d.hidden) <= 8192 && k_pad(d.wfmt, d.inter) <= 8192,
                "model_create: hidden/inter (padded to the weight format) > 8192 not supported");
@@ -2619,23 +2616,12 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     // (the second half: k_attn_sdpa's exchange counters)
     WF_ALLOC(m->attn_cnt, 2 * sizeof(unsigned) * (size_t)B * d.n_heads * kTailLine);
     WF_ALLOC(m->attn_row, 2 * (size_t)B * d.hidden);
-    WF_ALLOC(m->attn_xmax, sizeof(uint64_t) * 8 * (size_t)B * d.n_kv_heads);
-    if (attn_sdpa_path(m)) {  // k_attn_sdpa: splits, granule buffers, per-block launch counts
-        const int ns = sdpa_splits(B, d.n_kv_heads);
-        if (d.max_seq > ns * kSdpaMaxT) {
-            set_error("model_create: max_seq %d > %d: the batch-%d decode attention takes %d splits of <= %d keys", d.max_seq,
-                      ns * kSdpaMaxT, B, ns, kSdpaMaxT);
-            wf_model_destroy(m);
-            return WF_EINVAL;
-        }
-        const size_t blocks = (size_t)B * d.n_kv_heads * ns;
-        m->sdpa.ns = ns;
-        WF_ALLOC(m->sdpa.xg, sizeof(uint64_t) * kSdpaXG * blocks);
-        WF_ALLOC(m->sdpa.rec, sizeof(uint64_t) * kSdpaRec * blocks);
-        WF_ALLOC(m->sdpa.epoch, sizeof(unsigned) * blocks);
-        if ((e = hipMemset(m->sdpa.xg, 0, sizeof(uint64_t) * kSdpaXG * blocks)) != hipSuccess) return fail(e);
-        if ((e = hipMemset(m->sdpa.rec, 0, sizeof(uint64_t) * kSdpaRec * blocks)) != hipSuccess) return fail(e);
-        if ((e = hipMemset(m->sdpa.epoch, 0, sizeof(unsigned) * blocks)) != hipSuccess) return fail(e);
+    WF_ALLOC(m->attn_xmax, sizeof(uint64_t) * 3 * (size_t)B * d.n_heads * kAttnPartSplits1);
+    if (attn_sdpa_path(m) && d.max_seq > kAttnPartSplits1 * 1024) {  // k_attn_sdpa: 8 splits of <= 1024 keys
+        set_error("model_create: max_seq %d > %d: the batch-%d decode attention takes %d splits of <= 1024 keys", d.max_seq,
+                  kAttnPartSplits1 * 1024, B, kAttnPartSplits1);
+        wf_model_destroy(m);
+        return WF_EINVAL;
     }
     if ((e = hipHostMalloc((void**)&m->err_host, 64, hipHostMallocMapped)) != hipSuccess) return fail(e);
     *m->err_host = 0u;
@@ -2653,7 +2639,8 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     if ((e = hipMemset(m->seam, 0, sizeof(unsigned) * 2 * kSeamTiles * kSeamLine)) != hipSuccess) return fail(e);
     if ((e = hipMemset(m->attn_cnt, 0, 2 * sizeof(unsigned) * (size_t)B * d.n_heads * kTailLine)) != hipSuccess) return fail(e);
     // granule tags start at 0; the first launch's epoch is 1
-    if ((e = hipMemset(m->attn_xmax, 0, sizeof(uint64_t) * 8 * (size_t)B * d.n_kv_heads)) != hipSuccess) return fail(e);
+    if ((e = hipMemset(m->attn_xmax, 0, sizeof(uint64_t) * 3 * (size_t)B * d.n_heads * kAttnPartSplits1)) != hipSuccess)
+        return fail(e);
     fused_norm_plan(m);
     if ((e = hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking)) != hipSuccess) return fail(e);
     *out = m;
@@ -2666,7 +2653,7 @@ int wf_model_destroy(wf_model* m) {
     if (m->graph) (void)hipGraphDestroy(m->graph);
     if (m->cap) (void)hipStreamDestroy(m->cap);
     if (m->err_host) (void)hipHostFree(m->err_host);
-    void* ptrs[] = {m->sdpa.xg, m->sdpa.rec, m->sdpa.epoch, m->attn_cnt, m->attn_row, m->attn_xmax, m->attn_order, m->seq_lens, m->h_a, m->h_b, m->qbuf, m->part_ml, m->part_o, m->hn, m->act, m->q8, m->dec_ws,
+    void* ptrs[] = {m->attn_cnt, m->attn_row, m->attn_xmax, m->attn_order, m->seq_lens, m->h_a, m->h_b, m->qbuf, m->part_ml, m->part_o, m->hn, m->act, m->q8, m->dec_ws,
                     m->act_sf, m->act_sum, m->tickets, m->seam, m->am_part, m->embed_t, m->pf_h_a, m->pf_h_b, m->pf_q,
                     m->pf_attn, m->pf_act, m->pf_q8, m->pf_sf, m->pf_asum, m->pf_seq};
     for (void* p : ptrs)
@@ -2713,7 +2700,7 @@ int wf_model_attn_view(const wf_model* m, wf_attn_records* out) {
     out->q = m->qbuf;
     out->part_ml = reinterpret_cast<const float*>(m->part_ml);
     out->part_o = m->part_o;
-    out->records = 0;  // round 6: k_attn_sdpa keeps its split records as tagged granules
+    out->records = attn_sdpa_path(m) ? kAttnPartSplits1 : 0;
     out->attn_row = m->attn_row;
     return WF_OK;
 }
