@@ -137,6 +137,17 @@ int wf_kv_scatter(void* pool, int elem_bytes, int max_pages, int L, int H, int D
                   const int32_t* pages, int T, int layer, int32_t* bad, void* stream);
 int wf_kv_gather(const void* pool, int elem_bytes, int max_pages, int L, int H, int D, void* k_out, void* v_out,
                  const int32_t* pages, int T, int layer, int32_t* bad, void* stream);
+/* The same two calls on the decode engine's own paged pool (wf_model_desc.page_table's pages, bf16):
+ * k_pool / v_pool = one layer's [num_pages][H][32 * 128] of wf_model_desc.k_cache / v_cache; token
+ * row t of k / v ([T, H*128]) at page pages[t], slot slots[t] in [0, 32) -- the reference's
+ * slot_indices (tests/test_kv_cache_cpp.py:80-126), here the position within a 32-token page, stored
+ * in the K / V tile layouts the batched attention reads. So sgl_kernel.kvcache.KVCacheManager can
+ * hand out, fill and read the very pages the decode step attends over (invalid page / slot ids:
+ * skipped, counted in *bad). head_dim 128. */
+int wf_kv_scatter_tiles(void* k_pool, void* v_pool, int num_pages, int H, int D, const uint16_t* k, const uint16_t* v,
+                        const int32_t* pages, const int32_t* slots, int T, int32_t* bad, void* stream);
+int wf_kv_gather_tiles(const void* k_pool, const void* v_pool, int num_pages, int H, int D, uint16_t* k_out,
+                       uint16_t* v_out, const int32_t* pages, const int32_t* slots, int T, int32_t* bad, void* stream);
 /* KVCache._quantize_to_int8 / _quantize_to_fp8 (kv_cache/kv_cache.py:159-218): given m = max|x|
  * (device), q = clamp(rne(x * float(127/m')), -127, 127), m' = m or 1 if m < 1e-6. */
 int wf_kv_quant_i8(const void* x, int dtype, int64_t n, const float* absmax, int8_t* q, void* stream);

@@ -696,6 +696,79 @@ def test_decode_paged_kv_equals_dense():
     assert torch.equal(dense.logits[3].view(torch.int16), paged.logits[3].view(torch.int16)), t3
 
 
+def test_kv_manager_backed_by_decoder_pool():
+    """One paged pool behind both APIs (tests/test_kv_cache_cpp.py:283-373): the
+    reference's KVCacheManager, backed by a paged decoder, allocates the decoder's own 32-token pages,
+    scatters token rows [T, H*D] into them (slots = position within a page, the tile layouts the
+    batched attention reads), and the decoder -- its sequences mapped onto those pages -- decodes
+    bit-identically to the dense decoder holding the same history; gather_kv returns the rows, the
+    K/V rows the steps append included; freeing through the manager refills the decoder's pool."""
+    from sgl_kernel.kvcache import KVCacheManager
+    from wfamd.model import BitNetConfig, BitNetDecoder, from_kv_tiles, synthetic_weights
+    cfg = BitNetConfig(hidden=512, layers=2, n_heads=4, n_kv_heads=1, head_dim=128, inter=768, vocab=1024,
+                       max_seq=2048)
+    w = synthetic_weights(cfg, seed=5)
+    B, steps = 16, 5
+    dense = BitNetDecoder(cfg, w, batch=B)
+    paged = BitNetDecoder(cfg, w, batch=B, num_pages=B * cfg.max_seq // 32 // 2, page_seed=3)
+    mgr = KVCacheManager.from_decoder(paged)
+    free0 = mgr.num_free_pages()
+    assert free0 == paged.pool.num_free_pages() == paged.pool.num_pages
+    pos = [0, 1, 31, 32, 33, 100, 255, 256, 257, 511, 700, 1000, 1023, 1024, 1300, 1800]
+    gen = torch.Generator(device="cuda").manual_seed(21)
+    pages = []
+    for b in range(B):  # every sequence's pages for its history and the steps ahead, via the reference API
+        pg = mgr.allocate_pages((pos[b] + steps + 32) // 32)
+        assert len(pg) == (pos[b] + steps + 32) // 32
+        paged.map_pages(b, pg.numpy())
+        pages.append(pg)
+    assert mgr.num_free_pages() == paged.pool.num_free_pages() < free0
+    rows = {}
+    for l in range(cfg.layers):
+        k = torch.randn(B, 1, max(pos), 128, generator=gen, device="cuda").to(torch.bfloat16)
+        v = torch.randn(B, 1, max(pos), 128, generator=gen, device="cuda").to(torch.bfloat16)
+        for b in range(B):
+            k[b, :, pos[b]:] = 0
+            v[b, :, pos[b]:] = 0
+        dense.load_kv(l, k, v)
+        for b in range(B):
+            n = pos[b]
+            if n == 0:
+                continue
+            t = torch.arange(n)
+            pg, sl = pages[b][t // 32], (t % 32).to(torch.int32)
+            kr, vr = k[b, 0, :n].contiguous(), v[b, 0, :n].contiguous()  # [T, H*D], H = 1
+            mgr.scatter_kv(kr, vr, pg, sl, l)
+            rows[(l, b)] = (kr, vr, pg, sl)
+    for l, b in ((0, 5), (1, 14)):  # the reference's round trip, from the engine's tile layout
+        kr, vr, pg, sl = rows[(l, b)]
+        ko, vo = torch.zeros_like(kr), torch.zeros_like(vr)
+        mgr.gather_kv(ko, vo, pg, sl, l)
+        assert torch.equal(ko, kr) and torch.equal(vo, vr), (l, b)
+    toks = [(41 * b + 7) % cfg.vocab for b in range(B)]
+    for dec in (dense, paged):
+        dec.set_state(toks, pos)
+    for i in range(steps):
+        dense.step(graph=True)
+        paged.step(graph=True)
+        torch.cuda.synchronize()
+        assert torch.equal(dense.logits.view(torch.int16), paged.logits.view(torch.int16)), i
+        assert torch.equal(dense.tokens, paged.tokens)
+    assert mgr.invalid_page_count() == 0
+    for l in range(cfg.layers):  # the rows the steps appended, read back through the manager
+        kd, vd = from_kv_tiles(dense.k_cache[l], dense.v_cache[l])
+        for b in (0, 3, 9, 15):
+            n = pos[b] + steps
+            t = torch.arange(n)
+            ko = torch.zeros(n, 128, dtype=torch.bfloat16, device="cuda")
+            vo = torch.zeros_like(ko)
+            mgr.gather_kv(ko, vo, pages[b][t // 32], (t % 32).to(torch.int32), l)
+            assert torch.equal(ko, kd[b, 0, :n]) and torch.equal(vo, vd[b, 0, :n]), (l, b)
+    for b in range(B):
+        mgr.free_pages(pages[b])
+    assert mgr.num_free_pages() == paged.pool.num_free_pages() == free0
+
+
 @pytest.mark.parametrize("m,n,k", [(16, 16, 128), (130, 272, 384), (300, 3840, 2560), (513, 2560, 6912),
                                    (1024, 13824, 2560)])
 def test_prefill_gemm_tiled_vs_oracle(orc, m, n, k):

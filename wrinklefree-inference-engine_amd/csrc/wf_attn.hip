@@ -1641,6 +1641,29 @@ __global__ void k_kv_page_copy(uint8_t* __restrict__ pool, const uint8_t* __rest
     }
 }
 
+// The same scatter / gather on the decode engine's own paged pool (the pool wf_model_desc.page_table
+// addresses): page = 32 tokens of every kv head in the K / V tile layouts (wf_norm.h k_tile_off /
+// v_tile_off), token row t of k / v ([T][H * D]) at page pages[t], slot slots[t] < 32 -- the
+// reference's slot_indices (tests/test_kv_cache_cpp.py:80-126). One block per (token, K | V).
+__global__ void k_kv_tile_copy(uint16_t* __restrict__ kpool, uint16_t* __restrict__ vpool, const uint16_t* __restrict__ src_k,
+                               const uint16_t* __restrict__ src_v, uint16_t* __restrict__ dst_k, uint16_t* __restrict__ dst_v,
+                               const int32_t* __restrict__ pages, const int32_t* __restrict__ slots, int P, int H, int scatter,
+                               int32_t* __restrict__ bad) {
+    constexpr int D = 128;
+    const int t = blockIdx.x, kv = blockIdx.y;
+    const int page = pages[t], o = slots[t];
+    if (page < 0 || page >= P || o < 0 || o >= 32) {
+        if (threadIdx.x == 0 && kv == 0 && bad) atomicAdd(bad, 1);
+        return;
+    }
+    uint16_t* pool = (kv ? vpool : kpool) + (int64_t)page * H * 32 * D;
+    for (int e = threadIdx.x; e < H * D; e += blockDim.x) {
+        const int h = e / D, d = e - h * D;
+        const int64_t off = (int64_t)h * 32 * D + (kv ? v_tile_off(o, d) : k_tile_off(o, d));
+        if (scatter) pool[off] = (kv ? src_v : src_k)[(int64_t)t * H * D + e];
+        else (kv ? dst_v : dst_k)[(int64_t)t * H * D + e] = pool[off];
+    }
+}
 
 struct AttnArgs {
     const void* q; int qdt; int64_t q_sb, q_sh;
@@ -1752,6 +1775,31 @@ int wf_kv_scatter(void* pool, int elem_bytes, int max_pages, int L, int H, int D
     WF_REQUIRE(k && v, "kv_scatter: null k/v");
     return kv_page_common((uint8_t*)pool, elem_bytes, max_pages, L, H, D, k, v, nullptr, nullptr, pages, T, layer, bad,
                           1, stream);
+}
+
+static int kv_tile_common(void* kpool, void* vpool, int num_pages, int H, int D, const void* k, const void* v, void* ko,
+                          void* vo, const int32_t* pages, const int32_t* slots, int T, int32_t* bad, int scatter,
+                          void* stream) {
+    WF_REQUIRE(kpool && vpool && pages && slots && T >= 0 && num_pages > 0 && H > 0, "kv_tiles: bad arguments");
+    WF_REQUIRE(D == 128, "kv_tiles: the engine pool's tile layouts need head_dim 128 (got %d)", D);
+    if (T == 0) return WF_OK;
+    hipLaunchKernelGGL(k_kv_tile_copy, dim3(T, 2), dim3(256), 0, as_stream(stream), (uint16_t*)kpool, (uint16_t*)vpool,
+                       (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)ko, (uint16_t*)vo, pages, slots, num_pages, H,
+                       scatter, bad);
+    return check_launch("kv_tile_copy");
+}
+
+int wf_kv_scatter_tiles(void* k_pool, void* v_pool, int num_pages, int H, int D, const uint16_t* k, const uint16_t* v,
+                        const int32_t* pages, const int32_t* slots, int T, int32_t* bad, void* stream) {
+    WF_REQUIRE(k && v, "kv_scatter_tiles: null k/v");
+    return kv_tile_common(k_pool, v_pool, num_pages, H, D, k, v, nullptr, nullptr, pages, slots, T, bad, 1, stream);
+}
+
+int wf_kv_gather_tiles(const void* k_pool, const void* v_pool, int num_pages, int H, int D, uint16_t* k_out,
+                       uint16_t* v_out, const int32_t* pages, const int32_t* slots, int T, int32_t* bad, void* stream) {
+    WF_REQUIRE(k_out && v_out, "kv_gather_tiles: null outputs");
+    return kv_tile_common(const_cast<void*>(k_pool), const_cast<void*>(v_pool), num_pages, H, D, nullptr, nullptr, k_out,
+                          v_out, pages, slots, T, bad, 0, stream);
 }
 
 int wf_kv_gather(const void* pool, int elem_bytes, int max_pages, int L, int H, int D, void* k_out, void* v_out,

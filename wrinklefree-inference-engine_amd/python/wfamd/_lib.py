@@ -51,6 +51,8 @@ SIGNATURES = {
     "wf_bitnet_gemm_tiled": (i32, [vp, vp, f32, i32, i32, i32, vp, i64, vp]),
     "wf_kv_scatter": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp]),
     "wf_kv_gather": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp]),
+    "wf_kv_scatter_tiles": (i32, [vp, vp, i32, i32, i32, vp, vp, vp, vp, i32, vp, vp]),
+    "wf_kv_gather_tiles": (i32, [vp, vp, i32, i32, i32, vp, vp, vp, vp, i32, vp, vp]),
     "wf_kv_quant_i8": (i32, [vp, i32, i64, vp, vp, vp]),
     "wf_kv_dequant_i8": (i32, [vp, i64, vp, vp, i32, vp]),
     "wf_decode_attention_ws_bytes": (i64, [i32, i32, i32, i32]),

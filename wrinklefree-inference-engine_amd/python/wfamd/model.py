@@ -362,6 +362,21 @@ class BitNetDecoder:
         self._pt_host[b, :len(self.seq_pages[b])] = self.seq_pages[b]
         self.page_table[b].copy_(torch.from_numpy(self._pt_host[b]))
 
+    def map_pages(self, b: int, pages) -> None:
+        """Point sequence b's 32-token blocks at `pages` (block j -> pages[j]): pages a caller allocated
+        from this decoder's pool itself, e.g. through sgl_kernel.kvcache.KVCacheManager(backing=self),
+        the reference's paged-KV API over the same pool (tests/test_kv_cache_cpp.py:283-373). The
+        decoder releases them with the sequence (release)."""
+        pg = np.asarray(pages, dtype=np.int32).reshape(-1)
+        if not self.paged:
+            raise ValueError("map_pages needs a paged decoder (num_pages > 0)")
+        if len(pg) > self._pt_host.shape[1] or ((pg < 0) | (pg >= self.pool.num_pages)).any():
+            raise ValueError(f"sequence {b}: bad page list ({len(pg)} pages, pool of {self.pool.num_pages})")
+        self.seq_pages[b] = pg.copy()
+        self._pt_host[b] = 0
+        self._pt_host[b, :len(pg)] = pg
+        self.page_table[b].copy_(torch.from_numpy(self._pt_host[b]))
+
     def release(self, b: int) -> None:
         """Return sequence b's pages to the pool (a finished request)."""
         self.pool.free_pages(self.seq_pages[b])
