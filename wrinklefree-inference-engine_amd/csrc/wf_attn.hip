@@ -320,17 +320,20 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_split(
 // and the K/V load form.
 // ---------------------------------------------------------------------------------------------
 #ifndef WF_AP_THREADS  // study builds only (tools/build_variant.sh): threads per block
-#define WF_AP_THREADS 256
+#define WF_AP_THREADS 512
 #endif
 constexpr int kAttnPartThreads = WF_AP_THREADS;
-// keys per lane group per chunk (chunk = 16 U keys at 256 threads): a split that one 160-key chunk
-// covers (contexts <= 1280 at 8 splits) takes U = 10 -- one load round; longer splits the
-// double-buffered 128-key chunks (same-box, batch 1: U 10 vs 8 at ctx 1024 attention 5.59 -> 4.85 us,
-// 1080 -> 1104 tok/s; at ctx 4000 U 10 alone lost 10.3 -> 11.3 us). -DWF_AP_U=n: one U everywhere.
+// keys per lane group per chunk (chunk = (threads / 16) U keys): a split that one 160-key chunk
+// covers (contexts <= 1280 at 8 splits) takes one load round; longer splits the double-buffered
+// 128-key chunks. Round 6, k_attn_sdpa at ctx 1024 (same box, tools/ab_quick.sh): 256 threads x U 10
+// 10.7 us, 1,014 tok/s; 512 x 5 9.3 us, 1,060 tok/s (half the keys per lane: the QK, P.V and
+// permlane-merge chains of a wave halve, 2 waves per SIMD); 768 x 3 11.1 us; 512 x 5 at 4 splits
+// 12.0 us. (Round 2, exact softmax without the exchange: 512 threads lost, 5.72 -> 6.10 us.)
+// -DWF_AP_U=n: one U everywhere.
 #ifdef WF_AP_U
 constexpr int kApUShort = WF_AP_U, kApULong = WF_AP_U;
 #else
-constexpr int kApUShort = 10, kApULong = 8;
+constexpr int kApUShort = 160 / (kAttnPartThreads / 16), kApULong = 128 / (kAttnPartThreads / 16);
 #endif
 #ifndef WF_KV_NT  // decode-attention K/V loads with the non-temporal hint (each byte is read once per step)
 #define WF_KV_NT 1
