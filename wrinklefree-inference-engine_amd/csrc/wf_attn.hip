@@ -1207,7 +1207,7 @@ __device__ __forceinline__ float swap32_sum(float v) {
 // kernels do (KvFrag<KV8>); the K scale is folded into `scale`, the V scale multiplies the output
 // (k_attn_sdpa_mfma's arithmetic), so a prompt and its decode steps share the SDPA semantics.
 // F64: q.k as eight zero-C 16-product MFMA partials summed in f64 in both passes (study: 109 vs 307
-// of 911360 outputs off the oracle, +30 % kernel time; round 5).
+// of 911360 outputs off the oracle; 2.7x the kernel time on the round-6 build, 441 -> 1,178 us).
 template <int KV8, bool F64>
 __global__ __launch_bounds__(256, 2) void k_attn_prefill_sdpa(const uint16_t* __restrict__ q, int64_t q_rs,
                                                               const uint16_t* __restrict__ K,
@@ -1521,8 +1521,8 @@ int prefill_attention_check(int Hq, int Hkv, int pps) {
 // when the items split evenly over the 8 XCDs (each XCD streams one (slot, kv head) K/V at a time
 // from its own L2: 333 -> 250 us per layer at 8 x 2048). Rows come in aligned groups of 32 of one slot
 // (wf_model_prefill checks M % kPrefillRowGroup == 0).
-#ifndef WF_PF_QK_F64  // study: q.k partials in f64 in both passes (+30 % kernel time, round 5)
-#define WF_PF_QK_F64 0
+#ifndef WF_PF_QK_F64  // study: q.k partials in f64 in both passes (round 6, same box: 441 -> 1,178 us
+#define WF_PF_QK_F64 0   // per layer; 307 -> 109 sampled outputs, 54 -> 27 layer-1 positions off the oracle)
 #endif
 int prefill_attention(const uint16_t* q, int64_t q_rs, const uint16_t* k, const uint16_t* v, int64_t kv_sb,
                       int64_t kv_sh, int Hq, int Hkv, const int32_t* row_pos, const int32_t* row_slot, int M,
