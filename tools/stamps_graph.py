@@ -33,7 +33,7 @@ from wfamd.model import BITNET_2B, BitNetDecoder, synthetic_weights  # noqa: E40
 SLOTS, NBLK = 80, 16384
 GEMV_NAMES = {0: "entry", 1: "image", 2: "dot", 3: "out", 7: "qkv_out", 8: "p_ss", 9: "p_r", 10: "p_y", 11: "p_sf",
               12: "p_q", 13: "w_landed"}
-ATTN_NAMES = {0: "entry", 1: "qk_done", 2: "exchanged", 3: "records"}
+ATTN_NAMES = {0: "entry", 1: "qk_done", 2: "exchanged", 3: "records", 4: "merged"}
 LM_NAMES = {0: "entry", 1: "staged", 2: "dot", 3: "ticket", 4: "argmax"}
 GEMM_NAMES = {0: "entry", 14: "norm_published", 15: "rows_ready", 1: "issued", 2: "first_mma", 3: "mma_done",
               4: "combined", 5: "epilogue"}
@@ -109,7 +109,7 @@ def main():
     dc, at = read(lib, "wf_debug_stamps_decode"), read(lib, "wf_debug_stamps_attn")
     if B == 1:
         order = ("qkv", "attn", "o_proj", "gate_up", "down", "lm_head")
-        ops = {"qkv": (dc[0:512], GEMV_NAMES, 7), "attn": (at[0:2048], ATTN_NAMES, 3),
+        ops = {"qkv": (dc[0:512], GEMV_NAMES, 7), "attn": (at[0:2048], ATTN_NAMES, 4),
                "o_proj": (dc[512:1024], GEMV_NAMES, 3), "gate_up": (dc[1024:1536], GEMV_NAMES, 3),
                "down": (dc[1536:2048], GEMV_NAMES, 3), "lm_head": (dc[4096:4096 + 8016], LM_NAMES, 3)}
     else:

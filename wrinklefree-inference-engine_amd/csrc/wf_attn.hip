@@ -528,10 +528,11 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
                                                int Hkv, int S, const int32_t* __restrict__ seq_lens, float sm_scale,
                                                int b0, uint64_t* __restrict__ xg, float2* __restrict__ ml_out,
                                                float* __restrict__ o_out, uint16_t* __restrict__ row_out,
-                                               unsigned* __restrict__ cnt, unsigned* __restrict__ xep, int s, int hq,
+                                               uint64_t* __restrict__ xo, unsigned* __restrict__ xep, int s, int hq,
                                                unsigned* __restrict__ err, int stall) {
     constexpr int NS = kAttnPartSplits1, D = 128, LP = 16, NG = kAttnPartThreads / LP, CH = U * NG;
     constexpr int NWV = kAttnPartThreads / 64;
+    static_assert(NS * 16 == D, "split s merges dims 16 s .. 16 s + 15");
     const int b = b0 + (int)blockIdx.z;
     const int g = hq / (Hq / Hkv);
     const int gid = threadIdx.x / LP, li = threadIdx.x % LP, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -541,12 +542,14 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
     const int cb0 = t0 >> 9;
     const int64_t bh = (int64_t)b * Hq + hq;
     WF_STAMP(0);
+    // this launch's tag: the head's epoch word + 1, read before anything else (the word is advanced
+    // by split 0 once every split has published its maxima, i.e. has read it)
+    const unsigned ep = ld_sc1(xep + bh * kTailLine) + 1u;
     __shared__ float sc_lds[ONE ? 1 : kSdpaMaxT];
     __shared__ float red[NWV][3];
     __shared__ float blk_m[3], blk_r[3], fin_r;
     __shared__ float sm_l[NWV];
     __shared__ __attribute__((aligned(16))) float sm_o[NWV][D];
-    __shared__ int sh_last;
 
     const int64_t kvb = b * kv_sb + g * kv_sh + li * 8;
     const uint4 qv = *reinterpret_cast<const uint4*>(q + b * q_sb + (int64_t)hq * D + li * 8);
@@ -586,7 +589,6 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
     }
     __syncthreads();
     if (__builtin_amdgcn_readfirstlane(wv) == 0) {  // wave 0 (a scalar branch: no exec-masked loop)
-        const unsigned ep = ld_sc1(xep + bh * kTailLine) + 1u;  // this launch's tag
         const unsigned want = stall ? ep + 1u : ep;  // test hook (wf_model_debug_stall_attention): a tag nobody stores
         float bmx[3];  // the block's maxima (constant LDS indices: uniform scalars)
 #pragma unroll
@@ -613,6 +615,8 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
             }
             __builtin_amdgcn_s_sleep(WF_SDPA_SLEEP);
         }
+        // every split has published its maxima, so every split has read the epoch word: advance it
+        if (s == 0 && lane == 0) st_sc1(xep + bh * kTailLine, ep);
         const float val = __uint_as_float((uint32_t)gv);
         const int blk = lane < 3 * NS ? ((sp * T) >> 9) + ent : -1;
         const int NB = (Sb + 511) >> 9;
@@ -679,6 +683,12 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
     }
     __syncthreads();
     const float fr = sload(fin_r);
+    // ---- records, and the merge as an all-to-all of tagged granules ----
+    // Split s merges dims [16 s, 16 s + 16) of the head. Every split publishes, for each target split
+    // r, its 16 dims of r's range and its l as 8-byte {value, tag} granules (slot (bh, r, s) of
+    // kSdpaMergeSlot granules, one sc1 store per pair); wave 0 of split r polls the NS slots of its
+    // own range and sums them in split order -- the operations (and order) of a single merging block,
+    // without the drain, the arrival ticket and the last block's record reads.
     if (threadIdx.x < D / 4) {
         const int d = 4 * threadIdx.x;
         float ls = 0.f, os[4] = {0.f, 0.f, 0.f, 0.f};
@@ -688,46 +698,47 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
             const float4 ov = *reinterpret_cast<const float4*>(&sm_o[w][d]);
             os[0] += ov.x; os[1] += ov.y; os[2] += ov.z; os[3] += ov.w;
         }
+        ls *= fr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) os[j] *= fr;
+        const __amdgpu_buffer_rsrc_t rx = make_rsrc(xo);
+        const int slot = (int)(((bh * NS + (d >> 4)) * NS + s) * kSdpaMergeSlot) * 8;  // byte offset
+        st16_sc1(rx, slot + 8 * (d & 15), make_uint4(__float_as_uint(os[0]), ep, __float_as_uint(os[1]), ep));
+        st16_sc1(rx, slot + 8 * (d & 15) + 16, make_uint4(__float_as_uint(os[2]), ep, __float_as_uint(os[3]), ep));
+        if ((d & 15) == 0) st_sc1(xo + slot / 8 + 16, ((uint64_t)ep << 32) | __float_as_uint(ls));
+        // the records (the API's attention view): read by no kernel of this launch
         const int64_t rec = bh * NS + s;
-        st16_sc1(make_rsrc(o_out), (int)(4 * part_o_off<NS>(bh, s, d)),
-                 __builtin_bit_cast(uint4, make_float4(os[0] * fr, os[1] * fr, os[2] * fr, os[3] * fr)));
-        if (d == 0) st_sc1(reinterpret_cast<uint64_t*>(ml_out) + rec, __builtin_bit_cast(uint64_t, make_float2(0.f, ls * fr)));
+        *reinterpret_cast<float4*>(o_out + part_o_off<NS>(bh, s, d)) = make_float4(os[0], os[1], os[2], os[3]);
+        if (d == 0) *reinterpret_cast<float2*>(ml_out + rec) = make_float2(0.f, ls);
     }
     WF_STAMP(3);
-    // ---- the head's last block sums the NS records into the bf16 attention row ----
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned* c = cnt + bh * kTailLine;
-        const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sh_last = (old == (unsigned)NS - 1u);
-        if (old == (unsigned)NS - 1u) {  // every split is past its poll: re-arm, advance the epoch
-            st_sc1(c, 0u);
-            st_sc1(xep + bh * kTailLine, ld_sc1(xep + bh * kTailLine) + 1u);
+    if (__builtin_amdgcn_readfirstlane(wv) != 0) return;
+    // lane j < 16: dim 16 s + j of every source split; lane 16: the sources' l
+    const int64_t src = (bh * NS + s) * NS * kSdpaMergeSlot + min(lane, 16);
+    uint64_t gv[NS];
+    for (int it = 0;; ++it) {
+        bool okl = true;
+#pragma unroll
+        for (int u = 0; u < NS; ++u) {
+            gv[u] = lane <= 16 ? ld_sc1(xo + src + u * kSdpaMergeSlot) : ((uint64_t)ep << 32);
+            okl = okl && (unsigned)(gv[u] >> 32) == ep;
         }
-    }
-    __syncthreads();
-    if (!sh_last || threadIdx.x >= D / 4) return;
-    const int d = 4 * threadIdx.x;
-    const __amdgpu_buffer_rsrc_t rml = make_rsrc(ml_out), ro = make_rsrc(o_out);
-    float ll[NS];
-    float4 ov[NS];
+        if (__all(okl)) break;
+        if (it > WF_SDPA_SPIN) {
+            if (lane == 0) attn_fail(err, WF_ATTN_ERR_SDPA);
 #pragma unroll
-    for (int u = 0; u < NS / 2; ++u) {
-        const float4 v = __builtin_bit_cast(float4, ld16_sc1(rml, (int)(8 * (bh * NS) + 16 * u)));
-        ll[2 * u] = v.y; ll[2 * u + 1] = v.w;
+            for (int u = 0; u < NS; ++u) gv[u] = 0x7fc00000u;  // NaN row
+            break;
+        }
+        __builtin_amdgcn_s_sleep(WF_SDPA_SLEEP);
     }
+    float acc = 0.f;
 #pragma unroll
-    for (int u = 0; u < NS; ++u) ov[u] = __builtin_bit_cast(float4, ld16_sc1(ro, (int)(4 * part_o_off<NS>(bh, u, d))));
-    float L = 0.f, O[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < NS; ++u) {
-        L += ll[u];
-        O[0] += ov[u].x; O[1] += ov[u].y; O[2] += ov[u].z; O[3] += ov[u].w;
-    }
+    for (int u = 0; u < NS; ++u) acc += __uint_as_float((uint32_t)gv[u]);
+    const float L = __shfl(acc, 16, 64);
     const float inv = 1.0f / L;
-    *reinterpret_cast<uint2*>(row_out + bh * D + d) =
-        make_uint2(pk_bf16(O[0] * inv, O[1] * inv), pk_bf16(O[2] * inv, O[3] * inv));
+    if (lane < 16) row_out[bh * D + 16 * s + lane] = f2bf(acc * inv);
+    WF_STAMP(4);
 }
 
 __global__ __launch_bounds__(kAttnPartThreads) WF_SDPA_WPE void k_attn_sdpa(const uint16_t* __restrict__ q, int64_t q_sb,
@@ -737,7 +748,7 @@ __global__ __launch_bounds__(kAttnPartThreads) WF_SDPA_WPE void k_attn_sdpa(cons
                                                                 const int32_t* __restrict__ seq_lens, float sm_scale,
                                                                 int b0, uint64_t* __restrict__ xg,
                                                                 float2* __restrict__ ml_out, float* __restrict__ o_out,
-                                                                uint16_t* __restrict__ row_out, unsigned* __restrict__ cnt,
+                                                                uint16_t* __restrict__ row_out, uint64_t* __restrict__ xo,
                                                                 unsigned* __restrict__ xep, unsigned* __restrict__ err,
                                                                 int stall) {
     constexpr int NS = kAttnPartSplits1, NG = kAttnPartThreads / 16;
@@ -746,10 +757,10 @@ __global__ __launch_bounds__(kAttnPartThreads) WF_SDPA_WPE void k_attn_sdpa(cons
     const int T = ((Sb + NS - 1) / NS + 15) / 16 * 16;
     if (T <= kApUShort * NG)  // block-uniform: one load round holds the split
         attn_sdpa_body<kApUShort, true>(q, q_sb, K, V, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, b0, xg, ml_out,
-                                        o_out, row_out, cnt, xep, s, hq, err, stall);
+                                        o_out, row_out, xo, xep, s, hq, err, stall);
     else
         attn_sdpa_body<kApULong, false>(q, q_sb, K, V, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, b0, xg, ml_out,
-                                        o_out, row_out, cnt, xep, s, hq, err, stall);
+                                        o_out, row_out, xo, xep, s, hq, err, stall);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1584,10 +1595,11 @@ int decode_attention_partials(const uint16_t* q, int64_t q_sb, const uint16_t* k
         }
         const int chunk = std::max(1, cap / per_seq);
         unsigned* xep = merge_cnt + (int64_t)B * Hq * kTailLine;  // per-head launch epochs
+        uint64_t* xo = xmax + sdpa_xmax_granules(B, Hq);             // merge granules
         for (int b0 = 0; b0 < B; b0 += chunk) {
             hipLaunchKernelGGL(k_attn_sdpa, dim3(kAttnPartSplits1, Hq, std::min(chunk, B - b0)), dim3(kAttnPartThreads), 0, st,
                                q, q_sb, k, v, kv_sb, kv_sh, Hq, Hkv, S, seq_lens, sm_scale, b0, xmax, ml, o, merged_row,
-                               merge_cnt, xep, sb ? sb->err : nullptr, sb ? sb->stall : 0);
+                               xo, xep, sb ? sb->err : nullptr, sb ? sb->stall : 0);
             if (int rc = check_launch("decode_attention_partials")) return rc;
         }
         return WF_OK;

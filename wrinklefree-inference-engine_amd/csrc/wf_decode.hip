@@ -2616,7 +2616,10 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     // (the second half: k_attn_sdpa's exchange counters)
     WF_ALLOC(m->attn_cnt, 2 * sizeof(unsigned) * (size_t)B * d.n_heads * kTailLine);
     WF_ALLOC(m->attn_row, 2 * (size_t)B * d.hidden);
-    WF_ALLOC(m->attn_xmax, sizeof(uint64_t) * 3 * (size_t)B * d.n_heads * kAttnPartSplits1);
+    // k_attn_sdpa: split maxima + merge granules; k_attn_sdpa_mfma: [B][Hkv][8] (fits the maxima part)
+    const size_t xbytes = sizeof(uint64_t) * (size_t)(attn_sdpa_path(m) ? sdpa_xbuf_granules(B, d.n_heads)
+                                                                         : sdpa_xmax_granules(B, d.n_heads));
+    WF_ALLOC(m->attn_xmax, xbytes);
     if (attn_sdpa_path(m) && d.max_seq > kAttnPartSplits1 * 1024) {  // k_attn_sdpa: 8 splits of <= 1024 keys
         set_error("model_create: max_seq %d > %d: the batch-%d decode attention takes %d splits of <= 1024 keys", d.max_seq,
                   kAttnPartSplits1 * 1024, B, kAttnPartSplits1);
@@ -2639,8 +2642,7 @@ int wf_model_create(const wf_model_desc* dp, wf_model** out) {
     if ((e = hipMemset(m->seam, 0, sizeof(unsigned) * 2 * kSeamTiles * kSeamLine)) != hipSuccess) return fail(e);
     if ((e = hipMemset(m->attn_cnt, 0, 2 * sizeof(unsigned) * (size_t)B * d.n_heads * kTailLine)) != hipSuccess) return fail(e);
     // granule tags start at 0; the first launch's epoch is 1
-    if ((e = hipMemset(m->attn_xmax, 0, sizeof(uint64_t) * 3 * (size_t)B * d.n_heads * kAttnPartSplits1)) != hipSuccess)
-        return fail(e);
+    if ((e = hipMemset(m->attn_xmax, 0, xbytes)) != hipSuccess) return fail(e);
     fused_norm_plan(m);
     if ((e = hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking)) != hipSuccess) return fail(e);
     *out = m;

@@ -376,6 +376,13 @@ __device__ __forceinline__ int64_t bf_tile_off(int r, int p, int H) {
 constexpr int kAttnPartSplits = WF_SPLITS;    // records per (sequence, query head): batched decode (B >= 16)
 constexpr int kAttnPartSplits1 = WF_SPLITS1;  // batch < 16 (16 measured: attention 5.70 -> 5.63 us, O input 6.01 -> 7.27 us)
 constexpr int kAttnPartSplitsMax = 16;
+// k_attn_sdpa's exchange buffer (the model's attn_xmax): the split maxima [B][Hq][splits][3], then the
+// merge granules [B][Hq][target split][source split][kSdpaMergeSlot] (16 dims + l, padded to 16-byte pairs)
+constexpr int kSdpaMergeSlot = 18;
+inline int64_t sdpa_xmax_granules(int B, int Hq) { return 3LL * B * Hq * kAttnPartSplits1; }
+inline int64_t sdpa_xbuf_granules(int B, int Hq) {
+    return sdpa_xmax_granules(B, Hq) + (int64_t)B * Hq * kAttnPartSplits1 * kAttnPartSplits1 * kSdpaMergeSlot;
+}
 static_assert(kAttnPartSplits <= kAttnPartSplitsMax && kAttnPartSplits1 <= kAttnPartSplitsMax,
               "part_ml / part_o are sized for kAttnPartSplitsMax records per (sequence, head)");
 static_assert(kAttnPartSplits % 4 == 0 && kAttnPartSplits1 % 2 == 0, "record counts: whole 4-wave blocks / pairs");
