@@ -138,6 +138,11 @@ def main():
     out.parent.mkdir(exist_ok=True)
     out.write_text(json.dumps(res, indent=1))
     (out.parent / f"stamps_graph_b{B}_attn_raw.json").write_text(json.dumps(raw))
+    if B == 1:  # per-block LM head stamps (entry, staged, dot, ticket, argmax), us from t0
+        lr = ops["lm_head"][0]
+        lraw = [[int(i)] + [round(float((lr[i, sl] - t0) * 0.01), 2) if lr[i, sl] > 0 else None for sl in LM_NAMES]
+                for i in np.nonzero(lr[:, 0] > 0)[0]]
+        (out.parent / f"stamps_graph_b{B}_lm_raw.json").write_text(json.dumps(lraw))
 
 
 if __name__ == "__main__":

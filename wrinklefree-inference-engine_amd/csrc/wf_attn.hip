@@ -532,7 +532,8 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
                                                unsigned* __restrict__ err, int stall) {
     constexpr int NS = kAttnPartSplits1, D = 128, LP = 16, NG = kAttnPartThreads / LP, CH = U * NG;
     constexpr int NWV = kAttnPartThreads / 64;
-    static_assert(NS * 16 == D, "split s merges dims 16 s .. 16 s + 15");
+    constexpr int DM = kSdpaMergeDims;  // split s merges dims DM s .. DM s + DM - 1
+    static_assert(NS * DM == D && DM % 4 == 0 && DM < 64, "whole 4-dim pieces per merge range");
     const int b = b0 + (int)blockIdx.z;
     const int g = hq / (Hq / Hkv);
     const int gid = threadIdx.x / LP, li = threadIdx.x % LP, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -605,6 +606,8 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
         const int sp = lane / 3, ent = lane - 3 * sp;
         uint64_t gv = ((uint64_t)ep << 32) | 0xff800000u;  // lanes past the granules: -inf, tagged
         int ok = 1;
+        // (measured, not kept: two polls in flight; V loaded after the exchange or after the wave's
+        // q.k instead of with K -- profiles/ab_attn_merge_r06.txt)
         for (int it = 0;; ++it) {
             if (lane < 3 * NS) gv = ld_sc1(xg + bh * NS * 3 + lane);
             if (__all((unsigned)(gv >> 32) == want)) break;
@@ -684,8 +687,8 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
     __syncthreads();
     const float fr = sload(fin_r);
     // ---- records, and the merge as an all-to-all of tagged granules ----
-    // Split s merges dims [16 s, 16 s + 16) of the head. Every split publishes, for each target split
-    // r, its 16 dims of r's range and its l as 8-byte {value, tag} granules (slot (bh, r, s) of
+    // Split s merges dims [DM s, DM s + DM) of the head. Every split publishes, for each target split
+    // r, its DM dims of r's range and its l as 8-byte {value, tag} granules (slot (bh, r, s) of
     // kSdpaMergeSlot granules, one sc1 store per pair); wave 0 of split r polls the NS slots of its
     // own range and sums them in split order -- the operations (and order) of a single merging block,
     // without the drain, the arrival ticket and the last block's record reads.
@@ -702,10 +705,10 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
 #pragma unroll
         for (int j = 0; j < 4; ++j) os[j] *= fr;
         const __amdgpu_buffer_rsrc_t rx = make_rsrc(xo);
-        const int slot = (int)(((bh * NS + (d >> 4)) * NS + s) * kSdpaMergeSlot) * 8;  // byte offset
-        st16_sc1(rx, slot + 8 * (d & 15), make_uint4(__float_as_uint(os[0]), ep, __float_as_uint(os[1]), ep));
-        st16_sc1(rx, slot + 8 * (d & 15) + 16, make_uint4(__float_as_uint(os[2]), ep, __float_as_uint(os[3]), ep));
-        if ((d & 15) == 0) st_sc1(xo + slot / 8 + 16, ((uint64_t)ep << 32) | __float_as_uint(ls));
+        const int slot = (int)(((bh * NS + d / DM) * NS + s) * kSdpaMergeSlot) * 8;  // byte offset
+        st16_sc1(rx, slot + 8 * (d % DM), make_uint4(__float_as_uint(os[0]), ep, __float_as_uint(os[1]), ep));
+        st16_sc1(rx, slot + 8 * (d % DM) + 16, make_uint4(__float_as_uint(os[2]), ep, __float_as_uint(os[3]), ep));
+        if (d % DM == 0) st_sc1(xo + slot / 8 + DM, ((uint64_t)ep << 32) | __float_as_uint(ls));
         // the records (the API's attention view): read by no kernel of this launch
         const int64_t rec = bh * NS + s;
         *reinterpret_cast<float4*>(o_out + part_o_off<NS>(bh, s, d)) = make_float4(os[0], os[1], os[2], os[3]);
@@ -713,14 +716,14 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
     }
     WF_STAMP(3);
     if (__builtin_amdgcn_readfirstlane(wv) != 0) return;
-    // lane j < 16: dim 16 s + j of every source split; lane 16: the sources' l
-    const int64_t src = (bh * NS + s) * NS * kSdpaMergeSlot + min(lane, 16);
+    // lane j < DM: dim DM s + j of every source split; lane DM: the sources' l
+    const int64_t src = (bh * NS + s) * NS * kSdpaMergeSlot + min(lane, DM);
     uint64_t gv[NS];
     for (int it = 0;; ++it) {
         bool okl = true;
 #pragma unroll
         for (int u = 0; u < NS; ++u) {
-            gv[u] = lane <= 16 ? ld_sc1(xo + src + u * kSdpaMergeSlot) : ((uint64_t)ep << 32);
+            gv[u] = lane <= DM ? ld_sc1(xo + src + u * kSdpaMergeSlot) : ((uint64_t)ep << 32);
             okl = okl && (unsigned)(gv[u] >> 32) == ep;
         }
         if (__all(okl)) break;
@@ -735,9 +738,9 @@ __device__ __forceinline__ void attn_sdpa_body(const uint16_t* __restrict__ q, i
     float acc = 0.f;
 #pragma unroll
     for (int u = 0; u < NS; ++u) acc += __uint_as_float((uint32_t)gv[u]);
-    const float L = __shfl(acc, 16, 64);
+    const float L = __shfl(acc, DM, 64);
     const float inv = 1.0f / L;
-    if (lane < 16) row_out[bh * D + 16 * s + lane] = f2bf(acc * inv);
+    if (lane < DM) row_out[bh * D + DM * s + lane] = f2bf(acc * inv);
     WF_STAMP(4);
 }
 

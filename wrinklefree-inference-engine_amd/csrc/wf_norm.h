@@ -377,8 +377,10 @@ constexpr int kAttnPartSplits = WF_SPLITS;    // records per (sequence, query he
 constexpr int kAttnPartSplits1 = WF_SPLITS1;  // batch < 16 (16 measured: attention 5.70 -> 5.63 us, O input 6.01 -> 7.27 us)
 constexpr int kAttnPartSplitsMax = 16;
 // k_attn_sdpa's exchange buffer (the model's attn_xmax): the split maxima [B][Hq][splits][3], then the
-// merge granules [B][Hq][target split][source split][kSdpaMergeSlot] (16 dims + l, padded to 16-byte pairs)
-constexpr int kSdpaMergeSlot = 18;
+// merge granules [B][Hq][target split][source split][kSdpaMergeSlot] (the target's 128 / splits dims
+// + l, padded to 16-byte pairs)
+constexpr int kSdpaMergeDims = 128 / kAttnPartSplits1;
+constexpr int kSdpaMergeSlot = (kSdpaMergeDims + 2) & ~1;
 inline int64_t sdpa_xmax_granules(int B, int Hq) { return 3LL * B * Hq * kAttnPartSplits1; }
 inline int64_t sdpa_xbuf_granules(int B, int Hq) {
     return sdpa_xmax_granules(B, Hq) + (int64_t)B * Hq * kAttnPartSplits1 * kAttnPartSplits1 * kSdpaMergeSlot;
