@@ -58,6 +58,10 @@ constexpr bool kPermEpi = false;
 constexpr bool kPermEpi = true;
 #endif
 
+#ifndef WF_XFIRST  // batch-1 GEMV: a workgroup barrier between the input-row loads and the weight stream
+#define WF_XFIRST 1
+#endif
+constexpr bool kXFirst = WF_XFIRST;
 enum { MODE_QKV = 0, MODE_O = 1, MODE_GU = 2, MODE_DN = 3, MODE_LINEAR = 4 };  // LINEAR: BitNetLinear drop-in
 constexpr int kNT = 512;  // threads per GEMV / row-norm block (8 waves: 2 per SIMD hide the input-stage latency)
 
@@ -207,6 +211,9 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
                                  : make_uint4(0, 0, 0, 0);
             }
     }
+    // every wave's input-row loads reach the CU's load pipe before any wave's weight stream: a wave
+    // whose row loads queued behind the other waves' weights held the norm's first barrier
+    if constexpr (PPT > 0 && kXFirst) __builtin_amdgcn_s_barrier();
     const uint8_t* wr = a.w + (int64_t)min(row, N - 1) * F::row_bytes(K);
     uint4 wpre[kPrefetch];
 #pragma unroll
