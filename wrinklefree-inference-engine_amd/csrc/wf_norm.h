@@ -33,12 +33,18 @@ __device__ __forceinline__ uint4 ld16_sc1(__amdgpu_buffer_rsrc_t r, int byte_off
 }
 
 // Producer side of the launch ticket: all of this block's sc1 stores must be issued before the
-// call. Arrivals are spread over kTicketShards counters (one word takes ~88 atomics/us, so 800+
-// arrivals on one word would serialise for ~10 us); the last arriver of each shard re-arms its shard
-// and relays to the top counter. Returns true in exactly one block of the launch (the last
-// arriver), which must call ticket_rearm() when done. `t` points at kTicketShards + 1 words.
+// call. Arrivals are spread over kTicketShards counters, each on its own 128-byte line (memory-side
+// atomics serialise per LINE at ~88 per us: 501 LM-head arrivals on 32 shards packed into one line
+// queued for ~6 us, the median block's arrival in the in-graph stamps); the last arriver of each
+// shard re-arms its shard and relays to the top counter (a line of its own). Returns true in exactly
+// one block of the launch (the last arriver), which must call ticket_rearm() when done. `t` points
+// at kTicketWords words.
+#ifndef WF_TICKET_LINE  // study: 1 = the shards packed into one line (round 5)
+#define WF_TICKET_LINE 32
+#endif
 constexpr int kTicketShards = 32;
-constexpr int kTicketWords = 64;  // words reserved per ticket (>= kTicketShards + 1, 256-byte aligned)
+constexpr int kTicketLine = WF_TICKET_LINE;  // words between shards
+constexpr int kTicketWords = (kTicketShards + 1) * 32;  // words reserved per ticket (256-byte multiple)
 
 // `idx` in [0, n_blocks) names the arriving block within the ticket's arrival set.
 __device__ __forceinline__ bool ticket_arrive(unsigned* t, unsigned n_blocks, unsigned idx, int* sh_flag) {
@@ -50,11 +56,12 @@ __device__ __forceinline__ bool ticket_arrive(unsigned* t, unsigned n_blocks, un
         const unsigned sh = bid % nsh;
         const unsigned members = (n_blocks - sh + nsh - 1) / nsh;  // blocks with bid % nsh == sh
         bool last = false;
-        const unsigned old = __hip_atomic_fetch_add(t + sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned* ws = t + sh * kTicketLine;
+        const unsigned old = __hip_atomic_fetch_add(ws, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old == members - 1u) {
-            st_sc1(t + sh, 0u);  // every member of this shard has arrived: re-arm it
+            st_sc1(ws, 0u);  // every member of this shard has arrived: re-arm it
             const unsigned top =
-                __hip_atomic_fetch_add(t + kTicketShards, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(t + kTicketShards * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             last = (top == nsh - 1u);
         }
         *sh_flag = last;
@@ -66,7 +73,7 @@ __device__ __forceinline__ unsigned linear_block_id() {
     return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
 }
 __device__ __forceinline__ void ticket_rearm(unsigned* t) {
-    if (threadIdx.x == 0) st_sc1(t + kTicketShards, 0u);
+    if (threadIdx.x == 0) st_sc1(t + kTicketShards * 32, 0u);
 }
 
 // Diagnostic build only (make stamps -> lib/libwfbitnet_stamps.so): thread 0 of every block records
