@@ -208,6 +208,7 @@ INT8_DENSE_PEAK_TOPS = 5000.0  # MI355X dense int8 MFMA (MI355X_MICROARCH.md; no
 def sub_records(cfg, steps: int, warmup: int = 3) -> dict:
     """BASELINE's other single-GPU configurations under the same clock, each
     with its own roofline:
+      b1_tq     -- decode batch 1 at ctx 1024 on the ~1.6-bit TQ weights (configs[1], the other format);
       b128      -- decode batch 128, every sequence at ctx 1024 (configs[3] at a fixed context);
       b128_cfg4 -- decode batch 128 on paged KV, contexts U[1, max_seq - steps) seed 0 (configs[3]);
       prefill   -- 8 sequences x 2048 tokens through wf_model_prefill (configs[2]).
@@ -218,9 +219,30 @@ def sub_records(cfg, steps: int, warmup: int = 3) -> dict:
     import numpy as np
     import torch
     from wfamd.model import BitNetDecoder, synthetic_weights
+    from wfamd import WF_FMT_TQ
     out = {}
     st = torch.cuda.current_stream()
     w = synthetic_weights(cfg, seed=0, device="cuda")
+    # batch 1 on the ~1.6-bit TQ weights (north_star: "packs weights at ~1.6 bit"; the reference's
+    # 1.58 bits / weight, sglang_backend/bitnet_quantization.py:58-61), the headline's workload
+    dec = BitNetDecoder(cfg, w, batch=1, wfmt=WF_FMT_TQ)
+    dec.fill_kv_random(1024, seed=1)
+    dec.set_state([1], [1024])
+    n_tq = max(steps, 100)
+    for _ in range(warmup):
+        dec.step(graph=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n_tq):
+        dec.step(graph=True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    wb = cfg.weight_bytes_per_token(WF_FMT_TQ)
+    out["b1_tq"] = {"workload": "decode batch 1, ctx 1024, TQ weights (5 trits / byte, ~1.6 bit; BASELINE configs[1])",
+                    "tokens_per_s": round(n_tq / el, 1), "ms_per_step": round(1000.0 * el / n_tq, 4), "steps": n_tq,
+                    "weight_bytes_per_token": wb, "weight_gbs": round(wb / (el / n_tq) / 1e9, 1)}
+    del dec
+    torch.cuda.empty_cache()
     for name, dist_ in (("b128", "fixed"), ("b128_cfg4", "uniform")):
         B, total = 128, warmup + steps
         if dist_ == "uniform":
@@ -429,6 +451,8 @@ def main():
         del dec
         torch.cuda.empty_cache()
         sub = sub_records(cfg, args.sub_steps)
+        if wfmt == WF_FMT_I2S:  # the TQ batch-1 rate against this run's I2_S headline
+            sub["b1_tq"]["vs_i2s"] = round(sub["b1_tq"]["tokens_per_s"] / tok_s, 4)
     if cpu:
         cpu_gemv = cpu.pop("gemv")
         if gemv:

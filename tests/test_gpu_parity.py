@@ -432,16 +432,20 @@ def test_decode_batched_mfma_rows_match_single():
             assert int(decb.positions[b]) == step + 1
 
 
-def test_bitnet_linear_native_patch():
+@pytest.mark.parametrize("m", [3, 40, 300])
+def test_bitnet_linear_native_patch(m):
     """kernels/bitnet_patch.py BitNetLinearNative on the HIP kernels equals the reference formula
-    (per-tensor quantize, scale = ws * act_scale, raw blocked-layout kernel, no correction)."""
+    (per-tensor quantize, scale = ws * act_scale, raw blocked-layout kernel, no correction): the
+    reference's batched linear (kernels/bitnet_patch.py:55-78) pinned at M > 1, on the batched GEMV
+    (M < 16) and the int8 matrix-core GEMM (M >= 16) -- one activation scale for the whole tensor."""
     from oracle import oracle as orc
     from wrinklefree_inference.kernels.bitnet_patch import BitNetLinearNative
     rng = np.random.default_rng(9)
     w = rng.integers(-1, 2, size=(256, 512)).astype(np.float32)
     p = orc.pack_i2s(w)
     lin = BitNetLinearNative(512, 256, cu(p), torch.tensor(1.5))
-    x = rng.standard_normal((3, 512)).astype(np.float32)
+    x = rng.standard_normal((m, 512)).astype(np.float32)
+    x[m // 2, 7] = 9.0  # one outlier row sets the shared scale
     y = lin(cu(x)).cpu().numpy()
     q, s = orc.quantize_i8(x)
     ref = orc.gemm_i2s(p, q, np.float32(1.5 * s))
