@@ -2822,11 +2822,14 @@ static void pg_launch(const GemvArgs& a, int nbm, int nbn, hipStream_t st) {
     else
         hipLaunchKernelGGL((k_pgemm_fused<MODE, TNW, ALG, false>), dim3(nbm * nbn), dim3(512), 0, st, a, nbm, nbn);
 }
+#ifndef WF_PF_OD8  // study: o / down on 128 x 512 tiles too (per-fragment epilogue)
+#define WF_PF_OD8 0
+#endif
 template <int MODE>
 static void prefill_gemm(const GemvArgs& a, hipStream_t st) {
     const int nbm = (a.B + 127) / 128;
     if constexpr (MODE != MODE_QKV) {
-        if (pg_wide(a.N)) {  // gate|up: 128 x 512 tiles
+        if (pg_wide(a.N) || (WF_PF_OD8 && MODE != MODE_GU && a.N % 512 == 0)) {  // gate|up: 128 x 512 tiles
             pg_launch<MODE, 8, 0>(a, nbm, (a.N + 511) / 512, st);
             return;
         }
