@@ -12,7 +12,7 @@ for rep in 1 2; do
     if [ $L = product ]; then unset WF_BITNET_LIB; else export WF_BITNET_LIB=$PWD/wrinklefree-inference-engine_amd/lib/libwfbitnet_$L.so; fi
     timeout -k 10 300 python -u -c "
 import json, bench
-bench.GEMM_SWEEP = (bench.GEMM_SWEEP[0], bench.GEMM_SWEEP[1], (1, 2, 4, 8, 16, 32, 64, 128, 192, 256, 384))
+bench.GEMM_SWEEP = (bench.GEMM_SWEEP[0], bench.GEMM_SWEEP[1], (1, 2, 4, 8, 16, 32, 64, 128, 256))
 d = bench.gemm_sweep()
 print('$L', {m: v['us'] for m, v in d['by_M'].items()})" > $O/sweep_$L.log 2>&1 || { tail -5 $O/sweep_$L.log; exit 1; }
     tail -1 $O/sweep_$L.log

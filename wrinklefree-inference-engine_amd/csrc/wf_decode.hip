@@ -26,6 +26,7 @@
 #include "wf_device.h"
 #include "wf_norm.h"
 #include "wf_mfma.h"
+#include "wf_small.h"
 
 namespace wf {
 int prefill_attention_check(int Hq, int Hkv, int pps);
@@ -1398,6 +1399,13 @@ struct EpiLinear {
             const int m = r0 + 4 * q + r;
             if (m < g.B) sg.out[(int64_t)m * sg.ld + sg.col] = f2bf(corrected(acc[r], sg.ws, g.act_sum[m], g.act_sf[m]));
         }
+    }
+};
+// the same epilogue by value for the small-M kernel (wf_small.h)
+struct EpiLinearSmall {
+    GemvArgs a;
+    __device__ __forceinline__ void apply(int r0, int c0, const v4i_t& acc, int l16, int q) const {
+        EpiLinear{&a}.apply(r0, c0, acc, l16, q);
     }
 };
 __global__ __launch_bounds__(256) void k_linear_mfma(GemvArgs a) {
@@ -2822,14 +2830,11 @@ static void pg_launch(const GemvArgs& a, int nbm, int nbn, hipStream_t st) {
     else
         hipLaunchKernelGGL((k_pgemm_fused<MODE, TNW, ALG, false>), dim3(nbm * nbn), dim3(512), 0, st, a, nbm, nbn);
 }
-#ifndef WF_PF_OD8  // study: o / down on 128 x 512 tiles too (per-fragment epilogue)
-#define WF_PF_OD8 0
-#endif
 template <int MODE>
 static void prefill_gemm(const GemvArgs& a, hipStream_t st) {
     const int nbm = (a.B + 127) / 128;
     if constexpr (MODE != MODE_QKV) {
-        if (pg_wide(a.N) || (WF_PF_OD8 && MODE != MODE_GU && a.N % 512 == 0)) {  // gate|up: 128 x 512 tiles
+        if (pg_wide(a.N)) {  // gate|up: 128 x 512 tiles
             pg_launch<MODE, 8, 0>(a, nbm, (a.N + 511) / 512, st);
             return;
         }
@@ -2952,7 +2957,10 @@ int wf_bitnet_linear_fused(int fmt, const uint8_t* w, int nseg, const int* n, co
     if (norm_ppt(K) == 1) hipLaunchKernelGGL(k_quant_rows_lin<1>, dim3(M), dim3(kNT), 0, st, x, ldx, K, q8, q8s, sf, asum);
     else hipLaunchKernelGGL(k_quant_rows_lin<2>, dim3(M), dim3(kNT), 0, st, x, ldx, K, q8, q8s, sf, asum);
     a.q8 = q8; a.q8_stride = q8s; a.act_sf = sf; a.act_sum = asum;
-    hipLaunchKernelGGL(k_linear_mfma, dim3((N + 127) / 128, (M + 127) / 128), dim3(256), 0, st, a);
+    if (gemm_small_ok(M, N))  // 16-32-row tiles (wf_small.h; the 128 x 128 tiles give N / 128 blocks)
+        launch_gemm_small_mfma(w, q8, q8s, M, N, K, EpiLinearSmall{a}, st);
+    else
+        hipLaunchKernelGGL(k_linear_mfma, dim3((N + 127) / 128, (M + 127) / 128), dim3(256), 0, st, a);
     return check_launch("bitnet_linear");
 }
 

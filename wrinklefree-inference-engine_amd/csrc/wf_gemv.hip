@@ -10,6 +10,7 @@
 #include "wf_common.h"
 #include "wf_device.h"
 #include "wf_norm.h"  // stamps (diagnostic build)
+#include "wf_small.h"
 
 namespace wf {
 
@@ -200,119 +201,22 @@ static int launch_ternary_gemm(const uint8_t* w, const int8_t* a, int64_t lda, f
     return check_launch("ternary_gemm");
 }
 
-// ---------------------------------------------------------------------------------------------
-// Small-M GEMM on the int8 matrix cores, row-major operands as the API hands them over (2 <= M <=
-// kSmallMaxM; scripts/benchmark_kernels.py:140,162-170 sweeps M 1-32 on the down projection). The
-// 128 x 64 LDS-DMA tiles of the batched GEMM stage 128 activation rows and give the 2560-row down
-// projection 40 blocks -- 41 us at M = 16 -- while the VALU stream re-reads the activations from LDS
-// once per row (7.8 / 12.4 us at M = 4 / 8). Here a block owns ONE 16-row weight tile and up to 32
-// activation rows (TMT 16-row tiles): v_mfma_i32_16x16x64_i8 with B = the 16 weight rows, A = the
-// activation rows, so every product is useful; 8 waves split the row's 64-byte chunks. Lane (n, q)
-// loads bytes [64 j + 16 q, +16) of weight row n (16 rows x 64 contiguous bytes per instruction) and
-// masks each I2_S group in place (32 / 16 / 4 / 1 x code, one accumulator per group, divided out
-// exactly at the end); the group-g fields of its four dwords are the codes of k = 256 j + 128 (q >> 1)
-// + 16 (q & 1) + 32 g + 0..15, sixteen consecutive activation bytes lane (m, q) loads from row m.
-// Integer sums, then float(sum) * scale: bit-exact with the oracle.
-// ---------------------------------------------------------------------------------------------
-typedef int v4i_t __attribute__((ext_vector_type(4)));
-#ifndef WF_GS_MAXM  // study: largest M on the small-M kernel (above: the 128 x 64 / 128 x 128 LDS-DMA tiles)
-#define WF_GS_MAXM 256
-#endif
-constexpr int kSmallMaxM = WF_GS_MAXM;
-template <int TMT, int TNT, int PRE>
-__global__ __launch_bounds__(512) void k_gemm_small_mfma(const uint8_t* __restrict__ W, const int8_t* __restrict__ A,
-                                                         int64_t lda, float scale, int M, int N, int K,
-                                                         float* __restrict__ Y, int64_t ldy) {
-    constexpr int NW = 8;
-    static_assert(TMT * TNT <= NW, "one output tile per storing wave");
-    __shared__ v4i_t red[NW][TMT * TNT][64];
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int l16 = lane & 15, q = lane >> 4;
-    const int n0 = blockIdx.x * 16 * TNT, m0 = blockIdx.y * 16 * TMT;
-    const int rb = K >> 2, J = (rb + 63) >> 6;  // 64-byte chunks per weight row (the last may be half)
-    const uint8_t* wr[TNT];
+// Small-M GEMM (2 <= M <= kSmallMaxM): wf_small.h.
+// fp32 output of the raw GEMM: Y = float(sum) * scale (the small-M kernel's epilogue)
+struct EpiRawSmall {
+    float* Y;
+    int64_t ldy;
+    float scale;
+    int M, N;
+    __device__ __forceinline__ void apply(int r0, int c0, const v4i_t& acc, int l16, int q) const {
+        const int n = c0 + l16;
 #pragma unroll
-    for (int c = 0; c < TNT; ++c) wr[c] = W + (int64_t)min(n0 + 16 * c + l16, N - 1) * rb;
-    const int8_t* ar[TMT];
-#pragma unroll
-    for (int t = 0; t < TMT; ++t) ar[t] = A + (int64_t)min(m0 + 16 * t + l16, M - 1) * lda;
-    v4i_t ac[TMT][TNT][4];
-#pragma unroll
-    for (int t = 0; t < TMT; ++t)
-#pragma unroll
-        for (int c = 0; c < TNT; ++c)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) ac[t][c][g] = v4i_t{0, 0, 0, 0};
-    for (int j0 = wave; j0 < J; j0 += NW * PRE) {
-        uint4 w[PRE][TNT];
-        v4i_t af[PRE][TMT][4];
-#pragma unroll
-        for (int u = 0; u < PRE; ++u) {  // clamped loads (vmcnt stays exact); invalid chunks zeroed below
-            const int j = min(j0 + NW * u, J - 1);
-#pragma unroll
-            for (int c = 0; c < TNT; ++c) w[u][c] = ldg_nt(wr[c] + min(64 * j + 16 * q, rb - 16));
-            const int k0 = 256 * j + 128 * (q >> 1) + 16 * (q & 1);
-#pragma unroll
-            for (int t = 0; t < TMT; ++t)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) af[u][t][g] = *reinterpret_cast<const v4i_t*>(ar[t] + min(k0 + 32 * g, K - 16));
-        }
-#pragma unroll
-        for (int u = 0; u < PRE; ++u) {
-            const int j = j0 + NW * u;
-            if (j >= J) break;  // wave-uniform
-            const bool valid = 64 * j + 16 * q < rb;
-#pragma unroll
-            for (int c = 0; c < TNT; ++c) {
-                const uint4 x = valid ? w[u][c] : make_uint4(0, 0, 0, 0);
-                const v4i_t bf[4] = {
-                    v4i_t{(int)((x.x >> 1) & 0x60606060u), (int)((x.y >> 1) & 0x60606060u), (int)((x.z >> 1) & 0x60606060u),
-                          (int)((x.w >> 1) & 0x60606060u)},
-                    v4i_t{(int)(x.x & 0x30303030u), (int)(x.y & 0x30303030u), (int)(x.z & 0x30303030u), (int)(x.w & 0x30303030u)},
-                    v4i_t{(int)(x.x & 0x0c0c0c0cu), (int)(x.y & 0x0c0c0c0cu), (int)(x.z & 0x0c0c0c0cu), (int)(x.w & 0x0c0c0c0cu)},
-                    v4i_t{(int)(x.x & 0x03030303u), (int)(x.y & 0x03030303u), (int)(x.z & 0x03030303u), (int)(x.w & 0x03030303u)}};
-#pragma unroll
-                for (int t = 0; t < TMT; ++t)
-#pragma unroll
-                    for (int g = 0; g < 4; ++g)
-                        ac[t][c][g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[u][t][g], bf[g], ac[t][c][g], 0, 0, 0);
-            }
+        for (int r = 0; r < 4; ++r) {
+            const int m = r0 + 4 * q + r;
+            if (m < M && n < N) Y[(int64_t)m * ldy + n] = (float)acc[r] * scale;
         }
     }
-#pragma unroll
-    for (int t = 0; t < TMT; ++t)
-#pragma unroll
-        for (int c = 0; c < TNT; ++c)
-            red[wave][t * TNT + c][lane] = (ac[t][c][0] + 2 * ac[t][c][1] + 8 * ac[t][c][2] + 32 * ac[t][c][3]) >> 5;
-    __syncthreads();
-    if (wave >= TMT * TNT) return;  // wave = output tile (t, c): lane (n, q) holds rows 4 q .. 4 q + 3 of column n
-    v4i_t sum = red[0][wave][lane];
-#pragma unroll
-    for (int w2 = 1; w2 < NW; ++w2) sum += red[w2][wave][lane];
-    const int t = wave / TNT, c = wave % TNT;
-    const int n = n0 + 16 * c + l16;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int m = m0 + 16 * t + 4 * q + r;
-        if (m < M && n < N) Y[(int64_t)m * ldy + n] = (float)sum[r] * scale;
-    }
-}
-
-// Tile policy (same-box sweep on the down projection, tools/ab_gemm_sweep.sh, us per call at M = 2 /
-// 4 / 8 / 16 / 32 / 64 / 128): 16 x 16 tiles 4.4 / 4.8 / 5.5 / 6.8 (16 x 32: 5.3 / 5.8 / 6.9 / 8.9);
-// 32 x 16 at M = 32 10.8 (32 x 32: 13.0); 32 x 32 at M = 64 / 128 12.7 / 23.7 (32 x 16: 19.8 / --;
-// the 128 x 64 LDS-DMA tiles: 42.4 / 44.0) -- about 160 blocks for the 2560-row projection.
-static int launch_gemm_small_mfma(const uint8_t* w, const int8_t* a, int64_t lda, float scale, int M, int N, int K,
-                                  float* y, int64_t ldy, hipStream_t st) {
-#define WF_GS(TMTV, TNTV, PREV)                                                                                          \
-    hipLaunchKernelGGL((k_gemm_small_mfma<TMTV, TNTV, PREV>), dim3((N + 16 * TNTV - 1) / (16 * TNTV), (M + 16 * TMTV - 1) / (16 * TMTV)), \
-                       dim3(512), 0, st, w, a, lda, scale, M, N, K, y, ldy)
-    if (M <= 16) WF_GS(1, 1, 4);
-    else if (M <= 32) WF_GS(2, 1, 4);
-    else WF_GS(2, 2, 2);
-#undef WF_GS
-    return check_launch("gemm_small_mfma");
-}
+};
 
 // kernels/native.py:27-65: signed LSB-layout dot. Simple, correctness-first (not on the hot path:
 // the reference's own fast path is sgl-kernel's blocked layout above).
@@ -556,8 +460,8 @@ int wf_bitnet_gemm_ex(int fmt, const uint8_t* w, const int8_t* a, int64_t lda, f
 #ifndef WF_GEMM_SMALL  // study: 0 = M 2..64 on the VALU stream / 128 x 64 LDS-DMA tiles as before
 #define WF_GEMM_SMALL 1
 #endif
-    if (WF_GEMM_SMALL && fmt == WF_FMT_I2S && M >= 2 && M <= kSmallMaxM && K >= 16)
-        return launch_gemm_small_mfma(w, a, lda, scale, M, N, K, y, ldy, st);
+    if (WF_GEMM_SMALL && fmt == WF_FMT_I2S && gemm_small_ok(M, N) && K >= 16)
+        return launch_gemm_small_mfma(w, a, lda, M, N, K, EpiRawSmall{y, ldy, scale, M, N}, st), check_launch("gemm_small_mfma");
     if (fmt == WF_FMT_I2S && M >= kMfmaMinM) return launch_tgemm_mfma(w, a, lda, scale, M, N, K, y, ldy, st);
     if (fmt == WF_FMT_I2S) return launch_ternary_gemm<FmtI2S>(w, a, lda, scale, M, N, K, y, ldy, st);
     if (fmt == WF_FMT_TQ) return launch_ternary_gemm<FmtTQ>(w, a, lda, scale, M, N, K, y, ldy, st);
