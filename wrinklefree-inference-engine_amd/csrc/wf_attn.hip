@@ -795,12 +795,30 @@ __device__ __forceinline__ uint4 fp8x8_to_bf16(uint2 r) {
 // static per-layer scale): a fragment is 8 signed codes (8 bytes per lane), widened exactly -- each
 // byte biased to unsigned (xor 0x80), v_cvt_f32_ubyteN, -128 (packed), then bf16 (|code| <= 127 is
 // exact in bf16). Scales folded like FP8's.
+#ifndef WF_I8_PK  // 0: the round-5 form (hipcc folds the -128 into an integer subtract: SDWA + v_cvt_f32_i32)
+#define WF_I8_PK 1
+#endif
 __device__ __forceinline__ uint32_t i8x2_to_bf16(uint32_t u, int sh) {
     const float lo = (float)((u >> sh) & 0xffu) - 128.0f, hi = (float)((u >> (sh + 8)) & 0xffu) - 128.0f;
     return pk_bf16(lo, hi);
 }
+// four biased bytes -> floats (v_cvt_f32_ubyte0..3), -128 on pairs (v_pk_add_f32), packed to bf16
+__device__ __forceinline__ uint2 i8x4_to_bf16_pk(uint32_t x) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 a = {(float)(x & 0xffu), (float)((x >> 8) & 0xffu)};
+    f2 b = {(float)((x >> 16) & 0xffu), (float)(x >> 24)};
+    asm volatile("" : "+v"(a), "+v"(b));  // keep the conversions unsigned-byte (no integer -128 fold)
+    const f2 m = {-128.f, -128.f};
+    a += m;
+    b += m;
+    return make_uint2(pk_bf16(a.x, a.y), pk_bf16(b.x, b.y));
+}
 __device__ __forceinline__ uint4 i8x8_to_bf16(uint2 r) {
     const uint32_t x = r.x ^ 0x80808080u, y = r.y ^ 0x80808080u;
+    if constexpr (WF_I8_PK) {
+        const uint2 lo = i8x4_to_bf16_pk(x), hi = i8x4_to_bf16_pk(y);
+        return make_uint4(lo.x, lo.y, hi.x, hi.y);
+    }
     return make_uint4(i8x2_to_bf16(x, 0), i8x2_to_bf16(x, 16), i8x2_to_bf16(y, 0), i8x2_to_bf16(y, 16));
 }
 // KVQ: K/V cache element type -- 0 bf16, 1 OCP e4m3fn, 2 int8 (include/wf_bitnet.h WF_KV_*)
