@@ -345,17 +345,34 @@ __device__ __forceinline__ void decode_i2s(const uint4 w, uint32_t (&e)[4][4]) {
 // each 16-bit lane (3*255 < 768 -> {0,1,2}), the low byte is the next q.
 __device__ __forceinline__ void decode_tq(const uint4 w, uint32_t (&e)[5][4]) {
     const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#ifndef WF_TQ_PERM  // study: 0 = the shift / mask / and-or digit pick on 32-bit lanes (37 VALU per word)
+#define WF_TQ_PERM 2  // 1 = v_perm digit pick (25); 2 = + E and O multiplied as one 64-bit pair (20)
+#endif
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         uint32_t E = d[t] & 0x00ff00ffu;
         uint32_t O = (d[t] >> 8) & 0x00ff00ffu;
+        if constexpr (WF_TQ_PERM == 2) {
+            // {E, O} as one 64-bit value: 3 x every 16-bit lane in one v_lshl_add_u64 (lanes <= 765: no
+            // carry crosses a lane), the digit bytes {YE.b1, YO.b1, YE.b3, YO.b3} in one v_perm_b32
+            uint64_t eo = ((uint64_t)O << 32) | E;
 #pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const uint32_t YE = (E << 1) + E;  // v_lshl_add_u32
-            const uint32_t YO = (O << 1) + O;
-            e[i][t] = ((YE >> 8) & 0x00ff00ffu) | (YO & 0xff00ff00u);
-            E = YE & 0x00ff00ffu;
-            O = YO & 0x00ff00ffu;
+            for (int i = 0; i < 5; ++i) {
+                uint64_t y;
+                asm("v_lshl_add_u64 %0, %1, 1, %1" : "=v"(y) : "v"(eo));
+                e[i][t] = __builtin_amdgcn_perm((uint32_t)(y >> 32), (uint32_t)y, 0x07030501u);
+                eo = y & 0x00ff00ff00ff00ffull;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                const uint32_t YE = (E << 1) + E;  // v_lshl_add_u32
+                const uint32_t YO = (O << 1) + O;
+                if constexpr (WF_TQ_PERM == 1) e[i][t] = __builtin_amdgcn_perm(YO, YE, 0x07030501u);
+                else e[i][t] = ((YE >> 8) & 0x00ff00ffu) | (YO & 0xff00ff00u);
+                E = YE & 0x00ff00ffu;
+                O = YO & 0x00ff00ffu;
+            }
         }
     }
 }
