@@ -169,10 +169,30 @@ __device__ __forceinline__ float corrected(int S, float ws, int asum, float sf) 
 // PPT > 0 (MB == 1): the block normalises + quantises its input row itself (wf_norm.h) while its
 // first weight chunks stream in; PPT = 8-element pieces per thread (padded K <= 2048 * PPT).
 // PPT == 0: the codes come from k_rownorm (batch > 1).
+// TQ dot on the int8 matrix cores (batch 1, kTqMf): a TQ chunk's digit i is sixteen CONSECUTIVE
+// codes (k = 80 c + 16 i + 0..15), i.e. one v_mfma_i32_16x16x64_i8 B fragment as decoded. The block's
+// rows are 16-row tiles (8 / tiles waves per tile split the row's 4-chunk groups); lane (n, q) loads
+// chunk 4 g + q of weight row n (16 rows x 64 contiguous bytes per instruction), decodes it and issues
+// MFMA (g, i) with A = x[80 (4 g + q) + 16 i, +16) in every A row (plain LDS image; every output row
+// is the weight row's dot). The five v_dot4 per decoded word leave the VALU.
+// WF_TQ_MFMA: 0 off, 1 QKV / O / gate|up, 2 every batch-1 op. WF_TQ_CONTIG: a wave takes consecutive
+// 4-chunk groups of its rows (1) instead of every kWpt-th (0).
+#ifndef WF_TQ_MFMA
+#define WF_TQ_MFMA 1
+#endif
+#ifndef WF_TQ_CONTIG
+#define WF_TQ_CONTIG 0
+#endif
+template <int MODE>
+constexpr int tq_mf_pre() { return MODE == MODE_GU ? 4 : (MODE == MODE_DN ? 3 : 1); }
+typedef int v4i_tq __attribute__((ext_vector_type(4)));
 template <class F, int MODE, int LPR, int MB, int PPT>
 __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
     static_assert(PPT == 0 || MB == 1, "the norm prologue handles one activation row");
     constexpr int RPB = kNT / LPR;
+    constexpr bool kTqMf = (WF_TQ_MFMA == 2 || (WF_TQ_MFMA == 1 && MODE != MODE_DN)) && MB == 1 && PPT > 0 && MODE != MODE_LINEAR && __is_same(F, FmtTQ);
+    constexpr int kTiles = RPB >= 16 ? RPB / 16 : 1, kWpt = (kNT / 64) / kTiles;
+    constexpr int kTqPre = tq_mf_pre<MODE>();
     // 16-byte weight chunks in flight per lane (K = 2560 TQ: 1 per lane at LPR 32, 4 at LPR 8;
     // K = 6912 at LPR 32: 3)
     constexpr int kPrefetch = LPR >= 32 ? 4 : (LPR == 16 ? 4 : 8);
@@ -216,10 +236,25 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
     // whose row loads queued behind the other waves' weights held the norm's first barrier
     if constexpr (PPT > 0 && kXFirst) __builtin_amdgcn_s_barrier();
     const uint8_t* wr = a.w + (int64_t)min(row, N - 1) * F::row_bytes(K);
-    uint4 wpre[kPrefetch];
+    uint4 wpre[kTqMf ? 1 : kPrefetch];
+    uint4 wq[kTqMf ? kTqPre : 1];
+    const int tq_wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), tq_l16 = threadIdx.x & 15,
+              tq_q = (threadIdx.x >> 4) & 3;
+    const int tq_part = tq_wave / kTiles, tq_G = (C + 3) >> 2;  // 4-chunk groups per row
+    const int tq_gpw = (tq_G + kWpt - 1) / kWpt;                  // groups per wave
+    // wave part's u-th group (may be >= tq_G or, contiguous, past the part's share: see tq_ok)
+    const auto tq_g = [&](int u) { return WF_TQ_CONTIG ? tq_part * tq_gpw + u : tq_part + kWpt * u; };
+    const auto tq_ok = [&](int u) { return tq_g(u) < tq_G && (!WF_TQ_CONTIG || u < tq_gpw); };
+    const uint8_t* wqr = a.w + (int64_t)min((int)blockIdx.x * RPB + 16 * (tq_wave % kTiles) + tq_l16, N - 1) * F::row_bytes(K);
+    if constexpr (kTqMf) {
 #pragma unroll
-    for (int u = 0; u < kPrefetch; ++u)  // clamped (no branch): lanes past the row re-read its last chunk
-        wpre[u] = ldg_nt(wr + (int64_t)min(LPR * u + sub, C - 1) * 16);
+        for (int u = 0; u < kTqPre; ++u)  // unconditional (clamped): vmcnt stays exact
+            wq[u] = ldg_nt(wqr + 16 * (int64_t)min(4 * min(tq_g(u), tq_G - 1) + tq_q, C - 1));
+    } else {
+#pragma unroll
+        for (int u = 0; u < kPrefetch; ++u)  // clamped (no branch): lanes past the row re-read its last chunk
+            wpre[u] = ldg_nt(wr + (int64_t)min(LPR * u + sub, C - 1) * 16);
+    }
     // residual: unconditional (clamped) load -- a load under a lane condition makes hipcc wait
     // vmcnt(0) right there, i.e. for the whole weight prefetch before the prologue can start
     uint16_t resid_raw[MB];
@@ -256,7 +291,7 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
         } else {
             sf[0] = norm_row<kNormPPT, kNT, 512u * MODE>(nr, K, a.eps, y, red);
         }
-        const auto lds_at = [](int p) { return F::lds_off(8 * p); };
+        const auto lds_at = [](int p) { return kTqMf ? 8 * p : F::lds_off(8 * p); };  // kTqMf: codes in k order
         int as = quant_row<PPT, kNT, decltype(lds_at), 512u * MODE>(y, sf[0], F::k_pad(K) / 8, smem, lds_at);
         as = wave_sum_i(as);
         if ((threadIdx.x & 63) == 0) red_i[threadIdx.x >> 6] = as;
@@ -283,6 +318,35 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
     WF_STAMP(1);
     WF_STAMP_DRAIN(13);
 
+    int acc[MB];
+    if constexpr (kTqMf) {
+        __shared__ int tq_red[kNT / 64][16];
+        v4i_tq ac = v4i_tq{0, 0, 0, 0};
+        const int limg = lds_image_bytes<F>(K) - 16;
+        auto tq_group = [&](uint4 w, int g) __attribute__((always_inline)) {
+            const int c = 4 * g + tq_q;
+            Decoded<F> d;
+            d.load(c < C ? w : make_uint4(0, 0, 0, 0));
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                const v4i_tq bf = v4i_tq{(int)d.e[i][0], (int)d.e[i][1], (int)d.e[i][2], (int)d.e[i][3]};
+                const v4i_tq af = *reinterpret_cast<const v4i_tq*>(smem + min(80 * c + 16 * i, limg));
+                ac = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf, ac, 0, 0, 0);
+            }
+        };
+#pragma unroll
+        for (int u = 0; u < kTqPre; ++u)
+            if (tq_ok(u)) tq_group(wq[u], tq_g(u));  // wave-uniform
+        for (int u = kTqPre; tq_ok(u); ++u)  // rows longer than the prefetch
+            tq_group(ldg_nt(wqr + 16 * (int64_t)min(4 * tq_g(u) + tq_q, C - 1)), tq_g(u));
+        if (tq_q == 0) tq_red[tq_wave][tq_l16] = ac[0];
+        __syncthreads();
+        int sum = 0;
+#pragma unroll
+        for (int p = 0; p < kWpt; ++p) sum += tq_red[(lrow >> 4) + kTiles * p][lrow & 15];
+        acc[0] = sum;
+        WF_STAMP(2);
+    } else {
     DotAcc<F> dacc[MB];
 #pragma unroll
     for (int u = 0; u < kPrefetch; ++u) {
@@ -313,9 +377,9 @@ __global__ __launch_bounds__(kNT) void k_gemv(GemvArgs a) {
         }
     }
     WF_STAMP(2);
-    int acc[MB];
 #pragma unroll
     for (int m = 0; m < MB; ++m) acc[m] = group_reduce<LPR>(dacc[m].total(), OpAdd{});
+    }
 
     if constexpr (MODE == MODE_QKV) {
         // rows per head permuted: block t of head h = dims {8t..8t+7, 64+8t..64+8t+7} (RPB == 16)
